@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Groth16 proofs/sec on the ZK-FL training-step circuit (~2^18 constraints), 1..N MI355X.
+
+Workload (BASELINE.json metric): TrainingStepVerified(BATCH=128,
+DIM=4, DEPTH=7, PRECISION=1000) — the reference's sgd_verified.circom at the Report's N=128
+scale — with synthetic client inputs from the reference harness's seeded generator
+(tests/full_system_simulation.mjs:273-303, weights = 0, tau^2 = 1e8, round 1).
+A step = one full Groth16 proof (ABC, 3x coset NTT, 4 G1 + 1 G2 MSM, assembly) from a
+device-resident witness with the proving key resident in HBM; r, s from the OS CSPRNG.
+Multi-GPU: one process per GPU, independent proofs per rank (weak scaling, no collective on
+the data path); the barrier / max-over-ranks timing uses torch.distributed.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the roofline definitions).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd")
+sys.path.insert(0, PKG_DIR)
+
+METRIC = "Groth16 proofs/sec (training-step circuit, ~2^18 constraints) at 1/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# algorithmic bytes per accumulated (base, window) entry: 4 B sorted index + affine base
+BYTES_PER_ENTRY = {"msm_accumulate_g1": 4 + 64, "msm_accumulate_g2": 4 + 128}
+
+CIRCUITS = {
+    "M": ("sgd_verified", (128, 4, 7, 1000)),
+    "C2": ("sgd_verified", (8, 4, 3, 1000)),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline_leg(builder, inp, seconds_budget=20.0):
+    """Oracle ("port") on the host: the C restatement if built, else the Python one, timed on
+    a bounded sample of the same workload and scaled to proofs/s."""
+    sys.path.insert(0, ROOT)
+    try:
+        from oracle import cbaseline  # C oracle (built by oracle/Makefile)
+        return cbaseline.time_prove(builder, inp, seconds_budget)
+    except Exception as e:  # noqa: BLE001
+        log(f"[bench] C oracle unavailable ({e}); using the Python oracle sample")
+    from oracle import bn254 as bn
+    # sample: a 1024-point G1 MSM of the same kind as the proof's (random bases/scalars);
+    # one proof ~ (3*nVars + domain) G1 + nVars G2 (x3 cost) point-entries.
+    import random
+    rnd = random.Random(1)
+    pts = [bn.mul(bn.G1_GEN, rnd.randrange(bn.R)) for _ in range(256)] * 4
+    ss = [rnd.randrange(bn.R) for _ in range(1024)]
+    t0 = time.perf_counter()
+    bn.msm(pts, ss)
+    dt = time.perf_counter() - t0
+    n = 1 << max(1, (builder.n_constraints + builder.n_public).bit_length())
+    work = 3 * builder.n_wires + n + 3 * builder.n_wires
+    per_proof = dt * work / 1024
+    return {"value": 1.0 / per_proof, "unit": "proofs/s", "cores": 1, "kind": "port",
+            "sample": f"python oracle Pippenger G1 MSM of 1024 points ({dt:.2f} s), scaled by "
+                      f"{work} G1-equivalent MSM points per proof (MSMs only; NTT/ABC excluded)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+
+    from zkfl import circuits, clients, native, zkey
+
+    name, params = CIRCUITS[args.circuit]
+    t0 = time.perf_counter()
+    b = circuits.build(name, *params)
+    batch, dim, depth, precision = params
+    client = clients.Client(rank + 1, batch, dim, depth, clients.JsLcg(12345))
+    inp, _ = client.training_input(batch, precision, 100000000)
+    w = b.witness(inp)
+    log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires "
+        f"({time.perf_counter() - t0:.1f} s)")
+
+    ctx = native.Context(local_rank)
+    t0 = time.perf_counter()
+    zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
+    log(f"[bench r{rank}] dev setup {len(zk) / 1e6:.0f} MB zkey ({time.perf_counter() - t0:.1f} s)")
+    t0 = time.perf_counter()
+    key = native.ProvingKey(ctx, zk)
+    wt = zkey.wtns_bytes(w)
+    res = key.upload(wt)
+    log(f"[bench r{rank}] key load + witness upload ({time.perf_counter() - t0:.1f} s), domain {key.domain_size}")
+
+    def barrier_sync():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        key.prove_resident(res)
+    ctx.profile_reset()
+    ctx.set_profiling(True)
+    barrier_sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        key.prove_resident(res)
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    ctx.set_profiling(False)
+
+    prof = {k: ctx.profile(k) for k in ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")}
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = world * args.steps / elapsed
+        # roofline for the dominant instrumented kernel
+        cand = {k: v for k, v in prof.items() if k in BYTES_PER_ENTRY and v[1] > 0}
+        dom = max(cand, key=lambda k: cand[k][0])
+        ms_tot, launches, units = prof[dom]
+        avg_s = ms_tot / launches / 1e3
+        bytes_per_launch = units / launches * BYTES_PER_ENTRY[dom]
+        achieved = bytes_per_launch / avg_s / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
+                    "entries_per_launch": round(units / launches)}
+        stage_ms = {k: round(v[0] / max(1, args.steps), 3) for k, v in prof.items()}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline_leg(b, inp)
+            except Exception as e:  # noqa: BLE001
+                log(f"[bench] cpu baseline failed: {e}")
+        out = {
+            "metric": METRIC, "value": round(value, 4), "unit": "proofs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (reference harness seeded client generator)",
+            "config": {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
+                       "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
+                       "global_batch": world, "parallelism": f"replicas{world}"},
+            "roofline": roofline, "stage_ms_per_proof": stage_ms, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    res.close()
+    key.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * zkfl.h — C ABI of the MI355X-native Groth16/BN254 prover (libzkfl.so).
+ *
+ * Drop-in boundary for the reference's proving path.  The reference never links a prover:
+ * it shells out to snarkjs [ext].  Each entry point below replaces one
+ * snarkjs operation that a host binding (N-API / ctypes) calls:
+ *
+ *   zkfl_zkey_load            <- snarkjs reads `<c>_final.zkey` in `groth16 prove`
+ *                                (tests/full_system_simulation.mjs:773-776)
+ *   zkfl_groth16_prove        <- `npx snarkjs groth16 prove <zkey> <wtns> <proof> <public>`
+ *                                (tests/full_system_simulation.mjs:773-776,
+ *                                 tests/quick_integration_test.mjs:426-429,
+ *                                 tests/test_verified_gradient.mjs:480-483)
+ *   zkfl_groth16_prove_batch  <- the sequential per-client loop
+ *                                (tests/full_system_simulation.mjs:1298-1343)
+ *   zkfl_setup_*              <- the bulk fixed-base work of `snarkjs groth16 setup` +
+ *                                `zkey contribute` (tests/full_system_simulation.mjs:713-730)
+ *   zkfl_msm_*, zkfl_ntt_*    <- ffjavascript multiExpAffine / fft as used inside
+ *                                groth16 prove (exported for parity tests)
+ *
+ * Conventions (snarkjs/ffjavascript byte conventions):
+ *   - Field elements are 32-byte little-endian.  "std" = standard form, "mont" = Montgomery
+ *     form (x * 2^256 mod p), as stored in zkey sections 2-9.
+ *   - Affine points: G1 = x||y (64 B), G2 = x.c0||x.c1||y.c0||y.c1 (128 B); the point at
+ *     infinity is all-zero bytes.
+ *   - Proof buffer (256 B): pi_a (G1) || pi_b (G2) || pi_c (G1), affine, std form — exactly
+ *     the numbers snarkjs prints in proof.json (pi_a[0..1], pi_b[0..1][0..1], pi_c[0..1]).
+ *   - Blinding: rs = 64 bytes (r || s, std form, < r) for deterministic parity mode, or NULL
+ *     to draw r, s from the OS CSPRNG (snarkjs draws them with Fr.random()).
+ * All functions return 0 on success and a negative ZKFL_E_* code on failure; the message is
+ * in zkfl_last_error() (thread-local).  A context is bound to one device and one stream;
+ * contexts are independent (multi-GPU = one context per device, one process per GPU).
+ */
+#ifndef ZKFL_H
+#define ZKFL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZKFL_OK 0
+#define ZKFL_E_ARG -1        /* bad argument / null pointer */
+#define ZKFL_E_FORMAT -2     /* malformed zkey / wtns / r1cs bytes */
+#define ZKFL_E_PRIME -3      /* file prime is not BN254 r / q */
+#define ZKFL_E_MISMATCH -4   /* nWitness != nVars, wrong section sizes */
+#define ZKFL_E_DEVICE -5     /* HIP runtime error / no GPU */
+#define ZKFL_E_OOM -6        /* device allocation failed */
+#define ZKFL_E_CONSTRAINT -7 /* witness does not satisfy the circuit */
+
+typedef struct zkfl_ctx zkfl_ctx;
+typedef struct zkfl_key zkfl_key;
+typedef struct zkfl_witness zkfl_witness;
+
+int zkfl_version(void);
+const char* zkfl_last_error(void);
+int zkfl_device_count(int* count);
+
+int zkfl_ctx_create(int device, zkfl_ctx** out);
+int zkfl_ctx_destroy(zkfl_ctx* ctx);
+/* Per-kernel timing with HIP events on the context's stream (used by bench.py roofline). */
+int zkfl_ctx_set_profiling(zkfl_ctx* ctx, int enabled);
+/* name: "msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove".  Synchronises. */
+int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units);
+int zkfl_ctx_profile_reset(zkfl_ctx* ctx);
+int zkfl_ctx_synchronize(zkfl_ctx* ctx);
+
+/* Parse a snarkjs groth16 .zkey and make it device-resident (bases expanded per window).
+ * The caller keeps ownership of buf. */
+int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out);
+int zkfl_key_free(zkfl_key* key);
+int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
+
+/* Full prove from a .wtns byte image (host).  pub_out may be NULL; otherwise receives
+ * n_public x 32 B std-form public signals (witness[1..n_public]) and *npub their count. */
+int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len,
+                       const uint8_t* rs, uint8_t proof_out[256], uint8_t* pub_out, size_t* npub);
+
+/* Device-resident witnesses (steady-state proving: input already in HBM). */
+int zkfl_witness_upload(zkfl_ctx* ctx, const zkfl_key* key, const uint8_t* wtns, size_t wtns_len,
+                        zkfl_witness** out);
+int zkfl_witness_free(zkfl_witness* w);
+int zkfl_groth16_prove_resident(zkfl_ctx* ctx, zkfl_key* key, const zkfl_witness* w, const uint8_t* rs,
+                                uint8_t proof_out[256]);
+/* n independent proofs (rs: n x 64 B or NULL); proofs_out: n x 256 B. */
+int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
+                             const uint8_t* rs, uint8_t* proofs_out);
+
+/* Parity hooks: the deterministic core of one proof.
+ * h_out: domain_size x 32 B std (coset evaluations a*b-c, the H-MSM scalars) or NULL;
+ * msm_out: A (64) | B1 (64) | B2 (128) | C (64) | H (64) std affine MSM results over the
+ * zkey queries *without* the alpha/beta/delta/r/s terms, or NULL. */
+int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, uint8_t* h_out,
+                           uint8_t* msm_out);
+
+/* Stand-alone primitives (parity tests).  bases: mont affine; scalars: std, n x 32 B. */
+int zkfl_msm_g1(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[64]);
+int zkfl_msm_g2(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[128]);
+/* In place: 2^logn std-form evaluations on the domain -> evaluations on the odd coset
+ * (snarkjs ifft + batchApplyKey(inc) + fft). */
+int zkfl_ntt_coset(zkfl_ctx* ctx, uint8_t* data, uint32_t logn);
+
+/* Dev-ceremony fixed-base multiplications: out[i] = scalars[i] * generator, mont affine. */
+int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
+int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKFL_H */

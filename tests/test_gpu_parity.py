@@ -1,0 +1,287 @@
+"""HIP path (through the C ABI) vs the CPU oracle — run on an MI355X (-m gpu).
+
+Bar: bit-exact.  Small sizes compare against the oracle directly; larger sizes use
+size-independent identities (MSM over k_i*G equals (sum s_i k_i)*G; the coset NTT is linear
+and matches the oracle on a basis) plus pairing verification of every proof.
+"""
+import json
+import os
+import random
+
+import pytest
+
+from oracle import bn254 as bn
+from oracle import groth16 as og
+
+pytestmark = pytest.mark.gpu
+
+R = bn.R
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _le(x):
+    return int(x).to_bytes(32, "little")
+
+
+def _scal(vals):
+    return b"".join(_le(v) for v in vals)
+
+
+def _g1_std(b):
+    return bn.g1_from_bytes_std(b)
+
+
+def _g2_std(b):
+    return bn.g2_from_bytes_std(b)
+
+
+# ---------------------------------------------------------------------------
+# fixed-base (dev ceremony) multiplications
+# ---------------------------------------------------------------------------
+def test_gen_mul_g1_g2_match_oracle(gpu_ctx):
+    rnd = random.Random(7)
+    ks = [0, 1, 2, R - 1, rnd.randrange(R), rnd.randrange(R), 1 << 200, 12345]
+    g1 = gpu_ctx.g1_gen_mul(_scal(ks))
+    g2 = gpu_ctx.g2_gen_mul(_scal(ks))
+    for i, k in enumerate(ks):
+        assert bn.g1_from_bytes_mont(g1[64 * i:64 * i + 64]) == bn.mul(bn.G1_GEN, k)
+        assert bn.g2_from_bytes_mont(g2[128 * i:128 * i + 128]) == bn.mul(bn.G2_GEN, k)
+
+
+# ---------------------------------------------------------------------------
+# NTT (odd-coset shift of snarkjs groth16_prove)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("logn", [1, 2, 5, 10, 11, 13])
+def test_ntt_coset_matches_oracle(gpu_ctx, logn):
+    rnd = random.Random(logn)
+    a = [rnd.randrange(R) for _ in range(1 << logn)]
+    out = gpu_ctx.ntt_coset(_scal(a))
+    got = [int.from_bytes(out[32 * i:32 * i + 32], "little") for i in range(1 << logn)]
+    assert got == og.coset_evals(a)
+
+
+def test_ntt_coset_large_linearity(gpu_ctx):
+    """2^18 (metric domain): coset(e_k) known in closed form: inc^k * w^(i k) / ... checked via
+    linearity: coset(a + b) == coset(a) + coset(b) and one sampled output vs direct sum."""
+    logn = 18
+    n = 1 << logn
+    rnd = random.Random(5)
+    a = [rnd.randrange(R) for _ in range(n)]
+    b = [rnd.randrange(R) for _ in range(n)]
+    ca = gpu_ctx.ntt_coset(_scal(a))
+    cb = gpu_ctx.ntt_coset(_scal(b))
+    cab = gpu_ctx.ntt_coset(_scal([(x + y) % R for x, y in zip(a, b)]))
+    for i in rnd.sample(range(n), 64):
+        x = int.from_bytes(ca[32 * i:32 * i + 32], "little")
+        y = int.from_bytes(cb[32 * i:32 * i + 32], "little")
+        z = int.from_bytes(cab[32 * i:32 * i + 32], "little")
+        assert (x + y) % R == z
+    # delta input e_0: ifft -> all coefficients 1/n, so at coset point x_i = g w^i the value is
+    # (1/n)(x_i^n - 1)/(x_i - 1) = (-2/n)/(g w^i - 1)  (g = w_2n, g^n = -1)
+    e0 = [1] + [0] * (n - 1)
+    c0 = gpu_ctx.ntt_coset(_scal(e0))
+    ninv = pow(n, R - 2, R)
+    g, w = bn.FR_W[logn + 1], bn.FR_W[logn]
+    for i in range(0, n, 4099):
+        want = (R - 2) * ninv % R * pow((g * pow(w, i, R) - 1) % R, R - 2, R) % R
+        assert int.from_bytes(c0[32 * i:32 * i + 32], "little") == want
+
+
+# ---------------------------------------------------------------------------
+# MSM
+# ---------------------------------------------------------------------------
+def _bases_g1(ctx, ks):
+    return ctx.g1_gen_mul(_scal(ks))
+
+
+def _bases_g2(ctx, ks):
+    return ctx.g2_gen_mul(_scal(ks))
+
+
+def _expect(ks, ss):
+    return sum(k * s for k, s in zip(ks, ss)) % R
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 1000, 70000])
+def test_msm_g1_identity(gpu_ctx, n):
+    rnd = random.Random(n)
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [rnd.randrange(R) for _ in range(n)]
+    out = gpu_ctx.msm_g1(_bases_g1(gpu_ctx, ks), _scal(ss))
+    assert _g1_std(out) == bn.mul(bn.G1_GEN, _expect(ks, ss))
+
+
+def test_msm_g1_matches_oracle_pippenger(gpu_ctx):
+    rnd = random.Random(11)
+    pts = [bn.mul(bn.G1_GEN, rnd.randrange(R)) for _ in range(40)]
+    ss = [rnd.randrange(R) for _ in range(40)]
+    bases = b"".join(bn.g1_to_bytes_mont(p) for p in pts)
+    assert _g1_std(gpu_ctx.msm_g1(bases, _scal(ss))) == bn.msm(pts, ss)
+
+
+@pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max"])
+def test_msm_g1_edge_cases(gpu_ctx, case):
+    rnd = random.Random(hash(case) & 0xFFFF)
+    n = 3000
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [rnd.randrange(R) for _ in range(n)]
+    if case == "zeros":
+        ss = [0] * n
+    elif case == "ones":          # every entry in bucket 0: skewed accumulation
+        ss = [1] * n
+    elif case == "small":         # witness-like bits / small ints
+        ss = [rnd.choice([0, 1, 2, 3, 100, 65535, 65536, 1 << 15, (1 << 15) + 1]) for _ in range(n)]
+    elif case == "neg":           # digits near the signed boundary
+        ss = [(R - rnd.randrange(1, 1 << 20)) for _ in range(n)]
+    elif case == "dup":           # same base repeated: P + P inside a bucket
+        ks = [ks[0]] * n
+        ss = [ss[0]] * n
+    elif case == "cancel":        # P and -P with equal scalars
+        ks = [ks[i // 2] if i % 2 == 0 else R - ks[i // 2] for i in range(n)]
+        ss = [ss[i // 2] for i in range(n)]
+    elif case == "max":
+        ss = [R - 1] * n
+    bases = bytearray(_bases_g1(gpu_ctx, ks))
+    if case == "inf_base":
+        for i in range(0, n, 3):
+            bases[64 * i:64 * i + 64] = bytes(64)
+            ks[i] = 0
+    out = gpu_ctx.msm_g1(bytes(bases), _scal(ss))
+    want = _expect(ks, ss)
+    assert _g1_std(out) == (bn.mul(bn.G1_GEN, want) if want else None)
+
+
+@pytest.mark.parametrize("n", [1, 5, 500, 20000])
+def test_msm_g2_identity(gpu_ctx, n):
+    rnd = random.Random(100 + n)
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [rnd.randrange(R) for _ in range(n)]
+    out = gpu_ctx.msm_g2(_bases_g2(gpu_ctx, ks), _scal(ss))
+    assert _g2_std(out) == bn.mul(bn.G2_GEN, _expect(ks, ss))
+
+
+def test_msm_g2_small_scalars(gpu_ctx):
+    rnd = random.Random(3)
+    n = 2000
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [rnd.choice([0, 1, 2, 7, 1 << 16]) for _ in range(n)]
+    out = gpu_ctx.msm_g2(_bases_g2(gpu_ctx, ks), _scal(ss))
+    want = _expect(ks, ss)
+    assert _g2_std(out) == bn.mul(bn.G2_GEN, want)
+
+
+# ---------------------------------------------------------------------------
+# Full Groth16 proofs
+# ---------------------------------------------------------------------------
+def _setup(gpu_ctx, name, *params, toxic=None):
+    from zkfl import circuits, zkey
+    b = circuits.build(name, *params)
+    tx = toxic or zkey.Toxic(tau=31337, alpha=5, beta=6, gamma=7, delta=8)
+    return b, zkey.groth16_setup(b, gpu_ctx, tx)
+
+
+RS = _le(0x1234567) + _le(0x7654321)
+
+
+def test_gpu_setup_zkey_identical_to_oracle_backend(gpu_ctx):
+    from oracle_backend import OraclePoints
+    from zkfl import circuits, zkey
+    b = circuits.build("poseidon_hash2")
+    tx = zkey.Toxic(tau=987654321, alpha=111, beta=222, gamma=333, delta=444)
+    assert zkey.groth16_setup(b, gpu_ctx, tx) == zkey.groth16_setup(b, OraclePoints(), tx)
+
+
+def test_proof_poseidon_hash2_bit_exact(gpu_ctx):
+    from zkfl import native, zkey
+    b, zk = _setup(gpu_ctx, "poseidon_hash2")
+    w = b.witness({"left": 1, "right": 2})
+    key = native.ProvingKey(gpu_ctx, zk)
+    proof, pub = key.prove(zkey.wtns_bytes(w), RS)
+    z = og.parse_zkey(zk)
+    ref = og.prove(z, w, r=0x1234567, s=0x7654321)
+    assert proof == og.proof_bytes(ref)
+    assert pub == [7853200120776062878684798364095072458815029376092732009249414926327459813530]
+    assert og.verify(z, ref["public"], ref["pi_a"], ref["pi_b"], ref["pi_c"])
+    # deterministic core: h and the five plain MSMs
+    hs, parts = key.debug_parts(zkey.wtns_bytes(w))
+    assert hs == ref["h"]
+    assert _g1_std(parts["A"]) == ref["msm"]["A"]
+    assert _g1_std(parts["B1"]) == ref["msm"]["B1"]
+    assert _g2_std(parts["B2"]) == ref["msm"]["B2"]
+    assert _g1_std(parts["C"]) == ref["msm"]["C"]
+    assert _g1_std(parts["H"]) == ref["msm"]["H"]
+    key.close()
+
+
+def _verify_bytes(z, proof, pub):
+    pa = bn.g1_from_bytes_std(proof[0:64])
+    pb = bn.g2_from_bytes_std(proof[64:192])
+    pc = bn.g1_from_bytes_std(proof[192:256])
+    return og.verify(z, pub, pa, pb, pc)
+
+
+def test_proof_sgd_verified_reference_instance(gpu_ctx):
+    """sgd_verified(8,4,3,1000) with the harness's client-1 inputs: bit-exact vs oracle."""
+    from zkfl import clients, native, zkey
+    b, zk = _setup(gpu_ctx, "sgd_verified", 8, 4, 3, 1000)
+    c = clients.Client(1, 8, 4, 3, clients.JsLcg(12345))
+    inp, _ = c.training_input(8, 1000, 100000000)
+    w = b.witness(inp)
+    key = native.ProvingKey(gpu_ctx, zk)
+    proof, pub = key.prove(zkey.wtns_bytes(w), RS)
+    z = og.parse_zkey(zk)
+    ref = og.prove(z, w, r=0x1234567, s=0x7654321)
+    assert proof == og.proof_bytes(ref)
+    assert [str(x) for x in pub] == [inp[k] for k in ("client_id", "round", "root_D", "root_G", "root_W", "tauSquared")]
+    # random blinding (CSPRNG): still verifies; two proofs differ
+    p1, _ = key.prove(zkey.wtns_bytes(w))
+    p2, _ = key.prove(zkey.wtns_bytes(w))
+    assert p1 != p2
+    assert _verify_bytes(z, p1, pub) and _verify_bytes(z, p2, pub)
+    # tampered public signal does not verify
+    assert not _verify_bytes(z, p1, [pub[0] + 1] + pub[1:])
+    key.close()
+
+
+def test_fixture_v5_proof_verifies(gpu_ctx):
+    """The reference fixture data/test_input_v5.json through TrainingStepV5(8,16,7)."""
+    from zkfl import native, zkey
+    d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
+    b, zk = _setup(gpu_ctx, "sgd_step_v5", 8, 16, 7)
+    key = native.ProvingKey(gpu_ctx, zk)
+    proof, pub = key.prove(zkey.wtns_bytes(b.witness(d)))
+    assert [str(x) for x in pub] == [d["client_id"], d["round"], d["root_D"], d["root_G"], d["tauSquared"]]
+    assert _verify_bytes(og.parse_zkey(zk), proof, pub)
+    key.close()
+
+
+def test_resident_batch_and_errors(gpu_ctx):
+    from zkfl import clients, native, zkey
+    b, zk = _setup(gpu_ctx, "balance_unified", 8, 3, 4)
+    key = native.ProvingKey(gpu_ctx, zk)
+    wt = []
+    for cid in (1, 2, 3):
+        c = clients.Client(cid, 8, 4, 3, clients.JsLcg(12345 + cid))
+        wt.append(zkey.wtns_bytes(b.witness(c.balance_input())))
+    ws = [key.upload(x) for x in wt]
+    rs = b"".join(_le(11 + i) + _le(22 + i) for i in range(3))
+    batch = key.prove_batch(ws, rs)
+    for i in range(3):
+        assert batch[i] == key.prove_resident(ws[i], rs[64 * i:64 * i + 64])
+        assert batch[i] == key.prove(wt[i], rs[64 * i:64 * i + 64])[0]
+    z = og.parse_zkey(zk)
+    ref = og.prove(z, zkey.read_wtns(wt[0]), r=11, s=22)
+    assert batch[0] == og.proof_bytes(ref)
+    # wrong witness length -> ZKFL_E_MISMATCH; garbage zkey -> ZKFL_E_FORMAT; r >= r -> ZKFL_E_ARG
+    with pytest.raises(native.ZkflError) as e:
+        key.prove(zkey.wtns_bytes([1, 2, 3]))
+    assert e.value.code == -4
+    with pytest.raises(native.ZkflError) as e:
+        native.ProvingKey(gpu_ctx, b"zkey" + bytes(40))
+    assert e.value.code == -2
+    with pytest.raises(native.ZkflError) as e:
+        key.prove(wt[0], _le(R) + _le(1))
+    assert e.value.code == -1
+    for w in ws:
+        w.close()
+    key.close()

@@ -1,0 +1,292 @@
+// BN254 prime-field arithmetic for gfx950 (CDNA4), 8 x 32-bit limbs, Montgomery R = 2^256.
+//
+// Replaces the ffjavascript/wasmcurves Fq/Fr kernels (reference dependency ffjavascript
+// ^0.2.63, package.json:44; used by `snarkjs groth16 prove`, tests/full_system_simulation.mjs:773).
+// Representation: little-endian 32-bit limbs, values kept fully reduced (< p) between
+// operations.  Montgomery multiplication is CIOS with v_mad_u64_u32 (32x32+64 -> 64) carry
+// chains; both moduli are 254-bit so the 9-limb accumulator never overflows.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zkfl {
+
+#define ZK_DEV __device__ __forceinline__
+
+struct FqP {  // base field q
+  static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                      0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr uint32_t INV = 0xe4866389u;  // -q^-1 mod 2^32
+};
+
+struct FrP {  // scalar field r
+  static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                      0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr uint32_t INV = 0xefffffffu;  // -r^-1 mod 2^32
+};
+
+template <class PR>
+struct Fp {
+  uint32_t v[8];
+};
+
+using Fq = Fp<FqP>;
+using Fr = Fp<FrP>;
+
+template <class PR>
+ZK_DEV Fp<PR> fp_zero() {
+  Fp<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = 0;
+  return r;
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_one() {  // Montgomery one
+  Fp<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = PR::ONE[i];
+  return r;
+}
+
+template <class PR>
+ZK_DEV bool fp_is_zero(const Fp<PR>& a) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x |= a.v[i];
+  return x == 0;
+}
+
+template <class PR>
+ZK_DEV bool fp_eq(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x |= a.v[i] ^ b.v[i];
+  return x == 0;
+}
+
+// r = a - p if a >= p else a   (a < 2p)
+template <class PR>
+ZK_DEV void fp_reduce_once(uint32_t r[8], const uint32_t a[8]) {
+  uint32_t t[8];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a[i] - PR::P[i] - borrow;
+    t[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = borrow ? a[i] : t[i];
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_add(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t s[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    s[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, s);
+  return r;
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_sub(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t d[8];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
+    d[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  // if borrow, add p back
+  uint32_t mask = 0u - borrow;
+  uint64_t c = 0;
+  Fp<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)d[i] + (PR::P[i] & mask);
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return r;
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_neg(const Fp<PR>& a) {
+  return fp_sub<PR>(fp_zero<PR>(), a);
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_dbl(const Fp<PR>& a) {
+  return fp_add<PR>(a, a);
+}
+
+// Montgomery multiplication, CIOS.  a, b < p  ->  a*b*2^-256 mod p, < p.
+template <class PR>
+ZK_DEV Fp<PR> fp_mul(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t t[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+    const uint32_t bi = b.v[i];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c = (uint64_t)a.v[j] * bi + t[j] + c;
+      t[j] = (uint32_t)c;
+      c >>= 32;
+    }
+    uint32_t t8 = t[8] + (uint32_t)c;  // < 2^32 (accumulator < 2^287)
+    const uint32_t m = t[0] * PR::INV;
+    c = ((uint64_t)m * PR::P[0] + t[0]) >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      c = (uint64_t)m * PR::P[j] + t[j] + c;
+      t[j - 1] = (uint32_t)c;
+      c >>= 32;
+    }
+    c += t8;
+    t[7] = (uint32_t)c;
+    t[8] = (uint32_t)(c >> 32);
+  }
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, t);
+  return r;
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_sqr(const Fp<PR>& a) {
+  return fp_mul<PR>(a, a);
+}
+
+// Standard <-> Montgomery
+template <class PR>
+ZK_DEV Fp<PR> fp_to_mont(const Fp<PR>& a) {
+  Fp<PR> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = PR::R2[i];
+  return fp_mul<PR>(a, r2);
+}
+
+template <class PR>
+ZK_DEV Fp<PR> fp_from_mont(const Fp<PR>& a) {
+  Fp<PR> one;
+  one.v[0] = 1;
+#pragma unroll
+  for (int i = 1; i < 8; i++) one.v[i] = 0;
+  return fp_mul<PR>(a, one);
+}
+
+// a^e for a public exponent given as 8 little-endian limbs (left-to-right binary).
+template <class PR>
+ZK_DEV Fp<PR> fp_pow(const Fp<PR>& a, const uint32_t e[8]) {
+  Fp<PR> r = fp_one<PR>();
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      r = fp_sqr<PR>(r);
+      if ((e[i] >> b) & 1u) r = fp_mul<PR>(r, a);
+    }
+  }
+  return r;
+}
+
+// Inverse by Fermat (p - 2).  inv(0) = 0.
+template <class PR>
+ZK_DEV Fp<PR> fp_inv(const Fp<PR>& a) {
+  uint32_t e[8];
+  uint32_t borrow = 2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)PR::P[i] - borrow;
+    e[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return fp_pow<PR>(a, e);
+}
+
+// ---------------------------------------------------------------------------
+// Fq2 = Fq[u] / (u^2 + 1)
+// ---------------------------------------------------------------------------
+struct Fq2 {
+  Fq c0, c1;
+};
+
+ZK_DEV Fq2 f2_zero() { return {fp_zero<FqP>(), fp_zero<FqP>()}; }
+ZK_DEV Fq2 f2_one() { return {fp_one<FqP>(), fp_zero<FqP>()}; }
+ZK_DEV bool f2_is_zero(const Fq2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+ZK_DEV bool f2_eq(const Fq2& a, const Fq2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+ZK_DEV Fq2 f2_add(const Fq2& a, const Fq2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+ZK_DEV Fq2 f2_sub(const Fq2& a, const Fq2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+ZK_DEV Fq2 f2_neg(const Fq2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+ZK_DEV Fq2 f2_dbl(const Fq2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+ZK_DEV Fq2 f2_mul(const Fq2& a, const Fq2& b) {
+  Fq t0 = fp_mul(a.c0, b.c0);
+  Fq t1 = fp_mul(a.c1, b.c1);
+  Fq t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+ZK_DEV Fq2 f2_sqr(const Fq2& a) {
+  // (a0 + a1 u)^2 = (a0+a1)(a0-a1) + 2 a0 a1 u
+  Fq t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fq t1 = fp_mul(a.c0, a.c1);
+  return {t0, fp_dbl(t1)};
+}
+ZK_DEV Fq2 f2_inv(const Fq2& a) {
+  Fq n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  Fq ni = fp_inv(n);
+  return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+ZK_DEV Fq2 f2_from_mont(const Fq2& a) { return {fp_from_mont(a.c0), fp_from_mont(a.c1)}; }
+
+// ---------------------------------------------------------------------------
+// Uniform field interface used by the curve templates (G1 over Fq, G2 over Fq2)
+// ---------------------------------------------------------------------------
+struct FqOps {
+  using T = Fq;
+  static ZK_DEV T zero() { return fp_zero<FqP>(); }
+  static ZK_DEV T one() { return fp_one<FqP>(); }
+  static ZK_DEV bool is_zero(const T& a) { return fp_is_zero(a); }
+  static ZK_DEV bool eq(const T& a, const T& b) { return fp_eq(a, b); }
+  static ZK_DEV T add(const T& a, const T& b) { return fp_add(a, b); }
+  static ZK_DEV T sub(const T& a, const T& b) { return fp_sub(a, b); }
+  static ZK_DEV T neg(const T& a) { return fp_neg(a); }
+  static ZK_DEV T dbl(const T& a) { return fp_dbl(a); }
+  static ZK_DEV T mul(const T& a, const T& b) { return fp_mul(a, b); }
+  static ZK_DEV T sqr(const T& a) { return fp_sqr(a); }
+  static ZK_DEV T inv(const T& a) { return fp_inv(a); }
+  static ZK_DEV T from_mont(const T& a) { return fp_from_mont(a); }
+};
+
+struct Fq2Ops {
+  using T = Fq2;
+  static ZK_DEV T zero() { return f2_zero(); }
+  static ZK_DEV T one() { return f2_one(); }
+  static ZK_DEV bool is_zero(const T& a) { return f2_is_zero(a); }
+  static ZK_DEV bool eq(const T& a, const T& b) { return f2_eq(a, b); }
+  static ZK_DEV T add(const T& a, const T& b) { return f2_add(a, b); }
+  static ZK_DEV T sub(const T& a, const T& b) { return f2_sub(a, b); }
+  static ZK_DEV T neg(const T& a) { return f2_neg(a); }
+  static ZK_DEV T dbl(const T& a) { return f2_dbl(a); }
+  static ZK_DEV T mul(const T& a, const T& b) { return f2_mul(a, b); }
+  static ZK_DEV T sqr(const T& a) { return f2_sqr(a); }
+  static ZK_DEV T inv(const T& a) { return f2_inv(a); }
+  static ZK_DEV T from_mont(const T& a) { return f2_from_mont(a); }
+};
+
+}  // namespace zkfl

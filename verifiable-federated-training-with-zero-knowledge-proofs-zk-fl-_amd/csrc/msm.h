@@ -1,0 +1,321 @@
+// Pippenger multi-scalar multiplication on gfx950 for G1 (Fq) and G2 (Fq2).
+//
+// Replaces ffjavascript `G1.multiExpAffine` / `G2.multiExpAffine` as called by snarkjs
+// groth16_prove for the A, B1, B2, C and H queries (reference
+// call site tests/full_system_simulation.mjs:773-776).  Result semantics are identical:
+// sum_i s_i * P_i with scalars in standard form and affine bases in Montgomery form,
+// (0,0) bases and zero scalars contributing nothing.
+//
+// MI355X design:
+//  * Bases are fixed per proving key, so at key-load time every base P_i is expanded into
+//    W = 16 window copies 2^(16 j) P_i (affine, Montgomery), laid out [i][j] (64 B / 128 B
+//    each).  One MSM is then a single bucket set: every (i, j) with a non-zero signed 16-bit
+//    digit d_ij lands in bucket |d_ij|-1 (2^15 buckets), no per-window bucket reduction and
+//    no window combination.  288 GB of HBM makes the 16x base expansion (~2 GB for the
+//    2^18-constraint training circuit) free.
+//  * Signed digits in [-2^15, 2^15]; the sign is applied by negating y on the fly.
+//  * (bucket, entry) pairs are radix-sorted (rocPRIM, 16 key bits), bucket ranges found by
+//    adjacent-key compare, and the accumulation is split into tasks of <= L entries so a
+//    skewed bucket (e.g. all bit-valued witness wires) cannot serialise one lane.
+//  * Accumulation uses XYZZ + affine mixed additions (10 Fq mul for G1).
+//  * Bucket reduction sum_b (b+1) S_b uses grouped running sums (groups of RG buckets),
+//    recursively on the group sums, then a Horner combination.
+#pragma once
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "msm_api.h"
+
+namespace zkfl {
+
+// ---------------------------------------------------------------------------
+// Key-load-time window expansion: out[i*W + j] = 2^(16 j) * in[i]  (affine)
+// ---------------------------------------------------------------------------
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__ in, size_t n, Affine<F>* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  using T = typename F::T;
+  Affine<F> p = in[i];
+  if (aff_is_inf(p)) {
+    for (int j = 0; j < MSM_W; j++) out[i * MSM_W + j] = p;
+    return;
+  }
+  // Keep the 16 window copies in XYZZ in the output slots' scratch (global), with a
+  // Montgomery batch inversion of their ZZZ over the 16 copies.
+  XYZZ<F> acc = xyzz_from_affine<F>(p);
+  T pref[MSM_W];
+  XYZZ<F> pts[MSM_W];
+  for (int j = 0; j < MSM_W; j++) {
+    pts[j] = acc;
+    pref[j] = (j == 0) ? acc.ZZZ : F::mul(pref[j - 1], acc.ZZZ);
+    if (j + 1 < MSM_W)
+      for (int k = 0; k < MSM_C; k++) acc = xyzz_dbl<F>(acc);
+  }
+  T inv = F::inv(pref[MSM_W - 1]);
+  for (int j = MSM_W - 1; j >= 0; j--) {
+    T iZZZ = (j == 0) ? inv : F::mul(inv, pref[j - 1]);
+    if (j > 0) inv = F::mul(inv, pts[j].ZZZ);
+    T iZ = F::mul(pts[j].ZZ, iZZZ);
+    Affine<F> a;
+    a.x = F::mul(pts[j].X, F::sqr(iZ));
+    a.y = F::mul(pts[j].Y, iZZZ);
+    out[i * MSM_W + j] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-MSM kernels
+// ---------------------------------------------------------------------------
+// Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31.
+static __global__ void k_msm_digits(const uint32_t* __restrict__ scalars, size_t n,
+                             uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* sp = reinterpret_cast<const uint4*>(scalars + i * 8);
+  uint4 a = sp[0], b = sp[1];
+  uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < MSM_W; j++) {
+    uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+    int32_t d = (int32_t)(raw + carry);
+    if (d > MSM_NB) {
+      d -= (1 << MSM_C);
+      carry = 1;
+    } else {
+      carry = 0;
+    }
+    size_t e = i * MSM_W + j;
+    if (d == 0) {
+      keys[e] = MSM_KEY_NONE;
+      vals[e] = 0;
+    } else {
+      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      keys[e] = (uint16_t)(mag - 1);
+      vals[e] = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
+    }
+  }
+}
+
+static __global__ void k_msm_bounds(const uint16_t* __restrict__ keys, size_t m,
+                             uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend,
+                             uint32_t* __restrict__ nnz) {
+  size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  uint16_t k = keys[p];
+  if (k == MSM_KEY_NONE) return;
+  if (p == 0 || keys[p - 1] != k) bstart[k] = (uint32_t)p;
+  const bool last = (p == m - 1 || keys[p + 1] != k);
+  if (last) bend[k] = (uint32_t)(p + 1);
+  if (p == m - 1 || keys[p + 1] == MSM_KEY_NONE) *nnz = (uint32_t)(p + 1);  // non-zero digits
+}
+
+static __global__ void k_msm_task_count(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                                 uint32_t* __restrict__ tcount) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= MSM_NB) return;
+  uint32_t len = bend[b] - bstart[b];
+  tcount[b] = (len + MSM_L - 1) / MSM_L;
+}
+
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_accumulate(const uint32_t* __restrict__ vals,
+                                                        const Affine<F>* __restrict__ bases,
+                                                        const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ bend,
+                                                        const uint32_t* __restrict__ toff,
+                                                        size_t max_tasks,
+                                                        XYZZ<F>* __restrict__ partials) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= max_tasks) return;
+  const uint32_t total = toff[MSM_NB];
+  if (t >= total) return;
+  // bucket b: largest b with toff[b] <= t
+  int lo = 0, hi = MSM_NB - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (toff[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  const int b = lo;
+  const uint32_t k = (uint32_t)t - toff[b];
+  const uint32_t s = bstart[b] + k * MSM_L;
+  uint32_t e = s + MSM_L;
+  if (e > bend[b]) e = bend[b];
+  XYZZ<F> acc = xyzz_inf<F>();
+  for (uint32_t p = s; p < e; p++) {
+    uint32_t v = vals[p];
+    Affine<F> a = bases[v & 0x7FFFFFFFu];
+    if (v & 0x80000000u) a = aff_neg<F>(a);
+    acc = xyzz_madd<F>(acc, a);
+  }
+  partials[t] = acc;
+}
+
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_bucket_sum(const XYZZ<F>* __restrict__ partials, const uint32_t* __restrict__ toff,
+                                 XYZZ<F>* __restrict__ buckets) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= MSM_NB) return;
+  XYZZ<F> acc = xyzz_inf<F>();
+  for (uint32_t t = toff[b]; t < toff[b + 1]; t++) acc = xyzz_add<F>(acc, partials[t]);
+  buckets[b] = acc;
+}
+
+// One level of the grouped running-sum bucket reduction over in[0..K):
+//   acc[g] = sum_{k in group} (k - g*RG + 1) * in[k],   run[g] = sum_{k in group} in[k]
+// acc[g] is pre-scaled by RG^level (level doublings) so all levels sum together.
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_reduce_level(const XYZZ<F>* __restrict__ in, int K, int shift_dbls,
+                                   XYZZ<F>* __restrict__ acc_out, XYZZ<F>* __restrict__ run_out) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  int G = (K + MSM_RG - 1) / MSM_RG;
+  if (g >= G) return;
+  int lo = g * MSM_RG;
+  int hi = lo + MSM_RG;
+  if (hi > K) hi = K;
+  XYZZ<F> run = xyzz_inf<F>();
+  XYZZ<F> acc = xyzz_inf<F>();
+  for (int k = hi - 1; k >= lo; k--) {
+    run = xyzz_add<F>(run, in[k]);
+    acc = xyzz_add<F>(acc, run);
+  }
+  for (int d = 0; d < shift_dbls; d++) acc = xyzz_dbl<F>(acc);
+  acc_out[g] = acc;
+  run_out[g] = run;
+}
+
+// out[i] = sum of in[i*8 .. i*8+8)
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_sum8(const XYZZ<F>* __restrict__ in, int n, XYZZ<F>* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int lo = i * 8;
+  if (lo >= n) return;
+  int hi = lo + 8;
+  if (hi > n) hi = n;
+  XYZZ<F> acc = in[lo];
+  for (int k = lo + 1; k < hi; k++) acc = xyzz_add<F>(acc, in[k]);
+  out[i] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// Host-side plan
+// ---------------------------------------------------------------------------
+template <class F>
+hipError_t msm_plan_alloc(MsmPlan<F>& pl, size_t n, hipStream_t st) {
+  pl.n = n;
+  const size_t m = n * MSM_W;
+  ZK_CHECK(hipMalloc(&pl.bases_w, m * sizeof(Affine<F>)));
+  ZK_CHECK(hipMalloc(&pl.keys_in, m * sizeof(uint16_t)));
+  ZK_CHECK(hipMalloc(&pl.keys_out, m * sizeof(uint16_t)));
+  ZK_CHECK(hipMalloc(&pl.vals_in, m * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&pl.vals_out, m * sizeof(uint32_t)));
+  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, pl.sort_tmp_bytes, pl.keys_in, pl.keys_out, pl.vals_in,
+                                     pl.vals_out, m, 0, 16, st));
+  ZK_CHECK(hipMalloc(&pl.sort_tmp, pl.sort_tmp_bytes));
+  ZK_CHECK(rocprim::exclusive_scan(nullptr, pl.scan_tmp_bytes, pl.tcount, pl.toff, 0u,
+                                   (size_t)MSM_NB + 1, rocprim::plus<uint32_t>(), st));
+  ZK_CHECK(hipMalloc(&pl.scan_tmp, pl.scan_tmp_bytes));
+  ZK_CHECK(hipMalloc(&pl.bstart, MSM_NB * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&pl.bend, MSM_NB * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&pl.tcount, (MSM_NB + 1) * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&pl.toff, (MSM_NB + 1) * sizeof(uint32_t)));
+  pl.max_tasks = m / MSM_L + MSM_NB + 1;
+  ZK_CHECK(hipMalloc(&pl.partials, pl.max_tasks * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&pl.buckets, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&pl.red_acc, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&pl.red_run, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&pl.red_tmp, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&pl.nnz, sizeof(uint32_t)));
+  return hipSuccess;
+}
+
+template <class F>
+void msm_plan_free(MsmPlan<F>& pl) {
+  void* ptrs[] = {pl.bases_w, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, pl.sort_tmp, pl.scan_tmp,
+                  pl.bstart, pl.bend, pl.tcount, pl.toff, pl.partials, pl.buckets, pl.red_acc, pl.red_run,
+                  pl.red_tmp, pl.nnz};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  pl = MsmPlan<F>();
+}
+
+// Expand n affine bases (device pointer) into the plan's window table.
+template <class F>
+hipError_t msm_plan_set_bases(MsmPlan<F>& pl, const Affine<F>* d_bases, hipStream_t st) {
+  hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(pl.n, 64)), dim3(64), 0, st, d_bases, pl.n, pl.bases_w);
+  return hipGetLastError();
+}
+
+// Run one MSM: d_scalars = n standard-form scalars (8 x u32 each, device) -> *d_out (device).
+template <class F>
+hipError_t msm_run(MsmPlan<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out, hipStream_t st,
+                   Profiler* prof = nullptr, const char* tag = nullptr) {
+  const size_t m = pl.n * MSM_W;
+  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(pl.n, 256)), dim3(256), 0, st, d_scalars, pl.n, pl.keys_in,
+                     pl.vals_in);
+  ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, pl.sort_tmp_bytes, pl.keys_in, pl.keys_out, pl.vals_in,
+                                     pl.vals_out, m, 0, 16, st));
+  ZK_CHECK(hipMemsetAsync(pl.bstart, 0, MSM_NB * sizeof(uint32_t), st));
+  ZK_CHECK(hipMemsetAsync(pl.bend, 0, MSM_NB * sizeof(uint32_t), st));
+  ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_msm_bounds, dim3(zk_grid(m, 256)), dim3(256), 0, st, pl.keys_out, m, pl.bstart, pl.bend,
+                     pl.nnz);
+  ZK_CHECK(hipMemsetAsync(pl.tcount + MSM_NB, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_msm_task_count, dim3(zk_grid(MSM_NB, 256)), dim3(256), 0, st, pl.bstart, pl.bend,
+                     pl.tcount);
+  ZK_CHECK(rocprim::exclusive_scan(pl.scan_tmp, pl.scan_tmp_bytes, pl.tcount, pl.toff, 0u, (size_t)MSM_NB + 1,
+                                   rocprim::plus<uint32_t>(), st));
+  const int pidx = prof ? prof->begin(tag, st) : -1;
+  hipLaunchKernelGGL(k_msm_accumulate<F>, dim3(zk_grid(pl.max_tasks, 64)), dim3(64), 0, st, pl.vals_out,
+                     pl.bases_w, pl.bstart, pl.bend, pl.toff, pl.max_tasks, pl.partials);
+  if (prof) prof->end(pidx, st, 0.0, pl.nnz);
+  hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.partials, pl.toff,
+                     pl.buckets);
+  // grouped running-sum reduction
+  const XYZZ<F>* in = pl.buckets;
+  int K = MSM_NB;
+  int level = 0;
+  int nacc = 0;
+  XYZZ<F>* run_bufs[2] = {pl.red_run, pl.red_tmp};
+  while (K > 0) {
+    int G = (K + MSM_RG - 1) / MSM_RG;
+    int shift = 3 * level;  // RG = 8 = 2^3
+    XYZZ<F>* run_out = run_bufs[level & 1];
+    hipLaunchKernelGGL(k_msm_reduce_level<F>, dim3(zk_grid(G, 64)), dim3(64), 0, st, in, K, shift,
+                       pl.red_acc + nacc, run_out);
+    nacc += G;
+    in = run_out + 1;
+    K = G - 1;
+    level++;
+  }
+  // sum all acc entries
+  XYZZ<F>* src = pl.red_acc;
+  XYZZ<F>* dst = pl.red_tmp;
+  int cnt = nacc;
+  // red_tmp may hold the last run level's data; it is no longer needed here.
+  while (cnt > 1) {
+    int nout = (cnt + 7) / 8;
+    hipLaunchKernelGGL(k_msm_sum8<F>, dim3(zk_grid(nout, 64)), dim3(64), 0, st, src, cnt, dst);
+    XYZZ<F>* t = src;
+    src = dst;
+    dst = (t == pl.red_acc) ? pl.red_run : t;
+    cnt = nout;
+  }
+  ZK_CHECK(hipMemcpyAsync(d_out, src, sizeof(XYZZ<F>), hipMemcpyDeviceToDevice, st));
+  return hipGetLastError();
+}
+
+// Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
+#define ZKFL_MSM_DEFINE(SUF, F)                                                                   \
+  hipError_t msm_alloc_##SUF(MsmPlan<F>& pl, size_t n, hipStream_t st) { return msm_plan_alloc(pl, n, st); } \
+  void msm_free_##SUF(MsmPlan<F>& pl) { msm_plan_free(pl); }                                    \
+  hipError_t msm_set_bases_##SUF(MsmPlan<F>& pl, const Affine<F>* b, hipStream_t st) {           \
+    return msm_plan_set_bases(pl, b, st);                                                        \
+  }                                                                                              \
+  hipError_t msm_run_##SUF(MsmPlan<F>& pl, const uint32_t* s, XYZZ<F>* out, hipStream_t st, Profiler* prof, \
+                           const char* tag) {                                                    \
+    return msm_run(pl, s, out, st, prof, tag);                                                   \
+  }
+
+}  // namespace zkfl

@@ -1,0 +1,217 @@
+// NTT kernels (see ntt.h for the algorithm and the reference behaviour it replaces).
+#include "ntt.h"
+#include "fr_consts.h"
+
+namespace zkfl {
+
+constexpr int NTT_LDS_LOG = 10;
+constexpr int NTT_LDS_N = 1 << NTT_LDS_LOG;
+
+// tw[i] = root^i (Montgomery) for i < n/2
+__global__ void k_ntt_twiddles(Fr* __restrict__ tw, size_t half, Fr root_mont) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= half) return;
+  // root^i by square-and-multiply over the bits of i
+  Fr acc = fp_one<FrP>();
+  Fr base = root_mont;
+  size_t e = i;
+  while (e) {
+    if (e & 1) acc = fp_mul(acc, base);
+    base = fp_sqr(base);
+    e >>= 1;
+  }
+  tw[i] = acc;
+}
+
+// coset[p] = inc^{bitrev(p)} / n (Montgomery), p < n
+__global__ void k_ntt_coset_table(Fr* __restrict__ tab, size_t n, int logn, Fr inc_mont, Fr ninv_mont) {
+  size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  size_t i = __brevll((unsigned long long)p) >> (64 - logn);
+  Fr acc = ninv_mont;
+  Fr base = inc_mont;
+  size_t e = i;
+  while (e) {
+    if (e & 1) acc = fp_mul(acc, base);
+    base = fp_sqr(base);
+    e >>= 1;
+  }
+  tab[p] = acc;
+}
+
+// One global DIF stage (span `half`, len = 2*half); tw stride = n / len.
+__global__ void k_ntt_dif_stage(Fr* __restrict__ a, size_t n, size_t half, const Fr* __restrict__ tw,
+                                size_t twstride, int nvec, size_t vstride) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t nb = n >> 1;
+  if (t >= nb * nvec) return;
+  size_t v = t / nb;
+  t -= v * nb;
+  Fr* x = a + v * vstride;
+  size_t j = t & (half - 1);
+  size_t i0 = ((t - j) << 1) + j;
+  size_t i1 = i0 + half;
+  Fr u = x[i0], w = x[i1];
+  x[i0] = fp_add(u, w);
+  x[i1] = fp_mul(fp_sub(u, w), tw[j * twstride]);
+}
+
+__global__ void k_ntt_dit_stage(Fr* __restrict__ a, size_t n, size_t half, const Fr* __restrict__ tw,
+                                size_t twstride, int nvec, size_t vstride) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t nb = n >> 1;
+  if (t >= nb * nvec) return;
+  size_t v = t / nb;
+  t -= v * nb;
+  Fr* x = a + v * vstride;
+  size_t j = t & (half - 1);
+  size_t i0 = ((t - j) << 1) + j;
+  size_t i1 = i0 + half;
+  Fr u = x[i0];
+  Fr w = fp_mul(x[i1], tw[j * twstride]);
+  x[i0] = fp_add(u, w);
+  x[i1] = fp_sub(u, w);
+}
+
+// Fused small-span stages inside one LDS tile of T = min(n, 1024) elements.
+//   DIF: spans T/2 .. 1 (the last log2 T stages of the inverse transform)
+//   DIT: spans 1 .. T/2 (the first log2 T stages of the forward transform)
+template <bool DIF>
+__global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, int logt,
+                                                 const Fr* __restrict__ tw, int nvec, size_t vstride) {
+  __shared__ Fr tile[NTT_LDS_N];
+  const size_t T = (size_t)1 << logt;
+  const size_t tiles_per_vec = n >> logt;
+  const size_t tile_id = blockIdx.x;
+  const size_t v = tile_id / tiles_per_vec;
+  if (v >= (size_t)nvec) return;
+  Fr* x = a + v * vstride + (tile_id - v * tiles_per_vec) * T;
+  for (size_t i = threadIdx.x; i < T; i += blockDim.x) tile[i] = x[i];
+  __syncthreads();
+  const size_t nbf = T >> 1;
+  for (int s = 0; s < logt; s++) {
+    const size_t half = DIF ? (T >> (s + 1)) : ((size_t)1 << s);
+    const size_t len = half << 1;
+    const size_t twstride = n / len;
+    for (size_t t = threadIdx.x; t < nbf; t += blockDim.x) {
+      size_t j = t & (half - 1);
+      size_t i0 = ((t - j) << 1) + j;
+      size_t i1 = i0 + half;
+      Fr u = tile[i0], w = tile[i1];
+      Fr tws = tw[j * twstride];
+      if (DIF) {
+        tile[i0] = fp_add(u, w);
+        tile[i1] = fp_mul(fp_sub(u, w), tws);
+      } else {
+        w = fp_mul(w, tws);
+        tile[i0] = fp_add(u, w);
+        tile[i1] = fp_sub(u, w);
+      }
+    }
+    __syncthreads();
+  }
+  for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
+}
+
+__global__ void k_ntt_scale(Fr* __restrict__ a, size_t n, const Fr* __restrict__ tab, int nvec,
+                            size_t vstride) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * nvec) return;
+  size_t v = t / n;
+  size_t p = t - v * n;
+  a[v * vstride + p] = fp_mul(a[v * vstride + p], tab[p]);
+}
+
+
+static inline Fr fr_from_limbs(const uint32_t v[8]) {
+  Fr r;
+  for (int i = 0; i < 8; i++) r.v[i] = v[i];
+  return r;
+}
+
+__global__ void k_fr_to_mont_one(Fr* out, Fr in) { *out = fp_to_mont(in); }
+
+hipError_t ntt_plan_alloc(NttPlan& pl, int logn, hipStream_t st) {
+  pl.logn = logn;
+  pl.n = (size_t)1 << logn;
+  size_t half = pl.n > 1 ? pl.n / 2 : 1;
+  ZK_CHECK(hipMalloc(&pl.tw_fwd, half * sizeof(Fr)));
+  ZK_CHECK(hipMalloc(&pl.tw_inv, half * sizeof(Fr)));
+  ZK_CHECK(hipMalloc(&pl.coset, pl.n * sizeof(Fr)));
+  // roots in Montgomery form (converted on device)
+  Fr* tmp;
+  ZK_CHECK(hipMalloc(&tmp, 4 * sizeof(Fr)));
+  uint32_t inc_std[8];
+  for (int i = 0; i < 8; i++) inc_std[i] = (logn == 28) ? FR_SHIFT[i] : FR_ROOT[logn + 1][i];
+  hipLaunchKernelGGL(k_fr_to_mont_one, dim3(1), dim3(1), 0, st, tmp + 0, fr_from_limbs(FR_ROOT[logn]));
+  hipLaunchKernelGGL(k_fr_to_mont_one, dim3(1), dim3(1), 0, st, tmp + 1, fr_from_limbs(FR_ROOT_INV[logn]));
+  hipLaunchKernelGGL(k_fr_to_mont_one, dim3(1), dim3(1), 0, st, tmp + 2, fr_from_limbs(inc_std));
+  hipLaunchKernelGGL(k_fr_to_mont_one, dim3(1), dim3(1), 0, st, tmp + 3, fr_from_limbs(FR_INV_2K[logn]));
+  Fr h[4];
+  ZK_CHECK(hipMemcpyAsync(h, tmp, sizeof(h), hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  ZK_CHECK(hipFree(tmp));
+  hipLaunchKernelGGL(k_ntt_twiddles, dim3(zk_grid(half, 256)), dim3(256), 0, st, pl.tw_fwd, half, h[0]);
+  hipLaunchKernelGGL(k_ntt_twiddles, dim3(zk_grid(half, 256)), dim3(256), 0, st, pl.tw_inv, half, h[1]);
+  hipLaunchKernelGGL(k_ntt_coset_table, dim3(zk_grid(pl.n, 256)), dim3(256), 0, st, pl.coset, pl.n,
+                     logn, h[2], h[3]);
+  return hipGetLastError();
+}
+
+void ntt_plan_free(NttPlan& pl) {
+  if (pl.tw_fwd) (void)hipFree(pl.tw_fwd);
+  if (pl.tw_inv) (void)hipFree(pl.tw_inv);
+  if (pl.coset) (void)hipFree(pl.coset);
+  pl = NttPlan();
+}
+
+// DIF pass of the inverse transform (natural -> bit-reversed), without 1/n.
+static hipError_t ntt_dif(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size_t vstride, hipStream_t st) {
+  const size_t n = pl.n;
+  const int logt = pl.logn < NTT_LDS_LOG ? pl.logn : NTT_LDS_LOG;
+  const size_t nb = (n >> 1) * nvec;
+  for (int s = 0; s < pl.logn - logt; s++) {
+    size_t half = n >> (s + 1);
+    hipLaunchKernelGGL(k_ntt_dif_stage, dim3(zk_grid(nb, 256)), dim3(256), 0, st, d, n, half, tw, n / (2 * half),
+                       nvec, vstride);
+  }
+  if (logt > 0)
+    hipLaunchKernelGGL(k_ntt_lds<true>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
+                       nvec, vstride);
+  return hipGetLastError();
+}
+
+// DIT pass (bit-reversed -> natural).
+static hipError_t ntt_dit(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size_t vstride, hipStream_t st) {
+  const size_t n = pl.n;
+  const int logt = pl.logn < NTT_LDS_LOG ? pl.logn : NTT_LDS_LOG;
+  const size_t nb = (n >> 1) * nvec;
+  if (logt > 0)
+    hipLaunchKernelGGL(k_ntt_lds<false>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
+                       nvec, vstride);
+  for (int s = logt; s < pl.logn; s++) {
+    size_t half = (size_t)1 << s;
+    hipLaunchKernelGGL(k_ntt_dit_stage, dim3(zk_grid(nb, 256)), dim3(256), 0, st, d, n, half, tw, n / (2 * half),
+                       nvec, vstride);
+  }
+  return hipGetLastError();
+}
+
+// In place: nvec vectors (stride vstride) of evaluations on the domain -> evaluations on
+// the odd coset (snarkjs ifft + batchApplyKey + fft).
+hipError_t ntt_coset_shift(const NttPlan& pl, Fr* d, int nvec, size_t vstride, hipStream_t st) {
+  ZK_CHECK(ntt_dif(pl, d, pl.tw_inv, nvec, vstride, st));
+  hipLaunchKernelGGL(k_ntt_scale, dim3(zk_grid(pl.n * nvec, 256)), dim3(256), 0, st, d, pl.n, pl.coset, nvec,
+                     vstride);
+  return ntt_dit(pl, d, pl.tw_fwd, nvec, vstride, st);
+}
+
+// Plain transforms (natural order in and out) for parity tests: inverse includes 1/n.
+__global__ void k_bitrev_copy(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n, int logn) {
+  size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  size_t q = logn ? (__brevll((unsigned long long)p) >> (64 - logn)) : 0;
+  out[q] = in[p];
+}
+
+}  // namespace zkfl

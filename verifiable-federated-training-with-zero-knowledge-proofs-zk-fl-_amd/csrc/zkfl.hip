@@ -1,0 +1,856 @@
+// libzkfl: MI355X-native Groth16 prover (BN254) behind the C ABI in include/zkfl.h.
+//
+// Replaces `snarkjs groth16 prove` [ext] as invoked by the reference harness
+// (tests/full_system_simulation.mjs:773-776).  Algorithm per proof (snarkjs groth16_prove,
+// restated in oracle/groth16.py::prove):
+//   1. buildABC1: a = A.w, b = B.w over the domain rows (zkey section 4 coefficients),
+//      c = a o b                                           -> k_abc (CSR rows, Montgomery)
+//   2. a,b,c: ifft -> * inc^i -> fft  (odd coset)          -> ntt_coset_shift (3 vectors)
+//   3. joinABC: h = a*b - c, from Montgomery               -> k_join
+//   4. multiExpAffine A(w), B1(w), B2(w), C(w_priv), H(h)  -> msm_run (G1 x4, G2 x1)
+//   5. pi_a = A + alpha1 + r delta1, pi_b = B2 + beta2 + s delta2,
+//      pi_c = C + H + s pi_a + r (B1 + beta1 + s delta1) - r s delta1
+//      The constant terms are folded into the MSMs as extra bases (alpha1/delta1 on A,
+//      beta1/delta1 on B1, beta2/delta2 on B2, delta1 with scalar -rs on C); only
+//      s*pi_a + r*B1 remains for k_assemble (Shamir double-and-add), then affine, std form.
+// Everything from the device-resident witness to the 256-byte proof runs on the GPU; the host
+// only parses files, uploads, and launches.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "curve.h"
+#include "field.h"
+#include "msm_api.h"
+#include "ntt.h"
+#include "prof.h"
+#include "zkfl.h"
+
+using namespace zkfl;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? ZKFL_E_OOM : ZKFL_E_DEVICE;
+}
+
+#define HIP_TRY(x, where)                      \
+  do {                                         \
+    hipError_t _e = (x);                       \
+    if (_e != hipSuccess) return hip_fail(_e, where); \
+  } while (0)
+
+const uint32_t R_LIMBS[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                             0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+const uint32_t Q_LIMBS[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                             0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+
+bool lt_r(const uint32_t* v) {  // v < r
+  for (int i = 7; i >= 0; i--) {
+    if (v[i] != R_LIMBS[i]) return v[i] < R_LIMBS[i];
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// iden3 binfile reader
+// ---------------------------------------------------------------------------
+struct Section {
+  size_t off = 0, size = 0;
+  bool present = false;
+};
+
+int read_binfile(const uint8_t* buf, size_t len, const char* magic, std::vector<Section>& secs) {
+  if (!buf || len < 12) return fail(ZKFL_E_FORMAT, "file too short");
+  if (memcmp(buf, magic, 4) != 0) return fail(ZKFL_E_FORMAT, std::string("bad magic, expected ") + magic);
+  uint32_t nsec;
+  memcpy(&nsec, buf + 8, 4);
+  size_t off = 12;
+  secs.assign(16, Section());
+  for (uint32_t i = 0; i < nsec; i++) {
+    if (off + 12 > len) return fail(ZKFL_E_FORMAT, "truncated section header");
+    uint32_t typ;
+    uint64_t size;
+    memcpy(&typ, buf + off, 4);
+    memcpy(&size, buf + off + 4, 8);
+    off += 12;
+    if (off + size > len) return fail(ZKFL_E_FORMAT, "truncated section");
+    if (typ < secs.size() && !secs[typ].present) {
+      secs[typ].off = off;
+      secs[typ].size = size;
+      secs[typ].present = true;
+    }
+    off += size;
+  }
+  return ZKFL_OK;
+}
+
+struct WtnsView {
+  const uint8_t* data = nullptr;  // nWitness x 32 B std
+  uint32_t n = 0;
+};
+
+int parse_wtns(const uint8_t* buf, size_t len, WtnsView& out) {
+  std::vector<Section> s;
+  int rc = read_binfile(buf, len, "wtns", s);
+  if (rc) return rc;
+  if (!s[1].present || !s[2].present) return fail(ZKFL_E_FORMAT, "wtns: missing section");
+  const uint8_t* h = buf + s[1].off;
+  uint32_t n8;
+  memcpy(&n8, h, 4);
+  if (n8 != 32 || s[1].size < 4 + 32 + 4) return fail(ZKFL_E_FORMAT, "wtns: n8 != 32");
+  if (memcmp(h + 4, R_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "wtns: prime is not bn128 r");
+  memcpy(&out.n, h + 36, 4);
+  if (s[2].size != (size_t)out.n * 32) return fail(ZKFL_E_FORMAT, "wtns: section 2 size");
+  out.data = buf + s[2].off;
+  return ZKFL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+// ABC over CSR rows.  coef raw = coef * R^2 mod r (snarkjs zkey section 4), w std form, so
+// mont_mul(coef_raw, w) = (coef * w) in Montgomery form.
+__global__ void k_abc(const uint32_t* __restrict__ rowA, const uint32_t* __restrict__ rowB,
+                      const uint32_t* __restrict__ cols, const Fr* __restrict__ coefs,
+                      const Fr* __restrict__ w, size_t n, Fr* __restrict__ abc) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fr a = fp_zero<FrP>();
+  for (uint32_t k = rowA[j]; k < rowA[j + 1]; k++) a = fp_add(a, fp_mul(coefs[k], w[cols[k]]));
+  Fr b = fp_zero<FrP>();
+  for (uint32_t k = rowB[j]; k < rowB[j + 1]; k++) b = fp_add(b, fp_mul(coefs[k], w[cols[k]]));
+  abc[j] = a;
+  abc[n + j] = b;
+  abc[2 * n + j] = fp_mul(a, b);
+}
+
+// h = a*b - c (coset evaluations), to standard form for the H MSM.
+__global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fr v = fp_sub(fp_mul(abc[j], abc[n + j]), abc[2 * n + j]);
+  h[j] = fp_from_mont(v);
+}
+
+// Augmented scalar slots: A: [.., 1, r], B: [.., 1, s], C: [.., -r s].  plain -> zeros.
+__global__ void k_set_rs(const Fr* __restrict__ rs, Fr* __restrict__ wA, Fr* __restrict__ wB, Fr* __restrict__ wC,
+                         size_t nVars, size_t nC, int plain) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Fr one = fp_zero<FrP>();
+  one.v[0] = plain ? 0u : 1u;
+  Fr r = plain ? fp_zero<FrP>() : rs[0];
+  Fr s = plain ? fp_zero<FrP>() : rs[1];
+  wA[nVars] = one;
+  wA[nVars + 1] = r;
+  wB[nVars] = one;
+  wB[nVars + 1] = s;
+  Fr mrs = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
+  wC[nC] = mrs;
+}
+
+template <class F>
+__device__ void store_affine_std(const Affine<F>& a, uint32_t* out);
+
+template <>
+__device__ void store_affine_std<FqOps>(const Affine<FqOps>& a, uint32_t* out) {
+  Fq x = fp_from_mont(a.x), y = fp_from_mont(a.y);
+  for (int i = 0; i < 8; i++) {
+    out[i] = x.v[i];
+    out[8 + i] = y.v[i];
+  }
+}
+
+template <>
+__device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out) {
+  Fq2 x = f2_from_mont(a.x), y = f2_from_mont(a.y);
+  for (int i = 0; i < 8; i++) {
+    out[i] = x.c0.v[i];
+    out[8 + i] = x.c1.v[i];
+    out[16 + i] = y.c0.v[i];
+    out[24 + i] = y.c1.v[i];
+  }
+}
+
+// Final assembly (one lane).  res[0]=A', res[1]=B1', res[2]=C', res[3]=H; resB2 = B2'.
+__global__ void __launch_bounds__(64) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2, const Fr* __restrict__ rs,
+                           uint32_t* __restrict__ proof) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const G1P A = res[0], B1 = res[1];
+  G1P C = xyzz_add<FqOps>(res[2], res[3]);
+  // T = s*A + r*B1 (Shamir's trick)
+  const G1P AB = xyzz_add<FqOps>(A, B1);
+  const Fr r = rs[0], s = rs[1];
+  G1P T = xyzz_inf<FqOps>();
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      T = xyzz_dbl<FqOps>(T);
+      const uint32_t bs = (s.v[i] >> b) & 1u, br = (r.v[i] >> b) & 1u;
+      if (bs && br) T = xyzz_add<FqOps>(T, AB);
+      else if (bs) T = xyzz_add<FqOps>(T, A);
+      else if (br) T = xyzz_add<FqOps>(T, B1);
+    }
+  }
+  C = xyzz_add<FqOps>(C, T);
+  store_affine_std<FqOps>(xyzz_to_affine<FqOps>(A), proof);
+  store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
+  store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
+}
+
+// MSM result(s) -> std affine bytes (parity hooks)
+template <class F>
+__global__ void __launch_bounds__(64) k_point_out(const XYZZ<F>* __restrict__ p, int n, uint32_t* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  constexpr int words = sizeof(Affine<F>) / 4;
+  store_affine_std<F>(xyzz_to_affine<F>(p[i]), out + i * words);
+}
+
+__global__ void k_fr_std_to_mont(Fr* __restrict__ a, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  a[i] = fp_to_mont(a[i]);
+}
+
+__global__ void k_fr_mont_to_std(Fr* __restrict__ a, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  a[i] = fp_from_mont(a[i]);
+}
+
+// Dev ceremony: out[i] = k_i * G (mont affine)
+template <class F>
+__global__ void __launch_bounds__(64) k_gen_mul(const uint32_t* __restrict__ scalars, size_t n, Affine<F> gen_mont,
+                          Affine<F>* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int j = 0; j < 8; j++) k[j] = scalars[i * 8 + j];
+  XYZZ<F> g = xyzz_from_affine<F>(gen_mont);
+  out[i] = xyzz_to_affine<F>(xyzz_scalar_mul<F>(g, k));
+}
+
+__global__ void k_g1_gen_mont(G1Aff* out) {
+  Fq x = fp_zero<FqP>(), y = fp_zero<FqP>();
+  x.v[0] = 1;
+  y.v[0] = 2;
+  out->x = fp_to_mont(x);
+  out->y = fp_to_mont(y);
+}
+
+__global__ void k_g2_gen_mont(G2Aff* out) {
+  // snarkjs/ethereum bn128 G2 generator (std form limbs)
+  const uint32_t xc0[8] = {0xd992f6edu, 0x46debd5cu, 0xf75edaddu, 0x674322d4u, 0x5e5c4479u, 0x426a0066u, 0x121f1e76u, 0x1800deefu};
+  const uint32_t xc1[8] = {0xaef312c2u, 0x97e485b7u, 0x35a9e712u, 0xf1aa4933u, 0x31fb5d25u, 0x7260bfb7u, 0x920d483au, 0x198e9393u};
+  const uint32_t yc0[8] = {0x66fa7daau, 0x4ce6cc01u, 0x0c43d37bu, 0xe3d1e769u, 0x8dcb408fu, 0x4aab7180u, 0xdb8c6debu, 0x12c85ea5u};
+  const uint32_t yc1[8] = {0xd122975bu, 0x55acdadcu, 0x70b38ef3u, 0xbc4b3133u, 0x690c3395u, 0xec9e99adu, 0x585ff075u, 0x090689d0u};
+  Fq a, b, c, d;
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = xc0[i];
+    b.v[i] = xc1[i];
+    c.v[i] = yc0[i];
+    d.v[i] = yc1[i];
+  }
+  out->x = {fp_to_mont(a), fp_to_mont(b)};
+  out->y = {fp_to_mont(c), fp_to_mont(d)};
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Context / key / witness objects
+// ---------------------------------------------------------------------------
+struct zkfl_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  Profiler prof;
+};
+
+struct zkfl_key {
+  zkfl_ctx* ctx = nullptr;
+  uint32_t nVars = 0, nPub = 0, n = 0;
+  int logn = 0;
+  size_t nC = 0;  // C query length
+  size_t K = 0;
+  uint32_t* rowA = nullptr;  // [n+1]
+  uint32_t* rowB = nullptr;  // [n+1]
+  uint32_t* cols = nullptr;  // [K]
+  Fr* coefs = nullptr;       // [K]
+  MsmPlan<FqOps> pA, pB1, pC, pH;
+  MsmPlan<Fq2Ops> pB2;
+  NttPlan ntt;
+  // per-proof workspace
+  Fr* wA = nullptr;   // [nVars+2]
+  Fr* wB = nullptr;   // [nVars+2]
+  Fr* wC = nullptr;   // [nC+1]
+  Fr* abc = nullptr;  // [3n]
+  Fr* h = nullptr;    // [n]
+  G1P* res = nullptr;     // [4]
+  G2P* resB2 = nullptr;   // [1]
+  Fr* d_rs = nullptr;     // [2]
+  uint32_t* d_proof = nullptr;  // [64]
+  uint8_t* h_pinned = nullptr;  // 256 + 64 host staging
+};
+
+struct zkfl_witness {
+  const zkfl_key* key = nullptr;
+  Fr* d = nullptr;  // nVars std-form elements
+  std::vector<uint8_t> pub;  // nPub x 32 B
+};
+
+namespace {
+
+void key_release(zkfl_key* k) {
+  if (!k) return;
+  msm_free_g1(k->pA);
+  msm_free_g1(k->pB1);
+  msm_free_g1(k->pC);
+  msm_free_g1(k->pH);
+  msm_free_g2(k->pB2);
+  ntt_plan_free(k->ntt);
+  void* ptrs[] = {k->rowA, k->rowB, k->cols, k->coefs, k->wA, k->wB, k->wC, k->abc, k->h, k->res, k->resB2,
+                  k->d_rs, k->d_proof};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (k->h_pinned) (void)hipHostFree(k->h_pinned);
+  delete k;
+}
+
+int get_rs(const uint8_t* rs, uint32_t out[16]) {
+  if (rs) {
+    memcpy(out, rs, 64);
+    if (!lt_r(out) || !lt_r(out + 8)) return fail(ZKFL_E_ARG, "r/s must be < r");
+    return ZKFL_OK;
+  }
+  // CSPRNG, rejection-sample below r (snarkjs: Fr.random())
+  for (int k = 0; k < 2; k++) {
+    for (int tries = 0;; tries++) {
+      uint8_t b[32];
+      if (getrandom(b, 32, 0) != 32) return fail(ZKFL_E_DEVICE, "getrandom failed");
+      b[31] &= 0x3f;  // < 2^254
+      memcpy(out + 8 * k, b, 32);
+      if (lt_r(out + 8 * k)) break;
+      if (tries > 64) return fail(ZKFL_E_DEVICE, "rng");
+    }
+  }
+  return ZKFL_OK;
+}
+
+// Proof core on a device-resident witness.  plain = 1: no alpha/beta/delta/r/s terms
+// (parity hook); the proof is then not assembled.
+int prove_core(zkfl_ctx* ctx, zkfl_key* k, const Fr* d_w, const uint32_t rs_host[16], int plain) {
+  hipStream_t st = ctx->st;
+  Profiler* prof = &ctx->prof;
+  const size_t nV = k->nVars, n = k->n;
+  memcpy(k->h_pinned + 256, rs_host, 64);  // pinned staging (the stream is drained per proof)
+  HIP_TRY(hipMemcpyAsync(k->d_rs, k->h_pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
+  HIP_TRY(hipMemcpyAsync(k->wA, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wA");
+  HIP_TRY(hipMemcpyAsync(k->wB, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wB");
+  if (k->nC) HIP_TRY(hipMemcpyAsync(k->wC, d_w + k->nPub + 1, k->nC * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wC");
+  hipLaunchKernelGGL(k_set_rs, dim3(1), dim3(1), 0, st, k->d_rs, k->wA, k->wB, k->wC, nV, k->nC, plain);
+  int pi = prof->begin("abc", st);
+  hipLaunchKernelGGL(k_abc, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rowA, k->rowB, k->cols, k->coefs, d_w, n,
+                     k->abc);
+  prof->end(pi, st, (double)k->K);
+  pi = prof->begin("ntt", st);
+  HIP_TRY(ntt_coset_shift(k->ntt, k->abc, 3, n, st), "ntt");
+  prof->end(pi, st, 3.0 * (double)n);
+  hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->abc, n, k->h);
+  HIP_TRY(msm_run_g1(k->pH, (const uint32_t*)k->h, k->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
+  HIP_TRY(msm_run_g1(k->pA, (const uint32_t*)k->wA, k->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
+  HIP_TRY(msm_run_g1(k->pB1, (const uint32_t*)k->wB, k->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(msm_run_g2(k->pB2, (const uint32_t*)k->wB, k->resB2, st, prof, "msm_accumulate_g2"), "msm B2");
+  HIP_TRY(msm_run_g1(k->pC, (const uint32_t*)k->wC, k->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
+  if (!plain) hipLaunchKernelGGL(k_assemble, dim3(1), dim3(1), 0, st, k->res, k->resB2, k->d_rs, k->d_proof);
+  HIP_TRY(hipGetLastError(), "launch");
+  return ZKFL_OK;
+}
+
+int fetch_proof(zkfl_ctx* ctx, zkfl_key* k, uint8_t proof_out[256]) {
+  HIP_TRY(hipMemcpyAsync(k->h_pinned, k->d_proof, 256, hipMemcpyDeviceToHost, ctx->st), "download proof");
+  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
+  memcpy(proof_out, k->h_pinned, 256);
+  return ZKFL_OK;
+}
+
+hipError_t msm_alloc_any(MsmPlan<FqOps>& pl, size_t n, hipStream_t st) { return msm_alloc_g1(pl, n, st); }
+hipError_t msm_alloc_any(MsmPlan<Fq2Ops>& pl, size_t n, hipStream_t st) { return msm_alloc_g2(pl, n, st); }
+void msm_free_any(MsmPlan<FqOps>& pl) { msm_free_g1(pl); }
+void msm_free_any(MsmPlan<Fq2Ops>& pl) { msm_free_g2(pl); }
+hipError_t msm_set_bases_any(MsmPlan<FqOps>& pl, const G1Aff* b, hipStream_t st) { return msm_set_bases_g1(pl, b, st); }
+hipError_t msm_set_bases_any(MsmPlan<Fq2Ops>& pl, const G2Aff* b, hipStream_t st) { return msm_set_bases_g2(pl, b, st); }
+hipError_t msm_run_any(MsmPlan<FqOps>& pl, const uint32_t* s, G1P* o, hipStream_t st, Profiler* p) {
+  return msm_run_g1(pl, s, o, st, p, "msm_accumulate_g1");
+}
+hipError_t msm_run_any(MsmPlan<Fq2Ops>& pl, const uint32_t* s, G2P* o, hipStream_t st, Profiler* p) {
+  return msm_run_g2(pl, s, o, st, p, "msm_accumulate_g2");
+}
+
+template <class F>
+int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out) {
+  if (!ctx || !bases || !scalars || !out || n == 0) return fail(ZKFL_E_ARG, "msm: bad args");
+  hipStream_t st = ctx->st;
+  MsmPlan<F> pl;
+  Affine<F>* d_b = nullptr;
+  uint32_t* d_s = nullptr;
+  XYZZ<F>* d_r = nullptr;
+  uint32_t* d_o = nullptr;
+  int rc = ZKFL_OK;
+  hipError_t e = msm_alloc_any(pl, n, st);
+  if (e == hipSuccess) e = hipMalloc(&d_b, n * sizeof(Affine<F>));
+  if (e == hipSuccess) e = hipMalloc(&d_s, n * 32);
+  if (e == hipSuccess) e = hipMalloc(&d_r, sizeof(XYZZ<F>));
+  if (e == hipSuccess) e = hipMalloc(&d_o, sizeof(Affine<F>));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_b, bases, n * sizeof(Affine<F>), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = msm_set_bases_any(pl, d_b, st);
+  if (e == hipSuccess) e = msm_run_any(pl, d_s, d_r, st, &ctx->prof);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_point_out<F>, dim3(1), dim3(1), 0, st, d_r, 1, d_o);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_o, sizeof(Affine<F>), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) rc = hip_fail(e, "msm primitive");
+  msm_free_any(pl);
+  for (void* p : {(void*)d_b, (void*)d_s, (void*)d_r, (void*)d_o})
+    if (p) (void)hipFree(p);
+  return rc;
+}
+
+template <class F>
+int run_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out, bool g2) {
+  if (!ctx || !scalars || !out) return fail(ZKFL_E_ARG, "gen_mul: bad args");
+  if (n == 0) return ZKFL_OK;
+  hipStream_t st = ctx->st;
+  uint32_t* d_s = nullptr;
+  Affine<F>* d_o = nullptr;
+  Affine<F>* d_g = nullptr;
+  int rc = ZKFL_OK;
+  hipError_t e = hipMalloc(&d_s, n * 32);
+  if (e == hipSuccess) e = hipMalloc(&d_o, n * sizeof(Affine<F>));
+  if (e == hipSuccess) e = hipMalloc(&d_g, sizeof(Affine<F>));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    if (g2)
+      hipLaunchKernelGGL(k_g2_gen_mont, dim3(1), dim3(1), 0, st, (G2Aff*)d_g);
+    else
+      hipLaunchKernelGGL(k_g1_gen_mont, dim3(1), dim3(1), 0, st, (G1Aff*)d_g);
+    e = hipGetLastError();
+  }
+  Affine<F> g;
+  if (e == hipSuccess) e = hipMemcpyAsync(&g, d_g, sizeof(g), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_gen_mul<F>, dim3(zk_grid(n, 64)), dim3(64), 0, st, d_s, n, g, d_o);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_o, n * sizeof(Affine<F>), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) rc = hip_fail(e, "gen_mul");
+  for (void* p : {(void*)d_s, (void*)d_o, (void*)d_g})
+    if (p) (void)hipFree(p);
+  return rc;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int zkfl_version(void) { return 1; }
+
+const char* zkfl_last_error(void) { return g_err.c_str(); }
+
+int zkfl_device_count(int* count) {
+  if (!count) return fail(ZKFL_E_ARG, "null");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = c;
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_create(int device, zkfl_ctx** out) {
+  if (!out) return fail(ZKFL_E_ARG, "null out");
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || c == 0) return fail(ZKFL_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= c) return fail(ZKFL_E_ARG, "device index out of range");
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  zkfl_ctx* ctx = new zkfl_ctx();
+  ctx->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  *out = ctx;
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_destroy(zkfl_ctx* ctx) {
+  if (!ctx) return ZKFL_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->st);
+  ctx->prof.reset();
+  (void)hipStreamDestroy(ctx->st);
+  delete ctx;
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_set_profiling(zkfl_ctx* ctx, int enabled) {
+  if (!ctx) return fail(ZKFL_E_ARG, "null ctx");
+  ctx->prof.on = enabled != 0;
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units) {
+  if (!ctx || !name || !total_ms || !launches) return fail(ZKFL_E_ARG, "null");
+  (void)hipSetDevice(ctx->device);
+  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
+  ctx->prof.query(name, total_ms, launches, units);
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_profile_reset(zkfl_ctx* ctx) {
+  if (!ctx) return fail(ZKFL_E_ARG, "null ctx");
+  (void)hipStreamSynchronize(ctx->st);
+  ctx->prof.reset();
+  return ZKFL_OK;
+}
+
+int zkfl_ctx_synchronize(zkfl_ctx* ctx) {
+  if (!ctx) return fail(ZKFL_E_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
+  return ZKFL_OK;
+}
+
+int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out) {
+  if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
+  std::vector<Section> s;
+  int rc = read_binfile(buf, len, "zkey", s);
+  if (rc) return rc;
+  for (int i = 1; i <= 9; i++)
+    if (!s[i].present) return fail(ZKFL_E_FORMAT, "zkey: missing section " + std::to_string(i));
+  uint32_t proto;
+  memcpy(&proto, buf + s[1].off, 4);
+  if (proto != 1) return fail(ZKFL_E_FORMAT, "zkey: not a groth16 key");
+  const uint8_t* h = buf + s[2].off;
+  uint32_t n8q, n8r;
+  memcpy(&n8q, h, 4);
+  if (n8q != 32 || memcmp(h + 4, Q_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "zkey: q is not bn128");
+  memcpy(&n8r, h + 36, 4);
+  if (n8r != 32 || memcmp(h + 40, R_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "zkey: r is not bn128");
+  uint32_t nVars, nPub, dom;
+  memcpy(&nVars, h + 72, 4);
+  memcpy(&nPub, h + 76, 4);
+  memcpy(&dom, h + 80, 4);
+  const uint8_t* pts = h + 84;  // alpha1 64, beta1 64, beta2 128, gamma2 128, delta1 64, delta2 128
+  if (s[2].size < 84 + 64 * 3 + 128 * 3) return fail(ZKFL_E_FORMAT, "zkey: header size");
+  int logn = 0;
+  while ((1u << logn) < dom) logn++;
+  if ((1u << logn) != dom || logn > 28 || dom < 2) return fail(ZKFL_E_FORMAT, "zkey: domain size");
+  if (nVars < nPub + 1) return fail(ZKFL_E_FORMAT, "zkey: nVars < nPublic+1");
+  const size_t nC = nVars - nPub - 1;
+  if (s[3].size != (size_t)(nPub + 1) * 64 || s[5].size != (size_t)nVars * 64 || s[6].size != (size_t)nVars * 64 ||
+      s[7].size != (size_t)nVars * 128 || s[8].size != nC * 64 || s[9].size != (size_t)dom * 64)
+    return fail(ZKFL_E_MISMATCH, "zkey: section sizes do not match header");
+  // coefficients -> CSR
+  const uint8_t* cs = buf + s[4].off;
+  uint32_t ncoef;
+  memcpy(&ncoef, cs, 4);
+  if (s[4].size != 4 + (size_t)ncoef * 44) return fail(ZKFL_E_FORMAT, "zkey: coefficient section size");
+  std::vector<uint32_t> rowptr(2 * ((size_t)dom + 1), 0);
+  for (uint32_t i = 0; i < ncoef; i++) {
+    uint32_t mcs[3];
+    memcpy(mcs, cs + 4 + (size_t)i * 44, 12);
+    if (mcs[0] > 1 || mcs[1] >= dom || mcs[2] >= nVars) return fail(ZKFL_E_FORMAT, "zkey: coefficient out of range");
+    rowptr[mcs[0] * ((size_t)dom + 1) + mcs[1] + 1]++;
+  }
+  for (int m = 0; m < 2; m++) {
+    uint32_t* rp = rowptr.data() + m * ((size_t)dom + 1);
+    for (size_t j = 0; j < dom; j++) rp[j + 1] += rp[j];
+  }
+  // B rows are stored after A rows in one array: offset B by nnz(A)
+  const uint32_t nA = rowptr[dom];
+  for (size_t j = 0; j <= dom; j++) rowptr[dom + 1 + j] += nA;
+  std::vector<uint32_t> fill(rowptr.begin(), rowptr.end());
+  std::vector<uint32_t> cols(ncoef);
+  std::vector<uint32_t> coefs((size_t)ncoef * 8);
+  for (uint32_t i = 0; i < ncoef; i++) {
+    const uint8_t* e = cs + 4 + (size_t)i * 44;
+    uint32_t mcs[3];
+    memcpy(mcs, e, 12);
+    uint32_t pos = fill[mcs[0] * ((size_t)dom + 1) + mcs[1]]++;
+    cols[pos] = mcs[2];
+    memcpy(&coefs[(size_t)pos * 8], e + 12, 32);
+  }
+
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->st;
+  zkfl_key* k = new zkfl_key();
+  k->ctx = ctx;
+  k->nVars = nVars;
+  k->nPub = nPub;
+  k->n = dom;
+  k->logn = logn;
+  k->nC = nC;
+  k->K = ncoef;
+  auto cleanup = [&](int code) {
+    key_release(k);
+    return code;
+  };
+#define KTRY(x, where)                                  \
+  do {                                                  \
+    hipError_t _e = (x);                                \
+    if (_e != hipSuccess) return cleanup(hip_fail(_e, where)); \
+  } while (0)
+  KTRY(hipMalloc(&k->rowA, ((size_t)dom + 1) * 4), "alloc rows");
+  KTRY(hipMalloc(&k->rowB, ((size_t)dom + 1) * 4), "alloc rows");
+  KTRY(hipMalloc(&k->cols, (size_t)(ncoef ? ncoef : 1) * 4), "alloc cols");
+  KTRY(hipMalloc(&k->coefs, (size_t)(ncoef ? ncoef : 1) * 32), "alloc coefs");
+  KTRY(hipMemcpyAsync(k->rowA, rowptr.data(), ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st), "upload");
+  KTRY(hipMemcpyAsync(k->rowB, rowptr.data() + dom + 1, ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st), "upload");
+  if (ncoef) {
+    KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
+    KTRY(hipMemcpyAsync(k->coefs, coefs.data(), (size_t)ncoef * 32, hipMemcpyHostToDevice, st), "upload");
+  }
+  // MSM plans with augmented bases
+  KTRY(msm_alloc_g1(k->pA, (size_t)nVars + 2, st), "plan A");
+  KTRY(msm_alloc_g1(k->pB1, (size_t)nVars + 2, st), "plan B1");
+  KTRY(msm_alloc_g2(k->pB2, (size_t)nVars + 2, st), "plan B2");
+  KTRY(msm_alloc_g1(k->pC, nC + 1, st), "plan C");
+  KTRY(msm_alloc_g1(k->pH, dom, st), "plan H");
+  {
+    const uint8_t* alpha1 = pts;
+    const uint8_t* beta1 = pts + 64;
+    const uint8_t* beta2 = pts + 128;
+    const uint8_t* delta1 = pts + 384;
+    const uint8_t* delta2 = pts + 448;
+    size_t maxb = ((size_t)nVars + 2) * 128;
+    if ((size_t)dom * 64 > maxb) maxb = (size_t)dom * 64;
+    uint8_t* d_tmp = nullptr;
+    KTRY(hipMalloc(&d_tmp, maxb), "alloc tmp");
+    auto upload_g1 = [&](MsmPlan<FqOps>& pl, const uint8_t* sec, size_t cnt, const uint8_t* x0,
+                         const uint8_t* x1) -> hipError_t {
+      hipError_t e = hipMemcpyAsync(d_tmp, sec, cnt * 64, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess && x0) e = hipMemcpyAsync(d_tmp + cnt * 64, x0, 64, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess && x1) e = hipMemcpyAsync(d_tmp + (cnt + 1) * 64, x1, 64, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = msm_set_bases_g1(pl, (const G1Aff*)d_tmp, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      return e;
+    };
+    hipError_t e = upload_g1(k->pA, buf + s[5].off, nVars, alpha1, delta1);
+    if (e == hipSuccess) e = upload_g1(k->pB1, buf + s[6].off, nVars, beta1, delta1);
+    if (e == hipSuccess) e = upload_g1(k->pC, buf + s[8].off, nC, delta1, nullptr);
+    if (e == hipSuccess) e = upload_g1(k->pH, buf + s[9].off, dom, nullptr, nullptr);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp, buf + s[7].off, (size_t)nVars * 128, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + (size_t)nVars * 128, beta2, 128, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + ((size_t)nVars + 1) * 128, delta2, 128, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = msm_set_bases_g2(k->pB2, (const G2Aff*)d_tmp, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d_tmp);
+    if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
+  }
+  KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
+  KTRY(hipMalloc(&k->wA, ((size_t)nVars + 2) * 32), "alloc");
+  KTRY(hipMalloc(&k->wB, ((size_t)nVars + 2) * 32), "alloc");
+  KTRY(hipMalloc(&k->wC, (nC + 1) * 32), "alloc");
+  KTRY(hipMalloc(&k->abc, (size_t)dom * 3 * 32), "alloc");
+  KTRY(hipMalloc(&k->h, (size_t)dom * 32), "alloc");
+  KTRY(hipMalloc(&k->res, 4 * sizeof(G1P)), "alloc");
+  KTRY(hipMalloc(&k->resB2, sizeof(G2P)), "alloc");
+  KTRY(hipMalloc(&k->d_rs, 2 * 32), "alloc");
+  KTRY(hipMalloc(&k->d_proof, 256), "alloc");
+  KTRY(hipHostMalloc(&k->h_pinned, 512), "alloc pinned");
+  KTRY(hipStreamSynchronize(st), "sync");
+#undef KTRY
+  *out = k;
+  return ZKFL_OK;
+}
+
+int zkfl_key_free(zkfl_key* key) {
+  if (!key) return ZKFL_OK;
+  (void)hipSetDevice(key->ctx->device);
+  (void)hipStreamSynchronize(key->ctx->st);
+  key_release(key);
+  return ZKFL_OK;
+}
+
+int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size) {
+  if (!key) return fail(ZKFL_E_ARG, "null key");
+  if (n_vars) *n_vars = key->nVars;
+  if (n_public) *n_public = key->nPub;
+  if (domain_size) *domain_size = key->n;
+  return ZKFL_OK;
+}
+
+int zkfl_witness_upload(zkfl_ctx* ctx, const zkfl_key* key, const uint8_t* wtns, size_t wtns_len,
+                        zkfl_witness** out) {
+  if (!ctx || !key || !wtns || !out) return fail(ZKFL_E_ARG, "null argument");
+  WtnsView v;
+  int rc = parse_wtns(wtns, wtns_len, v);
+  if (rc) return rc;
+  if (v.n != key->nVars) return fail(ZKFL_E_MISMATCH, "wtns: nWitness != zkey nVars");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  zkfl_witness* w = new zkfl_witness();
+  w->key = key;
+  hipError_t e = hipMalloc(&w->d, (size_t)v.n * 32);
+  if (e == hipSuccess) e = hipMemcpyAsync(w->d, v.data, (size_t)v.n * 32, hipMemcpyHostToDevice, ctx->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->st);
+  if (e != hipSuccess) {
+    if (w->d) (void)hipFree(w->d);
+    delete w;
+    return hip_fail(e, "witness upload");
+  }
+  w->pub.assign(v.data + 32, v.data + 32 + (size_t)key->nPub * 32);
+  *out = w;
+  return ZKFL_OK;
+}
+
+int zkfl_witness_free(zkfl_witness* w) {
+  if (!w) return ZKFL_OK;
+  if (w->d) (void)hipFree(w->d);
+  delete w;
+  return ZKFL_OK;
+}
+
+int zkfl_groth16_prove_resident(zkfl_ctx* ctx, zkfl_key* key, const zkfl_witness* w, const uint8_t* rs,
+                                uint8_t proof_out[256]) {
+  if (!ctx || !key || !w || !proof_out) return fail(ZKFL_E_ARG, "null argument");
+  if (w->key != key) return fail(ZKFL_E_MISMATCH, "witness uploaded for another key");
+  uint32_t rsl[16];
+  int rc = get_rs(rs, rsl);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  int pi = ctx->prof.begin("prove", ctx->st);
+  rc = prove_core(ctx, key, w->d, rsl, 0);
+  ctx->prof.end(pi, ctx->st, 1.0);
+  if (rc) return rc;
+  return fetch_proof(ctx, key, proof_out);
+}
+
+int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
+                             const uint8_t* rs, uint8_t* proofs_out) {
+  if (!ctx || !key || (!w && n) || (!proofs_out && n)) return fail(ZKFL_E_ARG, "null argument");
+  for (size_t i = 0; i < n; i++) {
+    int rc = zkfl_groth16_prove_resident(ctx, key, w[i], rs ? rs + 64 * i : nullptr, proofs_out + 256 * i);
+    if (rc) return rc;
+  }
+  return ZKFL_OK;
+}
+
+int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, const uint8_t* rs,
+                       uint8_t proof_out[256], uint8_t* pub_out, size_t* npub) {
+  zkfl_witness* w = nullptr;
+  int rc = zkfl_witness_upload(ctx, key, wtns, wtns_len, &w);
+  if (rc) return rc;
+  rc = zkfl_groth16_prove_resident(ctx, key, w, rs, proof_out);
+  if (rc == ZKFL_OK) {
+    if (pub_out) memcpy(pub_out, w->pub.data(), w->pub.size());
+    if (npub) *npub = key->nPub;
+  }
+  zkfl_witness_free(w);
+  return rc;
+}
+
+int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, uint8_t* h_out,
+                           uint8_t* msm_out) {
+  zkfl_witness* w = nullptr;
+  int rc = zkfl_witness_upload(ctx, key, wtns, wtns_len, &w);
+  if (rc) return rc;
+  uint32_t zeros[16] = {0};
+  rc = prove_core(ctx, key, w->d, zeros, 1);
+  hipStream_t st = ctx->st;
+  uint32_t* d_o = nullptr;
+  if (rc == ZKFL_OK && msm_out) {
+    hipError_t e = hipMalloc(&d_o, 64 * 4 + 128);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_point_out<FqOps>, dim3(1), dim3(4), 0, st, key->res, 4, d_o);
+      hipLaunchKernelGGL(k_point_out<Fq2Ops>, dim3(1), dim3(1), 0, st, key->resB2, 1, d_o + 64);
+      e = hipGetLastError();
+    }
+    std::vector<uint8_t> tmp(64 * 4 + 128);
+    if (e == hipSuccess) e = hipMemcpyAsync(tmp.data(), d_o, tmp.size(), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = hip_fail(e, "debug parts");
+    if (rc == ZKFL_OK) {
+      // res order A, B1, C, H ; output order A | B1 | B2 | C | H
+      memcpy(msm_out, tmp.data(), 64);
+      memcpy(msm_out + 64, tmp.data() + 64, 64);
+      memcpy(msm_out + 128, tmp.data() + 256, 128);
+      memcpy(msm_out + 256, tmp.data() + 128, 64);
+      memcpy(msm_out + 320, tmp.data() + 192, 64);
+    }
+  }
+  if (rc == ZKFL_OK && h_out) {
+    hipError_t e = hipMemcpyAsync(h_out, key->h, (size_t)key->n * 32, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = hip_fail(e, "debug h");
+  }
+  if (d_o) (void)hipFree(d_o);
+  zkfl_witness_free(w);
+  return rc;
+}
+
+int zkfl_msm_g1(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[64]) {
+  return run_msm_primitive<FqOps>(ctx, bases, scalars, n, out);
+}
+
+int zkfl_msm_g2(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[128]) {
+  return run_msm_primitive<Fq2Ops>(ctx, bases, scalars, n, out);
+}
+
+int zkfl_ntt_coset(zkfl_ctx* ctx, uint8_t* data, uint32_t logn) {
+  if (!ctx || !data || logn < 1 || logn > 27) return fail(ZKFL_E_ARG, "ntt: bad args");
+  hipStream_t st = ctx->st;
+  NttPlan pl;
+  Fr* d = nullptr;
+  const size_t n = (size_t)1 << logn;
+  int rc = ZKFL_OK;
+  hipError_t e = ntt_plan_alloc(pl, (int)logn, st);
+  if (e == hipSuccess) e = hipMalloc(&d, n * 32);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, data, n * 32, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_fr_std_to_mont, dim3(zk_grid(n, 256)), dim3(256), 0, st, d, n);
+    e = ntt_coset_shift(pl, d, 1, n, st);
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_fr_mont_to_std, dim3(zk_grid(n, 256)), dim3(256), 0, st, d, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(data, d, n * 32, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) rc = hip_fail(e, "ntt");
+  ntt_plan_free(pl);
+  if (d) (void)hipFree(d);
+  return rc;
+}
+
+int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out) {
+  return run_gen_mul<FqOps>(ctx, scalars, n, out, false);
+}
+
+int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out) {
+  return run_gen_mul<Fq2Ops>(ctx, scalars, n, out, true);
+}
+
+}  // extern "C"

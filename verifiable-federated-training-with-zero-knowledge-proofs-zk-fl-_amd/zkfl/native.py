@@ -1,0 +1,237 @@
+"""ctypes binding of libzkfl.so (the C ABI declared in include/zkfl.h).
+
+This is the Python twin of the N-API binding shown in INTEGRATION.md.  The library is built
+in-tree (``make`` in the package directory, or ``__graft_entry__.build()``); if it is missing
+every call raises ``ZkflError`` — there is no CPU fallback on the proving path.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_DIR, "libzkfl.so")
+
+ZKFL_OK = 0
+ERRORS = {
+    -1: "ZKFL_E_ARG", -2: "ZKFL_E_FORMAT", -3: "ZKFL_E_PRIME", -4: "ZKFL_E_MISMATCH",
+    -5: "ZKFL_E_DEVICE", -6: "ZKFL_E_OOM", -7: "ZKFL_E_CONSTRAINT",
+}
+
+# every exported symbol of include/zkfl.h with (restype, argtypes)
+_P = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+SIGNATURES = {
+    "zkfl_version": (C.c_int, []),
+    "zkfl_last_error": (C.c_char_p, []),
+    "zkfl_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "zkfl_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "zkfl_ctx_destroy": (C.c_int, [_P]),
+    "zkfl_ctx_set_profiling": (C.c_int, [_P, C.c_int]),
+    "zkfl_ctx_profile": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_double)]),
+    "zkfl_ctx_profile_reset": (C.c_int, [_P]),
+    "zkfl_ctx_synchronize": (C.c_int, [_P]),
+    "zkfl_zkey_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "zkfl_key_free": (C.c_int, [_P]),
+    "zkfl_key_info": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "zkfl_groth16_prove": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, C.c_char_p, _U8P, _U8P,
+                                     C.POINTER(C.c_size_t)]),
+    "zkfl_witness_upload": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "zkfl_witness_free": (C.c_int, [_P]),
+    "zkfl_groth16_prove_resident": (C.c_int, [_P, _P, _P, C.c_char_p, _U8P]),
+    "zkfl_groth16_prove_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
+    "zkfl_debug_prove_parts": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, _U8P, _U8P]),
+    "zkfl_msm_g1": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_msm_g2": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_ntt_coset": (C.c_int, [_P, _U8P, C.c_uint32]),
+    "zkfl_setup_g1_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_setup_g2_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
+}
+
+
+class ZkflError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ZkflError(-5, f"{LIB_PATH} not built (run make in the package dir / __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != ZKFL_OK:
+        raise ZkflError(rc, lib().zkfl_last_error().decode(errors="replace"))
+
+
+def _buf(n):
+    return (C.c_uint8 * n)()
+
+
+class Context:
+    """One device, one HIP stream (one process per GPU for multi-GPU)."""
+
+    def __init__(self, device: int = 0):
+        h = _P()
+        check(lib().zkfl_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().zkfl_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # profiling (bench.py roofline)
+    def set_profiling(self, on: bool):
+        check(lib().zkfl_ctx_set_profiling(self.h, 1 if on else 0))
+
+    def profile(self, name: str):
+        ms, n, u = C.c_double(), C.c_uint64(), C.c_double()
+        check(lib().zkfl_ctx_profile(self.h, name.encode(), C.byref(ms), C.byref(n), C.byref(u)))
+        return ms.value, n.value, u.value
+
+    def profile_reset(self):
+        check(lib().zkfl_ctx_profile_reset(self.h))
+
+    def synchronize(self):
+        check(lib().zkfl_ctx_synchronize(self.h))
+
+    # primitives
+    def msm_g1(self, bases: bytes, scalars: bytes) -> bytes:
+        n = len(scalars) // 32
+        assert len(bases) == 64 * n
+        out = _buf(64)
+        check(lib().zkfl_msm_g1(self.h, bases, scalars, n, out))
+        return bytes(out)
+
+    def msm_g2(self, bases: bytes, scalars: bytes) -> bytes:
+        n = len(scalars) // 32
+        assert len(bases) == 128 * n
+        out = _buf(128)
+        check(lib().zkfl_msm_g2(self.h, bases, scalars, n, out))
+        return bytes(out)
+
+    def ntt_coset(self, data: bytes) -> bytes:
+        n = len(data) // 32
+        logn = n.bit_length() - 1
+        assert 1 << logn == n
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+        check(lib().zkfl_ntt_coset(self.h, buf, logn))
+        return bytes(buf)
+
+    def g1_gen_mul(self, scalars: bytes) -> bytes:
+        n = len(scalars) // 32
+        out = _buf(64 * n if n else 1)
+        check(lib().zkfl_setup_g1_gen_mul(self.h, scalars, n, out))
+        return bytes(out)[:64 * n]
+
+    def g2_gen_mul(self, scalars: bytes) -> bytes:
+        n = len(scalars) // 32
+        out = _buf(128 * n if n else 1)
+        check(lib().zkfl_setup_g2_gen_mul(self.h, scalars, n, out))
+        return bytes(out)[:128 * n]
+
+
+class ProvingKey:
+    """A .zkey made device-resident (bases expanded per MSM window)."""
+
+    def __init__(self, ctx: Context, zkey: bytes):
+        h = _P()
+        check(lib().zkfl_zkey_load(ctx.h, zkey, len(zkey), C.byref(h)))
+        self.h = h
+        self.ctx = ctx
+        nv, npub, dom = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().zkfl_key_info(h, C.byref(nv), C.byref(npub), C.byref(dom)))
+        self.n_vars, self.n_public, self.domain_size = nv.value, npub.value, dom.value
+
+    def close(self):
+        if self.h:
+            lib().zkfl_key_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prove(self, wtns: bytes, rs: bytes | None = None):
+        """-> (proof 256 B, [public signal ints])"""
+        proof = _buf(256)
+        pub = _buf(32 * max(1, self.n_public))
+        npub = C.c_size_t()
+        check(lib().zkfl_groth16_prove(self.ctx.h, self.h, wtns, len(wtns), rs, proof, pub, C.byref(npub)))
+        pb = bytes(pub)
+        return bytes(proof), [int.from_bytes(pb[32 * i:32 * i + 32], "little") for i in range(npub.value)]
+
+    def upload(self, wtns: bytes) -> "ResidentWitness":
+        return ResidentWitness(self, wtns)
+
+    def prove_resident(self, w: "ResidentWitness", rs: bytes | None = None) -> bytes:
+        proof = _buf(256)
+        check(lib().zkfl_groth16_prove_resident(self.ctx.h, self.h, w.h, rs, proof))
+        return bytes(proof)
+
+    def prove_batch(self, ws, rs: bytes | None = None) -> list:
+        n = len(ws)
+        arr = (_P * n)(*[w.h for w in ws])
+        out = _buf(256 * n)
+        check(lib().zkfl_groth16_prove_batch(self.ctx.h, self.h, n, arr, rs, out))
+        ob = bytes(out)
+        return [ob[256 * i:256 * i + 256] for i in range(n)]
+
+    def debug_parts(self, wtns: bytes):
+        """-> (h list of ints, dict of MSM results as std affine bytes)"""
+        h = _buf(32 * self.domain_size)
+        m = _buf(384)
+        check(lib().zkfl_debug_prove_parts(self.ctx.h, self.h, wtns, len(wtns), h, m))
+        hb, mb = bytes(h), bytes(m)
+        hs = [int.from_bytes(hb[32 * i:32 * i + 32], "little") for i in range(self.domain_size)]
+        parts = dict(A=mb[0:64], B1=mb[64:128], B2=mb[128:256], C=mb[256:320], H=mb[320:384])
+        return hs, parts
+
+
+class ResidentWitness:
+    def __init__(self, key: ProvingKey, wtns: bytes):
+        h = _P()
+        check(lib().zkfl_witness_upload(key.ctx.h, key.h, wtns, len(wtns), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().zkfl_witness_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
