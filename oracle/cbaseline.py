@@ -1,0 +1,65 @@
+"""ctypes wrapper of the C oracle (oracle/c/groth16_ref.c) — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ as the M-scale checker and by bench.py's cpu_baseline leg (kind "port")."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+
+_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libgroth16_ref.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            raise RuntimeError(f"{_LIB} not built (make -C oracle)")
+        L = C.CDLL(_LIB)
+        L.ref_prove.restype = C.c_int
+        L.ref_prove.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p,
+                                C.POINTER(C.c_uint8), C.c_int]
+        L.ref_msm_g1.restype = C.c_int
+        L.ref_msm_g1.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint8), C.c_int]
+        _lib = L
+    return _lib
+
+
+def prove(zkey: bytes, wtns: bytes, rs: bytes, threads: int = 0) -> bytes:
+    out = (C.c_uint8 * 256)()
+    rc = lib().ref_prove(zkey, len(zkey), wtns, len(wtns), rs, out, threads)
+    if rc:
+        raise RuntimeError(f"ref_prove failed: {rc}")
+    return bytes(out)
+
+
+def msm_g1(bases: bytes, scalars: bytes, threads: int = 0) -> bytes:
+    out = (C.c_uint8 * 64)()
+    lib().ref_msm_g1(bases, scalars, len(scalars) // 32, out, threads)
+    return bytes(out)
+
+
+def default_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def time_prove(zkey: bytes, wtns: bytes, seconds_budget: float = 20.0) -> dict:
+    """cpu_baseline leg: full proofs of the same zkey/wtns on the host until ~budget."""
+    threads = default_threads()
+    rs = (12345).to_bytes(32, "little") + (67890).to_bytes(32, "little")
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        prove(zkey, wtns, rs, threads)
+        k += 1
+        dt = time.perf_counter() - t0
+        if dt * (k + 1) / k > seconds_budget or k >= 5:
+            break
+    return {"value": round(k / dt, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
+            "sample": f"{k} full proof(s) of the same zkey/wtns by the C oracle "
+                      f"(oracle/c/groth16_ref.c, OpenMP {threads} threads) in {dt:.1f} s"}
