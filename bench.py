@@ -40,31 +40,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline_leg(builder, inp, seconds_budget=20.0):
-    """Oracle ("port") on the host: the C restatement if built, else the Python one, timed on
-    a bounded sample of the same workload and scaled to proofs/s."""
+def cpu_baseline_leg(zk: bytes, wt: bytes, seconds_budget=20.0):
+    """Oracle ("port") on the host cores: the C restatement (oracle/c/groth16_ref.c) proving
+    the same zkey/wtns, bounded to ~seconds_budget, reported as proofs/s."""
     sys.path.insert(0, ROOT)
-    try:
-        from oracle import cbaseline  # C oracle (built by oracle/Makefile)
-        return cbaseline.time_prove(builder, inp, seconds_budget)
-    except Exception as e:  # noqa: BLE001
-        log(f"[bench] C oracle unavailable ({e}); using the Python oracle sample")
-    from oracle import bn254 as bn
-    # sample: a 1024-point G1 MSM of the same kind as the proof's (random bases/scalars);
-    # one proof ~ (3*nVars + domain) G1 + nVars G2 (x3 cost) point-entries.
-    import random
-    rnd = random.Random(1)
-    pts = [bn.mul(bn.G1_GEN, rnd.randrange(bn.R)) for _ in range(256)] * 4
-    ss = [rnd.randrange(bn.R) for _ in range(1024)]
-    t0 = time.perf_counter()
-    bn.msm(pts, ss)
-    dt = time.perf_counter() - t0
-    n = 1 << max(1, (builder.n_constraints + builder.n_public).bit_length())
-    work = 3 * builder.n_wires + n + 3 * builder.n_wires
-    per_proof = dt * work / 1024
-    return {"value": 1.0 / per_proof, "unit": "proofs/s", "cores": 1, "kind": "port",
-            "sample": f"python oracle Pippenger G1 MSM of 1024 points ({dt:.2f} s), scaled by "
-                      f"{work} G1-equivalent MSM points per proof (MSMs only; NTT/ABC excluded)"}
+    from oracle import cbaseline
+    return cbaseline.time_prove(zk, wt, seconds_budget)
 
 
 def main():
@@ -74,6 +55,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--slots", type=int, default=3, help="proofs in flight per GPU (HIP stream sets)")
+    ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -95,11 +78,13 @@ def main():
     t0 = time.perf_counter()
     b = circuits.build(name, *params)
     batch, dim, depth, precision = params
-    client = clients.Client(rank + 1, batch, dim, depth, clients.JsLcg(12345))
-    inp, _ = client.training_input(batch, precision, 100000000)
-    w = b.witness(inp)
-    log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires "
-        f"({time.perf_counter() - t0:.1f} s)")
+    inputs = []
+    for c in range(args.clients):
+        client = clients.Client(rank * args.clients + c + 1, batch, dim, depth, clients.JsLcg(12345 + c))
+        inputs.append(client.training_input(batch, precision, 100000000)[0])
+    wits = [b.witness(inp) for inp in inputs]
+    log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires, "
+        f"{len(wits)} client witnesses ({time.perf_counter() - t0:.1f} s)")
 
     ctx = native.Context(local_rank)
     t0 = time.perf_counter()
@@ -107,9 +92,13 @@ def main():
     log(f"[bench r{rank}] dev setup {len(zk) / 1e6:.0f} MB zkey ({time.perf_counter() - t0:.1f} s)")
     t0 = time.perf_counter()
     key = native.ProvingKey(ctx, zk)
-    wt = zkey.wtns_bytes(w)
-    res = key.upload(wt)
-    log(f"[bench r{rank}] key load + witness upload ({time.perf_counter() - t0:.1f} s), domain {key.domain_size}")
+    key.set_slots(args.slots)
+    wts = [zkey.wtns_bytes(w) for w in wits]
+    res = [key.upload(wt) for wt in wts]
+    log(f"[bench r{rank}] key load + witness upload ({time.perf_counter() - t0:.1f} s), domain {key.domain_size}, "
+        f"slots {args.slots}")
+    steps_w = [res[i % len(res)] for i in range(args.steps)]
+    warm_w = [res[i % len(res)] for i in range(max(args.warmup, args.slots) if args.warmup else 0)]
 
     def barrier_sync():
         ctx.synchronize()
@@ -119,14 +108,13 @@ def main():
                 torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
-        key.prove_resident(res)
+    if warm_w:
+        key.prove_batch(warm_w)
     ctx.profile_reset()
     ctx.set_profiling(True)
     barrier_sync()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        key.prove_resident(res)
+    proofs = key.prove_batch(steps_w)          # K proofs, `slots` in flight
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     ctx.set_profiling(False)
@@ -156,7 +144,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline_leg(b, inp)
+                cpu = cpu_baseline_leg(zk, wts[0])
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
         out = {
@@ -166,11 +154,13 @@ def main():
             "data": "synthetic (reference harness seeded client generator)",
             "config": {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
                        "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
-                       "global_batch": world, "parallelism": f"replicas{world}"},
+                       "global_batch": world, "parallelism": f"replicas{world}", "slots_in_flight": args.slots},
             "roofline": roofline, "stage_ms_per_proof": stage_ms, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    res.close()
+    assert len(proofs) == args.steps and all(len(p) == 256 for p in proofs)
+    for r_ in res:
+        r_.close()
     key.close()
     ctx.close()
     if dist is not None:

@@ -1,0 +1,46 @@
+"""The C restatement of the oracle agrees with the pure-Python oracle (CPU)."""
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import bn254 as bn
+from oracle import groth16 as og
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def cb():
+    subprocess.run(["make", "-s"], cwd=os.path.join(ROOT, "oracle"), check=True)
+    from oracle import cbaseline
+    return cbaseline
+
+
+def test_c_msm_matches_python(cb):
+    rnd = random.Random(2)
+    pts = [bn.mul(bn.G1_GEN, rnd.randrange(bn.R)) for _ in range(50)] + [None]
+    ss = [rnd.randrange(bn.R) for _ in range(50)] + [5]
+    bases = b"".join(bn.g1_to_bytes_mont(p) for p in pts)
+    out = cb.msm_g1(bases, b"".join(s.to_bytes(32, "little") for s in ss), threads=2)
+    assert bn.g1_from_bytes_std(out) == bn.msm(pts, ss)
+
+
+@pytest.mark.parametrize("circ", [("poseidon_hash2",), ("sgd_verified", 8, 4, 3, 1000)])
+def test_c_prove_matches_python(cb, circ):
+    from oracle_backend import OraclePoints
+    from zkfl import circuits, clients, zkey
+    b = circuits.build(*circ)
+    if circ[0] == "poseidon_hash2":
+        w = b.witness({"left": 3, "right": 4})
+    else:
+        inp, _ = clients.Client(1, 8, 4, 3, clients.JsLcg(12345)).training_input(8, 1000, 100000000)
+        w = b.witness(inp)
+        if os.environ.get("ZKFL_FAST_TESTS"):
+            pytest.skip("slow python setup")
+    zk = zkey.groth16_setup(b, OraclePoints(), zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
+    rs = (777).to_bytes(32, "little") + (888).to_bytes(32, "little")
+    got = cb.prove(zk, zkey.wtns_bytes(w), rs, threads=4)
+    ref = og.prove(og.parse_zkey(zk), w, r=777, s=888)
+    assert got == og.proof_bytes(ref)

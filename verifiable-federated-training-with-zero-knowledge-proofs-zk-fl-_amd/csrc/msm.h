@@ -202,60 +202,76 @@ __global__ void __launch_bounds__(64) k_msm_sum8(const XYZZ<F>* __restrict__ in,
 // Host-side plan
 // ---------------------------------------------------------------------------
 template <class F>
-hipError_t msm_plan_alloc(MsmPlan<F>& pl, size_t n, hipStream_t st) {
-  pl.n = n;
-  const size_t m = n * MSM_W;
-  ZK_CHECK(hipMalloc(&pl.bases_w, m * sizeof(Affine<F>)));
-  ZK_CHECK(hipMalloc(&pl.keys_in, m * sizeof(uint16_t)));
-  ZK_CHECK(hipMalloc(&pl.keys_out, m * sizeof(uint16_t)));
-  ZK_CHECK(hipMalloc(&pl.vals_in, m * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&pl.vals_out, m * sizeof(uint32_t)));
-  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, pl.sort_tmp_bytes, pl.keys_in, pl.keys_out, pl.vals_in,
-                                     pl.vals_out, m, 0, 16, st));
-  ZK_CHECK(hipMalloc(&pl.sort_tmp, pl.sort_tmp_bytes));
-  ZK_CHECK(rocprim::exclusive_scan(nullptr, pl.scan_tmp_bytes, pl.tcount, pl.toff, 0u,
-                                   (size_t)MSM_NB + 1, rocprim::plus<uint32_t>(), st));
-  ZK_CHECK(hipMalloc(&pl.scan_tmp, pl.scan_tmp_bytes));
-  ZK_CHECK(hipMalloc(&pl.bstart, MSM_NB * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&pl.bend, MSM_NB * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&pl.tcount, (MSM_NB + 1) * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&pl.toff, (MSM_NB + 1) * sizeof(uint32_t)));
-  pl.max_tasks = m / MSM_L + MSM_NB + 1;
-  ZK_CHECK(hipMalloc(&pl.partials, pl.max_tasks * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&pl.buckets, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&pl.red_acc, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&pl.red_run, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&pl.red_tmp, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&pl.nnz, sizeof(uint32_t)));
+hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n) {
+  b.n = n;
+  ZK_CHECK(hipMalloc(&b.bases_w, n * MSM_W * sizeof(Affine<F>)));
   return hipSuccess;
 }
 
 template <class F>
-void msm_plan_free(MsmPlan<F>& pl) {
-  void* ptrs[] = {pl.bases_w, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, pl.sort_tmp, pl.scan_tmp,
-                  pl.bstart, pl.bend, pl.tcount, pl.toff, pl.partials, pl.buckets, pl.red_acc, pl.red_run,
-                  pl.red_tmp, pl.nnz};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-  pl = MsmPlan<F>();
+void msm_bases_free(MsmBases<F>& b) {
+  if (b.bases_w) (void)hipFree(b.bases_w);
+  b = MsmBases<F>();
 }
 
-// Expand n affine bases (device pointer) into the plan's window table.
+// Expand n affine bases (device pointer) into the window table.
 template <class F>
-hipError_t msm_plan_set_bases(MsmPlan<F>& pl, const Affine<F>* d_bases, hipStream_t st) {
-  hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(pl.n, 64)), dim3(64), 0, st, d_bases, pl.n, pl.bases_w);
+hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, hipStream_t st) {
+  hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
   return hipGetLastError();
 }
 
-// Run one MSM: d_scalars = n standard-form scalars (8 x u32 each, device) -> *d_out (device).
 template <class F>
-hipError_t msm_run(MsmPlan<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out, hipStream_t st,
-                   Profiler* prof = nullptr, const char* tag = nullptr) {
-  const size_t m = pl.n * MSM_W;
-  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(pl.n, 256)), dim3(256), 0, st, d_scalars, pl.n, pl.keys_in,
+hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
+  s.cap = cap;
+  const size_t m = cap * MSM_W;
+  ZK_CHECK(hipMalloc(&s.keys_in, m * sizeof(uint16_t)));
+  ZK_CHECK(hipMalloc(&s.keys_out, m * sizeof(uint16_t)));
+  ZK_CHECK(hipMalloc(&s.vals_in, m * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&s.vals_out, m * sizeof(uint32_t)));
+  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, s.sort_tmp_bytes, s.keys_in, s.keys_out, s.vals_in, s.vals_out, m, 0,
+                                     16, st));
+  ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
+  ZK_CHECK(hipMalloc(&s.bstart, MSM_NB * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&s.bend, MSM_NB * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&s.tcount, (MSM_NB + 1) * sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&s.toff, (MSM_NB + 1) * sizeof(uint32_t)));
+  ZK_CHECK(rocprim::exclusive_scan(nullptr, s.scan_tmp_bytes, s.tcount, s.toff, 0u, (size_t)MSM_NB + 1,
+                                   rocprim::plus<uint32_t>(), st));
+  ZK_CHECK(hipMalloc(&s.scan_tmp, s.scan_tmp_bytes));
+  s.max_tasks = m / MSM_L + MSM_NB + 1;
+  ZK_CHECK(hipMalloc(&s.partials, s.max_tasks * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.buckets, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.red_acc, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.red_run, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.red_tmp, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.nnz, sizeof(uint32_t)));
+  return hipSuccess;
+}
+
+template <class F>
+void msm_scratch_free(MsmScratch<F>& s) {
+  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.scan_tmp, s.bstart, s.bend,
+                  s.tcount, s.toff, s.partials, s.buckets, s.red_acc, s.red_run, s.red_tmp, s.nnz};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  s = MsmScratch<F>();
+}
+
+// One MSM: n = b.n standard-form scalars (8 x u32, device) -> *d_out (device XYZZ).
+template <class F>
+hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out,
+                   hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
+  if (b.n > pl.cap) return hipErrorInvalidValue;
+  const size_t m = b.n * MSM_W;
+  const size_t max_tasks = m / MSM_L + MSM_NB + 1;
+  size_t need = 0;
+  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
+  if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, b.n, pl.keys_in,
                      pl.vals_in);
-  ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, pl.sort_tmp_bytes, pl.keys_in, pl.keys_out, pl.vals_in,
-                                     pl.vals_out, m, 0, 16, st));
+  ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
+                                     st));
   ZK_CHECK(hipMemsetAsync(pl.bstart, 0, MSM_NB * sizeof(uint32_t), st));
   ZK_CHECK(hipMemsetAsync(pl.bend, 0, MSM_NB * sizeof(uint32_t), st));
   ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
@@ -267,8 +283,8 @@ hipError_t msm_run(MsmPlan<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out, hi
   ZK_CHECK(rocprim::exclusive_scan(pl.scan_tmp, pl.scan_tmp_bytes, pl.tcount, pl.toff, 0u, (size_t)MSM_NB + 1,
                                    rocprim::plus<uint32_t>(), st));
   const int pidx = prof ? prof->begin(tag, st) : -1;
-  hipLaunchKernelGGL(k_msm_accumulate<F>, dim3(zk_grid(pl.max_tasks, 64)), dim3(64), 0, st, pl.vals_out,
-                     pl.bases_w, pl.bstart, pl.bend, pl.toff, pl.max_tasks, pl.partials);
+  hipLaunchKernelGGL(k_msm_accumulate<F>, dim3(zk_grid(max_tasks, 64)), dim3(64), 0, st, pl.vals_out, b.bases_w,
+                     pl.bstart, pl.bend, pl.toff, max_tasks, pl.partials);
   if (prof) prof->end(pidx, st, 0.0, pl.nnz);
   hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.partials, pl.toff,
                      pl.buckets);
@@ -293,7 +309,6 @@ hipError_t msm_run(MsmPlan<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out, hi
   XYZZ<F>* src = pl.red_acc;
   XYZZ<F>* dst = pl.red_tmp;
   int cnt = nacc;
-  // red_tmp may hold the last run level's data; it is no longer needed here.
   while (cnt > 1) {
     int nout = (cnt + 7) / 8;
     hipLaunchKernelGGL(k_msm_sum8<F>, dim3(zk_grid(nout, 64)), dim3(64), 0, st, src, cnt, dst);
@@ -307,15 +322,19 @@ hipError_t msm_run(MsmPlan<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out, hi
 }
 
 // Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
-#define ZKFL_MSM_DEFINE(SUF, F)                                                                   \
-  hipError_t msm_alloc_##SUF(MsmPlan<F>& pl, size_t n, hipStream_t st) { return msm_plan_alloc(pl, n, st); } \
-  void msm_free_##SUF(MsmPlan<F>& pl) { msm_plan_free(pl); }                                    \
-  hipError_t msm_set_bases_##SUF(MsmPlan<F>& pl, const Affine<F>* b, hipStream_t st) {           \
-    return msm_plan_set_bases(pl, b, st);                                                        \
-  }                                                                                              \
-  hipError_t msm_run_##SUF(MsmPlan<F>& pl, const uint32_t* s, XYZZ<F>* out, hipStream_t st, Profiler* prof, \
-                           const char* tag) {                                                    \
-    return msm_run(pl, s, out, st, prof, tag);                                                   \
+#define ZKFL_MSM_DEFINE(SUF, F)                                                                          \
+  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n) { return msm_bases_alloc(b, n); }           \
+  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, hipStream_t st) {                 \
+    return msm_bases_set(b, src, st);                                                                    \
+  }                                                                                                      \
+  void msm_bases_free_##SUF(MsmBases<F>& b) { msm_bases_free(b); }                                       \
+  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st) {                     \
+    return msm_scratch_alloc(s, cap, st);                                                                \
+  }                                                                                                      \
+  void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* sc, XYZZ<F>* out,      \
+                           hipStream_t st, Profiler* prof, const char* tag) {                            \
+    return msm_run(b, s, sc, out, st, prof, tag);                                                        \
   }
 
 }  // namespace zkfl

@@ -16,11 +16,17 @@ constexpr int MSM_RG = 8;                  // running-sum group size in the buck
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
 
 
+// Read-only, per proving key: every base expanded into its W window copies.
 template <class F>
-struct MsmPlan {
+struct MsmBases {
   size_t n = 0;                  // number of bases (including augmentation slots)
   Affine<F>* bases_w = nullptr;  // [n][W] expanded affine bases (device)
-  // scratch
+};
+
+// Mutable, per in-flight proof (one stream at a time): sort/bucket/reduction scratch.
+template <class F>
+struct MsmScratch {
+  size_t cap = 0;                // max number of bases served
   uint16_t* keys_in = nullptr;
   uint16_t* keys_out = nullptr;
   uint32_t* vals_in = nullptr;
@@ -31,7 +37,7 @@ struct MsmPlan {
   size_t scan_tmp_bytes = 0;
   uint32_t* bstart = nullptr;  // [NB]
   uint32_t* bend = nullptr;    // [NB]
-  uint32_t* tcount = nullptr;  // [NB]
+  uint32_t* tcount = nullptr;  // [NB + 1]
   uint32_t* toff = nullptr;    // [NB + 1]
   size_t max_tasks = 0;
   XYZZ<F>* partials = nullptr;  // [max_tasks]
@@ -42,15 +48,16 @@ struct MsmPlan {
   uint32_t* nnz = nullptr;      // number of non-zero digits of the last run (device)
 };
 
-hipError_t msm_alloc_g1(MsmPlan<FqOps>& pl, size_t n, hipStream_t st);
-void msm_free_g1(MsmPlan<FqOps>& pl);
-hipError_t msm_set_bases_g1(MsmPlan<FqOps>& pl, const Affine<FqOps>* b, hipStream_t st);
-hipError_t msm_run_g1(MsmPlan<FqOps>& pl, const uint32_t* s, XYZZ<FqOps>* out, hipStream_t st, Profiler* prof,
-                      const char* tag);
-hipError_t msm_alloc_g2(MsmPlan<Fq2Ops>& pl, size_t n, hipStream_t st);
-void msm_free_g2(MsmPlan<Fq2Ops>& pl);
-hipError_t msm_set_bases_g2(MsmPlan<Fq2Ops>& pl, const Affine<Fq2Ops>* b, hipStream_t st);
-hipError_t msm_run_g2(MsmPlan<Fq2Ops>& pl, const uint32_t* s, XYZZ<Fq2Ops>* out, hipStream_t st, Profiler* prof,
-                      const char* tag);
+#define ZKFL_MSM_DECLARE(SUF, F)                                                                  \
+  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                     \
+  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, hipStream_t st);           \
+  void msm_bases_free_##SUF(MsmBases<F>& b);                                                      \
+  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st);               \
+  void msm_scratch_free_##SUF(MsmScratch<F>& s);                                                  \
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* scalars, XYZZ<F>* out, \
+                           hipStream_t st, Profiler* prof, const char* tag);
+
+ZKFL_MSM_DECLARE(g1, FqOps)
+ZKFL_MSM_DECLARE(g2, Fq2Ops)
 
 }  // namespace zkfl

@@ -20,6 +20,7 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -185,13 +186,12 @@ __device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out)
   }
 }
 
-// Final assembly (one lane).  res[0]=A', res[1]=B1', res[2]=C', res[3]=H; resB2 = B2'.
-__global__ void __launch_bounds__(64) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2, const Fr* __restrict__ rs,
-                           uint32_t* __restrict__ proof) {
+// s*A + r*B1 (Shamir's trick, one lane) -> T; also pi_a (= A) in std affine -> proof[0..15].
+// Runs on its own stream as soon as the A and B1 MSMs are done (overlaps the H/C/B2 MSMs).
+__global__ void __launch_bounds__(64) k_assemble_T(const G1P* __restrict__ res, const Fr* __restrict__ rs,
+                                                   G1P* __restrict__ T_out, uint32_t* __restrict__ proof) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const G1P A = res[0], B1 = res[1];
-  G1P C = xyzz_add<FqOps>(res[2], res[3]);
-  // T = s*A + r*B1 (Shamir's trick)
   const G1P AB = xyzz_add<FqOps>(A, B1);
   const Fr r = rs[0], s = rs[1];
   G1P T = xyzz_inf<FqOps>();
@@ -204,9 +204,21 @@ __global__ void __launch_bounds__(64) k_assemble(const G1P* __restrict__ res, co
       else if (br) T = xyzz_add<FqOps>(T, B1);
     }
   }
-  C = xyzz_add<FqOps>(C, T);
+  *T_out = T;
   store_affine_std<FqOps>(xyzz_to_affine<FqOps>(A), proof);
+}
+
+// pi_b affine -> proof[16..47] (G2 stream)
+__global__ void __launch_bounds__(64) k_b2_affine(const G2P* __restrict__ resB2, uint32_t* __restrict__ proof) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
   store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
+}
+
+// pi_c = C' + H + T -> proof[48..63]
+__global__ void __launch_bounds__(64) k_finalize(const G1P* __restrict__ res, uint32_t* __restrict__ proof) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  G1P C = xyzz_add<FqOps>(res[2], res[3]);
+  C = xyzz_add<FqOps>(C, res[4]);
   store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
 }
 
@@ -275,8 +287,28 @@ __global__ void k_g2_gen_mont(G2Aff* out) {
 // ---------------------------------------------------------------------------
 struct zkfl_ctx {
   int device = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr;  // primitives, key loading
   Profiler prof;
+};
+
+// One in-flight proof: its own streams, scratch and per-proof vectors.
+struct ProofSlot {
+  hipStream_t st_main = nullptr, st_g2 = nullptr, st_asm = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_ab = nullptr, ev_b2 = nullptr, ev_t = nullptr, ev_done = nullptr;
+  MsmScratch<FqOps> g1s;
+  MsmScratch<Fq2Ops> g2s;
+  Fr* wA = nullptr;   // [nVars+2]
+  Fr* wB = nullptr;   // [nVars+2]
+  Fr* wC = nullptr;   // [nC+1]
+  Fr* abc = nullptr;  // [3n]
+  Fr* h = nullptr;    // [n]
+  G1P* res = nullptr;     // [5]: A', B1', C', H, T
+  G2P* resB2 = nullptr;   // [1]
+  Fr* d_rs = nullptr;     // [2]
+  uint32_t* d_proof = nullptr;  // [64]
+  uint8_t* pinned = nullptr;    // proof (256) | rs (64)
+  bool busy = false;
+  size_t out_index = 0;
 };
 
 struct zkfl_key {
@@ -289,20 +321,11 @@ struct zkfl_key {
   uint32_t* rowB = nullptr;  // [n+1]
   uint32_t* cols = nullptr;  // [K]
   Fr* coefs = nullptr;       // [K]
-  MsmPlan<FqOps> pA, pB1, pC, pH;
-  MsmPlan<Fq2Ops> pB2;
+  MsmBases<FqOps> bA, bB1, bC, bH;
+  MsmBases<Fq2Ops> bB2;
   NttPlan ntt;
-  // per-proof workspace
-  Fr* wA = nullptr;   // [nVars+2]
-  Fr* wB = nullptr;   // [nVars+2]
-  Fr* wC = nullptr;   // [nC+1]
-  Fr* abc = nullptr;  // [3n]
-  Fr* h = nullptr;    // [n]
-  G1P* res = nullptr;     // [4]
-  G2P* resB2 = nullptr;   // [1]
-  Fr* d_rs = nullptr;     // [2]
-  uint32_t* d_proof = nullptr;  // [64]
-  uint8_t* h_pinned = nullptr;  // 256 + 64 host staging
+  std::vector<ProofSlot*> slots;
+  int max_slots = 3;
 };
 
 struct zkfl_witness {
@@ -313,19 +336,77 @@ struct zkfl_witness {
 
 namespace {
 
-void key_release(zkfl_key* k) {
-  if (!k) return;
-  msm_free_g1(k->pA);
-  msm_free_g1(k->pB1);
-  msm_free_g1(k->pC);
-  msm_free_g1(k->pH);
-  msm_free_g2(k->pB2);
-  ntt_plan_free(k->ntt);
-  void* ptrs[] = {k->rowA, k->rowB, k->cols, k->coefs, k->wA, k->wB, k->wC, k->abc, k->h, k->res, k->resB2,
-                  k->d_rs, k->d_proof};
+void slot_release(ProofSlot* s) {
+  if (!s) return;
+  for (hipStream_t st : {s->st_main, s->st_g2, s->st_asm})
+    if (st) (void)hipStreamSynchronize(st);
+  msm_scratch_free_g1(s->g1s);
+  msm_scratch_free_g2(s->g2s);
+  void* ptrs[] = {s->wA, s->wB, s->wC, s->abc, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  if (k->h_pinned) (void)hipHostFree(k->h_pinned);
+  if (s->pinned) (void)hipHostFree(s->pinned);
+  for (hipEvent_t e : {s->ev_ready, s->ev_ab, s->ev_b2, s->ev_t, s->ev_done})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t st : {s->st_main, s->st_g2, s->st_asm})
+    if (st) (void)hipStreamDestroy(st);
+  delete s;
+}
+
+hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
+  ProofSlot* s = new ProofSlot();
+  *out = s;
+  const size_t nV = k->nVars, n = k->n;
+  const size_t cap1 = std::max<size_t>({nV + 2, k->nC + 1, (size_t)n});
+  hipStream_t st = k->ctx->st;
+  ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
+  ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
+  ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
+    ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
+  ZK_CHECK(msm_scratch_alloc_g2(s->g2s, nV + 2, st));
+  ZK_CHECK(hipMalloc(&s->wA, (nV + 2) * 32));
+  ZK_CHECK(hipMalloc(&s->wB, (nV + 2) * 32));
+  ZK_CHECK(hipMalloc(&s->wC, (k->nC + 1) * 32));
+  ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
+  ZK_CHECK(hipMalloc(&s->h, n * 32));
+  ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
+  ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
+  ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32));
+  ZK_CHECK(hipMalloc(&s->d_proof, 256));
+  ZK_CHECK(hipHostMalloc(&s->pinned, 512));
+  return hipStreamSynchronize(st);
+}
+
+int get_slot(zkfl_key* k, size_t idx, ProofSlot** out) {
+  size_t want = idx % (size_t)k->max_slots;
+  while (k->slots.size() <= want) {
+    ProofSlot* s = nullptr;
+    hipError_t e = slot_create(k, &s);
+    if (e != hipSuccess) {
+      slot_release(s);
+      return hip_fail(e, "proof slot allocation");
+    }
+    k->slots.push_back(s);
+  }
+  *out = k->slots[want];
+  return ZKFL_OK;
+}
+
+void key_release(zkfl_key* k) {
+  if (!k) return;
+  for (ProofSlot* s : k->slots) slot_release(s);
+  k->slots.clear();
+  msm_bases_free_g1(k->bA);
+  msm_bases_free_g1(k->bB1);
+  msm_bases_free_g1(k->bC);
+  msm_bases_free_g1(k->bH);
+  msm_bases_free_g2(k->bB2);
+  ntt_plan_free(k->ntt);
+  void* ptrs[] = {k->rowA, k->rowB, k->cols, k->coefs};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
   delete k;
 }
 
@@ -349,75 +430,107 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
   return ZKFL_OK;
 }
 
-// Proof core on a device-resident witness.  plain = 1: no alpha/beta/delta/r/s terms
-// (parity hook); the proof is then not assembled.
-int prove_core(zkfl_ctx* ctx, zkfl_key* k, const Fr* d_w, const uint32_t rs_host[16], int plain) {
-  hipStream_t st = ctx->st;
+// Enqueue one proof on a slot (asynchronous).  Stream graph:
+//   main : rs, scalar vectors, [ev_ready] MSM A, MSM B1 [ev_ab] ABC, coset NTT x3, join,
+//          MSM H, MSM C, wait(ev_t, ev_b2), finalize, proof D2H [ev_done]
+//   g2   : wait(ev_ready) MSM B2, pi_b affine [ev_b2]
+//   asm  : wait(ev_ab) T = s*A + r*B1, pi_a affine [ev_t]
+// plain = 1 (parity hook): alpha/beta/delta/r/s terms zeroed, nothing assembled.
+int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
   Profiler* prof = &ctx->prof;
+  hipStream_t st = s->st_main;
   const size_t nV = k->nVars, n = k->n;
-  memcpy(k->h_pinned + 256, rs_host, 64);  // pinned staging (the stream is drained per proof)
-  HIP_TRY(hipMemcpyAsync(k->d_rs, k->h_pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
-  HIP_TRY(hipMemcpyAsync(k->wA, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wA");
-  HIP_TRY(hipMemcpyAsync(k->wB, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wB");
-  if (k->nC) HIP_TRY(hipMemcpyAsync(k->wC, d_w + k->nPub + 1, k->nC * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wC");
-  hipLaunchKernelGGL(k_set_rs, dim3(1), dim3(1), 0, st, k->d_rs, k->wA, k->wB, k->wC, nV, k->nC, plain);
+  memcpy(s->pinned + 256, rs_host, 64);
+  int pp = prof->begin("prove", st);
+  HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
+  HIP_TRY(hipMemcpyAsync(s->wA, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wA");
+  HIP_TRY(hipMemcpyAsync(s->wB, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wB");
+  if (k->nC) HIP_TRY(hipMemcpyAsync(s->wC, d_w + k->nPub + 1, k->nC * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wC");
+  hipLaunchKernelGGL(k_set_rs, dim3(1), dim3(1), 0, st, s->d_rs, s->wA, s->wB, s->wC, nV, k->nC, plain);
+  HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
+  // G2 stream
+  HIP_TRY(hipStreamWaitEvent(s->st_g2, s->ev_ready, 0), "wait");
+  HIP_TRY(msm_run_g2(k->bB2, s->g2s, (const uint32_t*)s->wB, s->resB2, s->st_g2, prof, "msm_accumulate_g2"), "msm B2");
+  if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, s->st_g2, s->resB2, s->d_proof);
+  HIP_TRY(hipEventRecord(s->ev_b2, s->st_g2), "event");
+  // main: A, B1 first so the assembly chain can start early
+  HIP_TRY(msm_run_g1(k->bA, s->g1s, (const uint32_t*)s->wA, s->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
+  HIP_TRY(msm_run_g1(k->bB1, s->g1s, (const uint32_t*)s->wB, s->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
+  if (!plain) {
+    HIP_TRY(hipStreamWaitEvent(s->st_asm, s->ev_ab, 0), "wait");
+    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, s->st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
+    HIP_TRY(hipEventRecord(s->ev_t, s->st_asm), "event");
+  }
   int pi = prof->begin("abc", st);
   hipLaunchKernelGGL(k_abc, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rowA, k->rowB, k->cols, k->coefs, d_w, n,
-                     k->abc);
+                     s->abc);
   prof->end(pi, st, (double)k->K);
   pi = prof->begin("ntt", st);
-  HIP_TRY(ntt_coset_shift(k->ntt, k->abc, 3, n, st), "ntt");
+  HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
   prof->end(pi, st, 3.0 * (double)n);
-  hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->abc, n, k->h);
-  HIP_TRY(msm_run_g1(k->pH, (const uint32_t*)k->h, k->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
-  HIP_TRY(msm_run_g1(k->pA, (const uint32_t*)k->wA, k->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
-  HIP_TRY(msm_run_g1(k->pB1, (const uint32_t*)k->wB, k->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
-  HIP_TRY(msm_run_g2(k->pB2, (const uint32_t*)k->wB, k->resB2, st, prof, "msm_accumulate_g2"), "msm B2");
-  HIP_TRY(msm_run_g1(k->pC, (const uint32_t*)k->wC, k->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
-  if (!plain) hipLaunchKernelGGL(k_assemble, dim3(1), dim3(1), 0, st, k->res, k->resB2, k->d_rs, k->d_proof);
+  hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
+  HIP_TRY(msm_run_g1(k->bH, s->g1s, (const uint32_t*)s->h, s->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
+  HIP_TRY(msm_run_g1(k->bC, s->g1s, (const uint32_t*)s->wC, s->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
+  HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
+  if (!plain) {
+    HIP_TRY(hipStreamWaitEvent(st, s->ev_t, 0), "wait");
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, st, s->res, s->d_proof);
+    HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
+  }
+  prof->end(pp, st, 1.0);
+  HIP_TRY(hipEventRecord(s->ev_done, st), "event");
   HIP_TRY(hipGetLastError(), "launch");
   return ZKFL_OK;
 }
 
-int fetch_proof(zkfl_ctx* ctx, zkfl_key* k, uint8_t proof_out[256]) {
-  HIP_TRY(hipMemcpyAsync(k->h_pinned, k->d_proof, 256, hipMemcpyDeviceToHost, ctx->st), "download proof");
-  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
-  memcpy(proof_out, k->h_pinned, 256);
+int wait_slot(ProofSlot* s, uint8_t* proof_out) {
+  HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
+  if (proof_out) memcpy(proof_out, s->pinned, 256);
+  s->busy = false;
   return ZKFL_OK;
 }
 
-hipError_t msm_alloc_any(MsmPlan<FqOps>& pl, size_t n, hipStream_t st) { return msm_alloc_g1(pl, n, st); }
-hipError_t msm_alloc_any(MsmPlan<Fq2Ops>& pl, size_t n, hipStream_t st) { return msm_alloc_g2(pl, n, st); }
-void msm_free_any(MsmPlan<FqOps>& pl) { msm_free_g1(pl); }
-void msm_free_any(MsmPlan<Fq2Ops>& pl) { msm_free_g2(pl); }
-hipError_t msm_set_bases_any(MsmPlan<FqOps>& pl, const G1Aff* b, hipStream_t st) { return msm_set_bases_g1(pl, b, st); }
-hipError_t msm_set_bases_any(MsmPlan<Fq2Ops>& pl, const G2Aff* b, hipStream_t st) { return msm_set_bases_g2(pl, b, st); }
-hipError_t msm_run_any(MsmPlan<FqOps>& pl, const uint32_t* s, G1P* o, hipStream_t st, Profiler* p) {
-  return msm_run_g1(pl, s, o, st, p, "msm_accumulate_g1");
+hipError_t msm_run_any(const MsmBases<FqOps>& b, MsmScratch<FqOps>& s, const uint32_t* sc, G1P* o, hipStream_t st,
+                       Profiler* p) {
+  return msm_run_g1(b, s, sc, o, st, p, "msm_accumulate_g1");
 }
-hipError_t msm_run_any(MsmPlan<Fq2Ops>& pl, const uint32_t* s, G2P* o, hipStream_t st, Profiler* p) {
-  return msm_run_g2(pl, s, o, st, p, "msm_accumulate_g2");
+hipError_t msm_run_any(const MsmBases<Fq2Ops>& b, MsmScratch<Fq2Ops>& s, const uint32_t* sc, G2P* o, hipStream_t st,
+                       Profiler* p) {
+  return msm_run_g2(b, s, sc, o, st, p, "msm_accumulate_g2");
 }
+hipError_t bases_alloc_any(MsmBases<FqOps>& b, size_t n) { return msm_bases_alloc_g1(b, n); }
+hipError_t bases_alloc_any(MsmBases<Fq2Ops>& b, size_t n) { return msm_bases_alloc_g2(b, n); }
+hipError_t bases_set_any(MsmBases<FqOps>& b, const G1Aff* src, hipStream_t st) { return msm_bases_set_g1(b, src, st); }
+hipError_t bases_set_any(MsmBases<Fq2Ops>& b, const G2Aff* src, hipStream_t st) { return msm_bases_set_g2(b, src, st); }
+void bases_free_any(MsmBases<FqOps>& b) { msm_bases_free_g1(b); }
+void bases_free_any(MsmBases<Fq2Ops>& b) { msm_bases_free_g2(b); }
+hipError_t scratch_alloc_any(MsmScratch<FqOps>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g1(s, n, st); }
+hipError_t scratch_alloc_any(MsmScratch<Fq2Ops>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g2(s, n, st); }
+void scratch_free_any(MsmScratch<FqOps>& s) { msm_scratch_free_g1(s); }
+void scratch_free_any(MsmScratch<Fq2Ops>& s) { msm_scratch_free_g2(s); }
 
 template <class F>
 int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out) {
   if (!ctx || !bases || !scalars || !out || n == 0) return fail(ZKFL_E_ARG, "msm: bad args");
   hipStream_t st = ctx->st;
-  MsmPlan<F> pl;
+  MsmBases<F> mb;
+  MsmScratch<F> ms;
   Affine<F>* d_b = nullptr;
   uint32_t* d_s = nullptr;
   XYZZ<F>* d_r = nullptr;
   uint32_t* d_o = nullptr;
   int rc = ZKFL_OK;
-  hipError_t e = msm_alloc_any(pl, n, st);
+  hipError_t e = bases_alloc_any(mb, n);
+  if (e == hipSuccess) e = scratch_alloc_any(ms, n, st);
   if (e == hipSuccess) e = hipMalloc(&d_b, n * sizeof(Affine<F>));
   if (e == hipSuccess) e = hipMalloc(&d_s, n * 32);
   if (e == hipSuccess) e = hipMalloc(&d_r, sizeof(XYZZ<F>));
   if (e == hipSuccess) e = hipMalloc(&d_o, sizeof(Affine<F>));
   if (e == hipSuccess) e = hipMemcpyAsync(d_b, bases, n * sizeof(Affine<F>), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = msm_set_bases_any(pl, d_b, st);
-  if (e == hipSuccess) e = msm_run_any(pl, d_s, d_r, st, &ctx->prof);
+  if (e == hipSuccess) e = bases_set_any(mb, d_b, st);
+  if (e == hipSuccess) e = msm_run_any(mb, ms, d_s, d_r, st, &ctx->prof);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_point_out<F>, dim3(1), dim3(1), 0, st, d_r, 1, d_o);
     e = hipGetLastError();
@@ -425,7 +538,8 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   if (e == hipSuccess) e = hipMemcpyAsync(out, d_o, sizeof(Affine<F>), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) rc = hip_fail(e, "msm primitive");
-  msm_free_any(pl);
+  bases_free_any(mb);
+  scratch_free_any(ms);
   for (void* p : {(void*)d_b, (void*)d_s, (void*)d_r, (void*)d_o})
     if (p) (void)hipFree(p);
   return rc;
@@ -633,12 +747,13 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
     KTRY(hipMemcpyAsync(k->coefs, coefs.data(), (size_t)ncoef * 32, hipMemcpyHostToDevice, st), "upload");
   }
-  // MSM plans with augmented bases
-  KTRY(msm_alloc_g1(k->pA, (size_t)nVars + 2, st), "plan A");
-  KTRY(msm_alloc_g1(k->pB1, (size_t)nVars + 2, st), "plan B1");
-  KTRY(msm_alloc_g2(k->pB2, (size_t)nVars + 2, st), "plan B2");
-  KTRY(msm_alloc_g1(k->pC, nC + 1, st), "plan C");
-  KTRY(msm_alloc_g1(k->pH, dom, st), "plan H");
+  // MSM bases with augmentation slots (alpha1/delta1 on A, beta1/delta1 on B1, beta2/delta2 on B2,
+  // delta1 on C), expanded per window
+  KTRY(msm_bases_alloc_g1(k->bA, (size_t)nVars + 2), "bases A");
+  KTRY(msm_bases_alloc_g1(k->bB1, (size_t)nVars + 2), "bases B1");
+  KTRY(msm_bases_alloc_g2(k->bB2, (size_t)nVars + 2), "bases B2");
+  KTRY(msm_bases_alloc_g1(k->bC, nC + 1), "bases C");
+  KTRY(msm_bases_alloc_g1(k->bH, dom), "bases H");
   {
     const uint8_t* alpha1 = pts;
     const uint8_t* beta1 = pts + 64;
@@ -649,38 +764,33 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     if ((size_t)dom * 64 > maxb) maxb = (size_t)dom * 64;
     uint8_t* d_tmp = nullptr;
     KTRY(hipMalloc(&d_tmp, maxb), "alloc tmp");
-    auto upload_g1 = [&](MsmPlan<FqOps>& pl, const uint8_t* sec, size_t cnt, const uint8_t* x0,
+    auto upload_g1 = [&](MsmBases<FqOps>& mb, const uint8_t* sec, size_t cnt, const uint8_t* x0,
                          const uint8_t* x1) -> hipError_t {
       hipError_t e = hipMemcpyAsync(d_tmp, sec, cnt * 64, hipMemcpyHostToDevice, st);
       if (e == hipSuccess && x0) e = hipMemcpyAsync(d_tmp + cnt * 64, x0, 64, hipMemcpyHostToDevice, st);
       if (e == hipSuccess && x1) e = hipMemcpyAsync(d_tmp + (cnt + 1) * 64, x1, 64, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) e = msm_set_bases_g1(pl, (const G1Aff*)d_tmp, st);
+      if (e == hipSuccess) e = msm_bases_set_g1(mb, (const G1Aff*)d_tmp, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       return e;
     };
-    hipError_t e = upload_g1(k->pA, buf + s[5].off, nVars, alpha1, delta1);
-    if (e == hipSuccess) e = upload_g1(k->pB1, buf + s[6].off, nVars, beta1, delta1);
-    if (e == hipSuccess) e = upload_g1(k->pC, buf + s[8].off, nC, delta1, nullptr);
-    if (e == hipSuccess) e = upload_g1(k->pH, buf + s[9].off, dom, nullptr, nullptr);
+    hipError_t e = upload_g1(k->bA, buf + s[5].off, nVars, alpha1, delta1);
+    if (e == hipSuccess) e = upload_g1(k->bB1, buf + s[6].off, nVars, beta1, delta1);
+    if (e == hipSuccess) e = upload_g1(k->bC, buf + s[8].off, nC, delta1, nullptr);
+    if (e == hipSuccess) e = upload_g1(k->bH, buf + s[9].off, dom, nullptr, nullptr);
     if (e == hipSuccess) e = hipMemcpyAsync(d_tmp, buf + s[7].off, (size_t)nVars * 128, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + (size_t)nVars * 128, beta2, 128, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + ((size_t)nVars + 1) * 128, delta2, 128, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = msm_set_bases_g2(k->pB2, (const G2Aff*)d_tmp, st);
+    if (e == hipSuccess) e = msm_bases_set_g2(k->bB2, (const G2Aff*)d_tmp, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(d_tmp);
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
-  KTRY(hipMalloc(&k->wA, ((size_t)nVars + 2) * 32), "alloc");
-  KTRY(hipMalloc(&k->wB, ((size_t)nVars + 2) * 32), "alloc");
-  KTRY(hipMalloc(&k->wC, (nC + 1) * 32), "alloc");
-  KTRY(hipMalloc(&k->abc, (size_t)dom * 3 * 32), "alloc");
-  KTRY(hipMalloc(&k->h, (size_t)dom * 32), "alloc");
-  KTRY(hipMalloc(&k->res, 4 * sizeof(G1P)), "alloc");
-  KTRY(hipMalloc(&k->resB2, sizeof(G2P)), "alloc");
-  KTRY(hipMalloc(&k->d_rs, 2 * 32), "alloc");
-  KTRY(hipMalloc(&k->d_proof, 256), "alloc");
-  KTRY(hipHostMalloc(&k->h_pinned, 512), "alloc pinned");
+  {
+    ProofSlot* s0 = nullptr;
+    int rc0 = get_slot(k, 0, &s0);  // first slot eagerly: surfaces OOM at load time
+    if (rc0) return cleanup(rc0);
+  }
   KTRY(hipStreamSynchronize(st), "sync");
 #undef KTRY
   *out = k;
@@ -735,27 +845,54 @@ int zkfl_witness_free(zkfl_witness* w) {
 
 int zkfl_groth16_prove_resident(zkfl_ctx* ctx, zkfl_key* key, const zkfl_witness* w, const uint8_t* rs,
                                 uint8_t proof_out[256]) {
-  if (!ctx || !key || !w || !proof_out) return fail(ZKFL_E_ARG, "null argument");
-  if (w->key != key) return fail(ZKFL_E_MISMATCH, "witness uploaded for another key");
-  uint32_t rsl[16];
-  int rc = get_rs(rs, rsl);
-  if (rc) return rc;
-  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-  int pi = ctx->prof.begin("prove", ctx->st);
-  rc = prove_core(ctx, key, w->d, rsl, 0);
-  ctx->prof.end(pi, ctx->st, 1.0);
-  if (rc) return rc;
-  return fetch_proof(ctx, key, proof_out);
+  return zkfl_groth16_prove_batch(ctx, key, 1, &w, rs, proof_out);
+}
+
+int zkfl_key_set_slots(zkfl_key* key, int slots) {
+  if (!key || slots < 1 || slots > 16) return fail(ZKFL_E_ARG, "slots must be in 1..16");
+  (void)hipSetDevice(key->ctx->device);
+  for (ProofSlot* s : key->slots) {
+    if (s->busy) return fail(ZKFL_E_ARG, "slots busy");
+  }
+  while ((int)key->slots.size() > slots) {
+    slot_release(key->slots.back());
+    key->slots.pop_back();
+  }
+  key->max_slots = slots;
+  return ZKFL_OK;
 }
 
 int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
                              const uint8_t* rs, uint8_t* proofs_out) {
   if (!ctx || !key || (!w && n) || (!proofs_out && n)) return fail(ZKFL_E_ARG, "null argument");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   for (size_t i = 0; i < n; i++) {
-    int rc = zkfl_groth16_prove_resident(ctx, key, w[i], rs ? rs + 64 * i : nullptr, proofs_out + 256 * i);
-    if (rc) return rc;
+    if (!w[i] || w[i]->key != key) return fail(ZKFL_E_MISMATCH, "witness uploaded for another key");
   }
-  return ZKFL_OK;
+  int rc = ZKFL_OK;
+  for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
+    uint32_t rsl[16];
+    rc = get_rs(rs ? rs + 64 * i : nullptr, rsl);
+    if (rc) break;
+    ProofSlot* s = nullptr;
+    rc = get_slot(key, i, &s);
+    if (rc) break;
+    if (s->busy) {
+      rc = wait_slot(s, proofs_out + 256 * s->out_index);
+      if (rc) break;
+    }
+    rc = enqueue_proof(ctx, key, s, w[i]->d, rsl, 0);
+    if (rc) break;
+    s->busy = true;
+    s->out_index = i;
+  }
+  for (ProofSlot* s : key->slots) {
+    if (s->busy) {
+      int r2 = wait_slot(s, proofs_out + 256 * s->out_index);
+      if (rc == ZKFL_OK) rc = r2;
+    }
+  }
+  return rc;
 }
 
 int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, const uint8_t* rs,
@@ -777,15 +914,18 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   zkfl_witness* w = nullptr;
   int rc = zkfl_witness_upload(ctx, key, wtns, wtns_len, &w);
   if (rc) return rc;
+  ProofSlot* s = nullptr;
+  rc = get_slot(key, 0, &s);
   uint32_t zeros[16] = {0};
-  rc = prove_core(ctx, key, w->d, zeros, 1);
-  hipStream_t st = ctx->st;
+  if (rc == ZKFL_OK) rc = enqueue_proof(ctx, key, s, w->d, zeros, 1);
+  if (rc == ZKFL_OK) rc = wait_slot(s, nullptr);
+  hipStream_t st = s ? s->st_main : ctx->st;
   uint32_t* d_o = nullptr;
   if (rc == ZKFL_OK && msm_out) {
     hipError_t e = hipMalloc(&d_o, 64 * 4 + 128);
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(k_point_out<FqOps>, dim3(1), dim3(4), 0, st, key->res, 4, d_o);
-      hipLaunchKernelGGL(k_point_out<Fq2Ops>, dim3(1), dim3(1), 0, st, key->resB2, 1, d_o + 64);
+      hipLaunchKernelGGL(k_point_out<FqOps>, dim3(1), dim3(4), 0, st, s->res, 4, d_o);
+      hipLaunchKernelGGL(k_point_out<Fq2Ops>, dim3(1), dim3(1), 0, st, s->resB2, 1, d_o + 64);
       e = hipGetLastError();
     }
     std::vector<uint8_t> tmp(64 * 4 + 128);
@@ -802,7 +942,7 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
     }
   }
   if (rc == ZKFL_OK && h_out) {
-    hipError_t e = hipMemcpyAsync(h_out, key->h, (size_t)key->n * 32, hipMemcpyDeviceToHost, st);
+    hipError_t e = hipMemcpyAsync(h_out, s->h, (size_t)key->n * 32, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) rc = hip_fail(e, "debug h");
   }

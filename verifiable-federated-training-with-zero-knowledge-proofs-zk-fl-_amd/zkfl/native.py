@@ -36,6 +36,7 @@ SIGNATURES = {
     "zkfl_zkey_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "zkfl_key_free": (C.c_int, [_P]),
     "zkfl_key_info": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "zkfl_key_set_slots": (C.c_int, [_P, C.c_int]),
     "zkfl_groth16_prove": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, C.c_char_p, _U8P, _U8P,
                                      C.POINTER(C.c_size_t)]),
     "zkfl_witness_upload": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
@@ -182,6 +183,10 @@ class ProvingKey:
             self.close()
         except Exception:
             pass
+
+    def set_slots(self, slots: int):
+        """Proofs kept in flight by prove_batch (each slot = 3 HIP streams + scratch)."""
+        check(lib().zkfl_key_set_slots(self.h, slots))
 
     def prove(self, wtns: bytes, rs: bytes | None = None):
         """-> (proof 256 B, [public signal ints])"""
