@@ -569,3 +569,74 @@ int ref_msm_g1(const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* 
   g1_to_std_aff(out, &r);
   return 0;
 }
+
+/* fixed-base k*G (dev-ceremony backend for CPU tests): out = Montgomery affine, (0,0) = inf */
+static void g1_to_mont_aff(uint8_t* out, const g1_jac* p) {
+  if (g1_is_inf(p)) { memset(out, 0, 64); return; }
+  fe zi, zi2, zi3, x, y;
+  qinv(&zi, &p->Z);
+  QMUL(&zi2, &zi, &zi);
+  QMUL(&zi3, &zi2, &zi);
+  QMUL(&x, &p->X, &zi2);
+  QMUL(&y, &p->Y, &zi3);
+  memcpy(out, x.v, 32);
+  memcpy(out + 32, y.v, 32);
+}
+
+static void g2_to_mont_aff(uint8_t* out, const g2_jac* p) {
+  if (g2_is_inf(p)) { memset(out, 0, 128); return; }
+  fe2 zi, zi2, zi3, x, y;
+  f2inv(&zi, &p->Z);
+  f2mul(&zi2, &zi, &zi);
+  f2mul(&zi3, &zi2, &zi);
+  f2mul(&x, &p->X, &zi2);
+  f2mul(&y, &p->Y, &zi3);
+  memcpy(out, x.c0.v, 32); memcpy(out + 32, x.c1.v, 32);
+  memcpy(out + 64, y.c0.v, 32); memcpy(out + 96, y.c1.v, 32);
+}
+
+static void q_to_mont(fe* x) { QMUL(x, x, &Q_R2); }
+
+int ref_g1_gen_mul(const uint8_t* scalars, size_t n, uint8_t* out, int threads) {
+  init_consts();
+  if (threads > 0) omp_set_num_threads(threads);
+  g1_jac G;
+  memset(&G, 0, sizeof G);
+  G.X.v[0] = 1; G.Y.v[0] = 2;
+  q_to_mont(&G.X); q_to_mont(&G.Y);
+  G.Z = Q_ONE;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (size_t i = 0; i < n; i++) {
+    g1_jac r;
+    g1_mul_scalar(&r, &G, (const fe*)(scalars + 32 * i));
+    g1_to_mont_aff(out + 64 * i, &r);
+  }
+  return 0;
+}
+
+int ref_g2_gen_mul(const uint8_t* scalars, size_t n, uint8_t* out, int threads) {
+  init_consts();
+  if (threads > 0) omp_set_num_threads(threads);
+  static const uint64_t gx0[4] = {0x46debd5cd992f6edull, 0x674322d4f75edaddull, 0x426a00665e5c4479ull, 0x1800deef121f1e76ull};
+  static const uint64_t gx1[4] = {0x97e485b7aef312c2ull, 0xf1aa493335a9e712ull, 0x7260bfb731fb5d25ull, 0x198e9393920d483aull};
+  static const uint64_t gy0[4] = {0x4ce6cc0166fa7daaull, 0xe3d1e7690c43d37bull, 0x4aab71808dcb408full, 0x12c85ea5db8c6debull};
+  static const uint64_t gy1[4] = {0x55acdadcd122975bull, 0xbc4b313370b38ef3ull, 0xec9e99ad690c3395ull, 0x090689d0585ff075ull};
+  g2_jac G;
+  memcpy(G.X.c0.v, gx0, 32); memcpy(G.X.c1.v, gx1, 32);
+  memcpy(G.Y.c0.v, gy0, 32); memcpy(G.Y.c1.v, gy1, 32);
+  q_to_mont(&G.X.c0); q_to_mont(&G.X.c1); q_to_mont(&G.Y.c0); q_to_mont(&G.Y.c1);
+  G.Z.c0 = Q_ONE; memset(&G.Z.c1, 0, 32);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (size_t i = 0; i < n; i++) {
+    const fe* k = (const fe*)(scalars + 32 * i);
+    g2_jac acc;
+    memset(&acc, 0, sizeof acc);
+    for (int w = 3; w >= 0; w--)
+      for (int b = 63; b >= 0; b--) {
+        g2_dbl(&acc, &acc);
+        if ((k->v[w] >> b) & 1) g2_add(&acc, &acc, &G);
+      }
+    g2_to_mont_aff(out + 128 * i, &acc);
+  }
+  return 0;
+}

@@ -22,6 +22,10 @@ def lib():
                                 C.POINTER(C.c_uint8), C.c_int]
         L.ref_msm_g1.restype = C.c_int
         L.ref_msm_g1.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint8), C.c_int]
+        for nm in ("ref_g1_gen_mul", "ref_g2_gen_mul"):
+            f = getattr(L, nm)
+            f.restype = C.c_int
+            f.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_uint8), C.c_int]
         _lib = L
     return _lib
 
@@ -63,3 +67,17 @@ def time_prove(zkey: bytes, wtns: bytes, seconds_budget: float = 20.0) -> dict:
     return {"value": round(k / dt, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
             "sample": f"{k} full proof(s) of the same zkey/wtns by the C oracle "
                       f"(oracle/c/groth16_ref.c, OpenMP {threads} threads) in {dt:.1f} s"}
+
+
+def g1_gen_mul(scalars: bytes, threads: int = 0) -> bytes:
+    n = len(scalars) // 32
+    out = (C.c_uint8 * max(1, 64 * n))()
+    lib().ref_g1_gen_mul(scalars, n, out, threads)
+    return bytes(out)[:64 * n]
+
+
+def g2_gen_mul(scalars: bytes, threads: int = 0) -> bytes:
+    n = len(scalars) // 32
+    out = (C.c_uint8 * max(1, 128 * n))()
+    lib().ref_g2_gen_mul(scalars, n, out, threads)
+    return bytes(out)[:128 * n]

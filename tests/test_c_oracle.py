@@ -29,7 +29,7 @@ def test_c_msm_matches_python(cb):
 
 @pytest.mark.parametrize("circ", [("poseidon_hash2",), ("sgd_verified", 8, 4, 3, 1000)])
 def test_c_prove_matches_python(cb, circ):
-    from oracle_backend import OraclePoints
+    from oracle_backend import COraclePoints, OraclePoints
     from zkfl import circuits, clients, zkey
     b = circuits.build(*circ)
     if circ[0] == "poseidon_hash2":
@@ -37,10 +37,16 @@ def test_c_prove_matches_python(cb, circ):
     else:
         inp, _ = clients.Client(1, 8, 4, 3, clients.JsLcg(12345)).training_input(8, 1000, 100000000)
         w = b.witness(inp)
-        if os.environ.get("ZKFL_FAST_TESTS"):
-            pytest.skip("slow python setup")
-    zk = zkey.groth16_setup(b, OraclePoints(), zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
+    backend = OraclePoints() if circ[0] == "poseidon_hash2" else COraclePoints()
+    zk = zkey.groth16_setup(b, backend, zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
     rs = (777).to_bytes(32, "little") + (888).to_bytes(32, "little")
     got = cb.prove(zk, zkey.wtns_bytes(w), rs, threads=4)
     ref = og.prove(og.parse_zkey(zk), w, r=777, s=888)
     assert got == og.proof_bytes(ref)
+
+
+def test_c_gen_mul_matches_python(cb):
+    from oracle_backend import COraclePoints, OraclePoints
+    ks = b"".join(k.to_bytes(32, "little") for k in (0, 1, 5, bn.R - 1, 1 << 250, 123456789))
+    assert COraclePoints().g1_gen_mul(ks) == OraclePoints().g1_gen_mul(ks)
+    assert COraclePoints().g2_gen_mul(ks) == OraclePoints().g2_gen_mul(ks)

@@ -1,0 +1,151 @@
+// Microbenchmark: Fq Montgomery multiplication throughput variants on gfx950.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I<pkg>/csrc -o fp_microbench fp_microbench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "field.h"
+using namespace zkfl;
+
+template <class PR>
+__device__ __forceinline__ Fp<PR> fips_mul(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t m[8], u[9];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+  uint64_t cc;
+#define MACV(x, y) asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1" : "+v"(lo), "=&s"(cc), "+v"(hi) : "v"(x), "v"(y) : "vcc");
+#define MACS(x, y) asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1" : "+v"(lo), "=&s"(cc), "+v"(hi) : "v"(x), "s"(y) : "vcc");
+#define SHIFT() { lo = (lo >> 32) | ((uint64_t)hi << 32); hi = 0; }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) { MACV(a.v[j], b.v[i - j]); MACS(m[j], PR::P[i - j]); }
+    MACV(a.v[i], b.v[0]);
+    m[i] = (uint32_t)lo * PR::INV;
+    MACS(m[i], PR::P[0]);
+    SHIFT();
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) { MACV(a.v[j], b.v[i - j]); MACS(m[j], PR::P[i - j]); }
+    u[i - 8] = (uint32_t)lo;
+    SHIFT();
+  }
+  u[8] = (uint32_t)lo;
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, u);
+  return r;
+}
+
+
+template <class PR>
+__device__ __forceinline__ Fp<PR> fips_mul_vcc(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t m[8], u[9];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#define MACV2(x, y) asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "v"(y) : "vcc");
+#define MACS2(x, y) asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "s"(y) : "vcc");
+#define SHIFT2() { lo = (lo >> 32) | ((uint64_t)hi << 32); hi = 0; }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) { MACV2(a.v[j], b.v[i - j]); MACS2(m[j], PR::P[i - j]); }
+    MACV2(a.v[i], b.v[0]);
+    m[i] = (uint32_t)lo * PR::INV;
+    MACS2(m[i], PR::P[0]);
+    SHIFT2();
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) { MACV2(a.v[j], b.v[i - j]); MACS2(m[j], PR::P[i - j]); }
+    u[i - 8] = (uint32_t)lo;
+    SHIFT2();
+  }
+  u[8] = (uint32_t)lo;
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, u);
+  return r;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) kbench(Fq* data, int iters) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq x0 = data[i], x1 = data[i + 1], x2 = data[i + 2], x3 = data[i + 3];
+  const Fq y = data[0];
+  for (int k = 0; k < iters; k++) {
+    if (V == 0) { x0 = fp_mul(x0, y); x1 = fp_mul(x1, y); x2 = fp_mul(x2, y); x3 = fp_mul(x3, y); }
+    else if (V == 1) { x0 = fips_mul(x0, y); x1 = fips_mul(x1, y); x2 = fips_mul(x2, y); x3 = fips_mul(x3, y); }
+    else { x0 = fips_mul_vcc(x0, y); x1 = fips_mul_vcc(x1, y); x2 = fips_mul_vcc(x2, y); x3 = fips_mul_vcc(x3, y); }
+  }
+  data[i] = fp_add(fp_add(x0, x1), fp_add(x2, x3));
+}
+
+// latency: one lane, one dependent chain
+template <int V>
+__global__ void klat(Fq* data, int iters) {
+  Fq x = data[1];
+  const Fq y = data[0];
+  for (int k = 0; k < iters; k++) x = V == 0 ? fp_mul(x, y) : (V == 1 ? fips_mul(x, y) : fips_mul_vcc(x, y));
+  data[1] = x;
+}
+
+__global__ void kcheck(const Fq* a, const Fq* b, int n, int* bad) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fq r0 = fp_mul(a[i], b[i]), r1 = fips_mul(a[i], b[i]), r2 = fips_mul_vcc(a[i], b[i]);
+  if (!fp_eq(r0, r1)) atomicAdd(bad, 1);
+  if (!fp_eq(r0, r2)) atomicAdd(bad + 1, 1);
+}
+
+int main() {
+  const int blocks = 256 * 8, threads = 256, iters = 2000;
+  size_t n = (size_t)blocks * threads + 8;
+  Fq* d;
+  hipMalloc(&d, n * sizeof(Fq));
+  hipMemset(d, 0x11, n * sizeof(Fq));
+  {
+    // correctness on pseudo-random inputs < q
+    const int m = 1 << 20;
+    Fq* h = (Fq*)malloc(2 * m * sizeof(Fq));
+    uint64_t st = 88172645463325252ull;
+    for (int i = 0; i < 2 * m; i++)
+      for (int j = 0; j < 8; j++) {
+        st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+        h[i].v[j] = (uint32_t)st & (j == 7 ? 0x1fffffffu : 0xffffffffu);
+      }
+    Fq* dd; int* bad; int hb[2] = {0, 0};
+    hipMalloc(&dd, 2 * m * sizeof(Fq)); hipMalloc(&bad, 8);
+    hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, 8);
+    hipLaunchKernelGGL(kcheck, dim3(m / 256), dim3(256), 0, 0, dd, dd + m, m, bad);
+    hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost);
+    printf("mismatches vs CIOS: fips_sgpr=%d fips_vcc=%d (of %d)\n", hb[0], hb[1], m);
+  }
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int v = 0; v < 3; v++) {
+    for (int rep = 0; rep < 2; rep++) {
+      hipEventRecord(a);
+      if (v == 0) hipLaunchKernelGGL(kbench<0>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      else if (v == 1) hipLaunchKernelGGL(kbench<1>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      else hipLaunchKernelGGL(kbench<2>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      double muls = (double)blocks * threads * iters * 4;
+      if (rep) printf("variant %d throughput: %.1f G Fq-mul/s (%.2f ms)\n", v, muls / ms / 1e6, ms);
+    }
+    hipEventRecord(a);
+    if (v == 0) hipLaunchKernelGGL(klat<0>, dim3(1), dim3(1), 0, 0, d, 10000);
+    else if (v == 1) hipLaunchKernelGGL(klat<1>, dim3(1), dim3(1), 0, 0, d, 10000);
+    else hipLaunchKernelGGL(klat<2>, dim3(1), dim3(1), 0, 0, d, 10000);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("variant %d single-lane latency: %.1f ns / mul\n", v, ms * 1e6 / 10000);
+  }
+  return 0;
+}
+

@@ -3,8 +3,8 @@
 // Replaces the ffjavascript/wasmcurves Fq/Fr kernels (reference dependency ffjavascript
 // ^0.2.63, package.json:44; used by `snarkjs groth16 prove`, tests/full_system_simulation.mjs:773).
 // Representation: little-endian 32-bit limbs, values kept fully reduced (< p) between
-// operations.  Montgomery multiplication is CIOS with v_mad_u64_u32 (32x32+64 -> 64) carry
-// chains; both moduli are 254-bit so the 9-limb accumulator never overflows.
+// operations.  Montgomery multiplication is product scanning (FIPS) on v_mad_u64_u32 with the
+// column carry routed through VCC (see fp_mul).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -136,37 +136,51 @@ ZK_DEV Fp<PR> fp_dbl(const Fp<PR>& a) {
   return fp_add<PR>(a, a);
 }
 
-// Montgomery multiplication, CIOS.  a, b < p  ->  a*b*2^-256 mod p, < p.
+// Montgomery multiplication, finely integrated product scanning (FIPS).  a, b < p  ->
+// a*b*2^-256 mod p, < p.  Column sums are accumulated in a 3-word register triple
+// (lo:64 | hi:32): each 32x32 product is ONE v_mad_u64_u32 whose 64-bit addend is the running
+// column and whose carry-out goes through VCC into `hi` (v_addc_co_u32).  The compiler's own
+// lowering of the same C++ needs a v_cmp + v_cndmask per product and ~270 v_mov per multiply
+// for 64-bit zero-extension; measured on MI355X (tools/fp_microbench.hip): 124 vs 94 G Fq-mul/s
+// at full occupancy, 0.86 vs 1.34 us single-lane latency.  Both moduli are 254-bit so the
+// column accumulator never exceeds 3 words.
+#define ZK_MAC_VV(lo, hi, x, y) \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "v"(y) : "vcc")
+#define ZK_MAC_VS(lo, hi, x, y) \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "s"(y) : "vcc")
+
 template <class PR>
 ZK_DEV Fp<PR> fp_mul(const Fp<PR>& a, const Fp<PR>& b) {
-  uint32_t t[9];
-#pragma unroll
-  for (int i = 0; i < 9; i++) t[i] = 0;
+  uint32_t m[8], u[9];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    uint64_t c = 0;
-    const uint32_t bi = b.v[i];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      c = (uint64_t)a.v[j] * bi + t[j] + c;
-      t[j] = (uint32_t)c;
-      c >>= 32;
+    for (int j = 0; j < i; j++) {
+      ZK_MAC_VV(lo, hi, a.v[j], b.v[i - j]);
+      ZK_MAC_VS(lo, hi, m[j], PR::P[i - j]);
     }
-    uint32_t t8 = t[8] + (uint32_t)c;  // < 2^32 (accumulator < 2^287)
-    const uint32_t m = t[0] * PR::INV;
-    c = ((uint64_t)m * PR::P[0] + t[0]) >> 32;
-#pragma unroll
-    for (int j = 1; j < 8; j++) {
-      c = (uint64_t)m * PR::P[j] + t[j] + c;
-      t[j - 1] = (uint32_t)c;
-      c >>= 32;
-    }
-    c += t8;
-    t[7] = (uint32_t)c;
-    t[8] = (uint32_t)(c >> 32);
+    ZK_MAC_VV(lo, hi, a.v[i], b.v[0]);
+    m[i] = (uint32_t)lo * PR::INV;
+    ZK_MAC_VS(lo, hi, m[i], PR::P[0]);
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
   }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) {
+      ZK_MAC_VV(lo, hi, a.v[j], b.v[i - j]);
+      ZK_MAC_VS(lo, hi, m[j], PR::P[i - j]);
+    }
+    u[i - 8] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  u[8] = (uint32_t)lo;
   Fp<PR> r;
-  fp_reduce_once<PR>(r.v, t);
+  fp_reduce_once<PR>(r.v, u);
   return r;
 }
 
