@@ -68,11 +68,14 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
 // Per-MSM kernels
 // ---------------------------------------------------------------------------
 // Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31.
-static __global__ void k_msm_digits(const uint32_t* __restrict__ scalars, size_t n,
-                             uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+static __global__ void k_msm_digits(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra,
+                                    const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t n,
+                                    uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4* sp = reinterpret_cast<const uint4*>(scalars + i * 8);
+  const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
+  const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
+  const uint4* sp = reinterpret_cast<const uint4*>(src);
   uint4 a = sp[0], b = sp[1];
   uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t carry = 0;
@@ -204,20 +207,28 @@ __global__ void __launch_bounds__(64) k_msm_sum8(const XYZZ<F>* __restrict__ in,
 template <class F>
 hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n) {
   b.n = n;
-  ZK_CHECK(hipMalloc(&b.bases_w, n * MSM_W * sizeof(Affine<F>)));
+  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * MSM_W * sizeof(Affine<F>)));
   return hipSuccess;
 }
 
 template <class F>
 void msm_bases_free(MsmBases<F>& b) {
   if (b.bases_w) (void)hipFree(b.bases_w);
+  if (b.sidx) (void)hipFree(b.sidx);
   b = MsmBases<F>();
 }
 
-// Expand n affine bases (device pointer) into the window table.
+// Expand b.n affine bases (device pointer) into the window table; h_sidx (host, b.n entries)
+// is the scalar index map or nullptr for identity.
 template <class F>
-hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, hipStream_t st) {
-  hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
+hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_t* h_sidx, uint32_t extra_start,
+                         hipStream_t st) {
+  b.extra_start = extra_start;
+  if (h_sidx && b.n) {
+    ZK_CHECK(hipMalloc(&b.sidx, b.n * sizeof(uint32_t)));
+    ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  }
+  if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
   return hipGetLastError();
 }
 
@@ -260,16 +271,25 @@ void msm_scratch_free(MsmScratch<F>& s) {
 
 // One MSM: n = b.n standard-form scalars (8 x u32, device) -> *d_out (device XYZZ).
 template <class F>
-hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_scalars, XYZZ<F>* d_out,
-                   hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
+__global__ void k_msm_set_inf(XYZZ<F>* out) {
+  *out = xyzz_inf<F>();
+}
+
+template <class F>
+hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_scalars, const uint32_t* d_extra,
+                   XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
   if (b.n > pl.cap) return hipErrorInvalidValue;
+  if (b.n == 0) {
+    hipLaunchKernelGGL(k_msm_set_inf<F>, dim3(1), dim3(1), 0, st, d_out);
+    return hipGetLastError();
+  }
   const size_t m = b.n * MSM_W;
   const size_t max_tasks = m / MSM_L + MSM_NB + 1;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
   if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, b.n, pl.keys_in,
-                     pl.vals_in);
+  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
+                     b.extra_start, b.n, pl.keys_in, pl.vals_in);
   ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
                                      st));
   ZK_CHECK(hipMemsetAsync(pl.bstart, 0, MSM_NB * sizeof(uint32_t), st));
@@ -324,17 +344,18 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
 // Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
 #define ZKFL_MSM_DEFINE(SUF, F)                                                                          \
   hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n) { return msm_bases_alloc(b, n); }           \
-  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, hipStream_t st) {                 \
-    return msm_bases_set(b, src, st);                                                                    \
+  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,          \
+                                 uint32_t extra_start, hipStream_t st) {                                 \
+    return msm_bases_set(b, src, h_sidx, extra_start, st);                                               \
   }                                                                                                      \
   void msm_bases_free_##SUF(MsmBases<F>& b) { msm_bases_free(b); }                                       \
   hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st) {                     \
     return msm_scratch_alloc(s, cap, st);                                                                \
   }                                                                                                      \
   void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
-  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* sc, XYZZ<F>* out,      \
-                           hipStream_t st, Profiler* prof, const char* tag) {                            \
-    return msm_run(b, s, sc, out, st, prof, tag);                                                        \
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* sc, const uint32_t* ex, \
+                           XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag) {              \
+    return msm_run(b, s, sc, ex, out, st, prof, tag);                                                    \
   }
 
 }  // namespace zkfl

@@ -17,10 +17,15 @@ constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every buck
 
 
 // Read-only, per proving key: every base expanded into its W window copies.
+// Bases are compacted at key load (infinity points dropped); sidx[i] maps compacted base i to
+// its scalar: sidx < extra_start -> scalars_main[sidx], else scalars_extra[sidx - extra_start]
+// (the proof's 1 / r / s / -rs blinding slots).  sidx == nullptr means identity.
 template <class F>
 struct MsmBases {
-  size_t n = 0;                  // number of bases (including augmentation slots)
+  size_t n = 0;                  // number of (compacted) bases incl. augmentation slots
   Affine<F>* bases_w = nullptr;  // [n][W] expanded affine bases (device)
+  uint32_t* sidx = nullptr;      // [n] scalar index map (device) or nullptr
+  uint32_t extra_start = 0xFFFFFFFFu;
 };
 
 // Mutable, per in-flight proof (one stream at a time): sort/bucket/reduction scratch.
@@ -50,12 +55,13 @@ struct MsmScratch {
 
 #define ZKFL_MSM_DECLARE(SUF, F)                                                                  \
   hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                     \
-  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, hipStream_t st);           \
+  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,    \
+                                 uint32_t extra_start, hipStream_t st);                            \
   void msm_bases_free_##SUF(MsmBases<F>& b);                                                      \
   hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st);               \
   void msm_scratch_free_##SUF(MsmScratch<F>& s);                                                  \
-  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* scalars, XYZZ<F>* out, \
-                           hipStream_t st, Profiler* prof, const char* tag);
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* scalars,            \
+                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
 
 ZKFL_MSM_DECLARE(g1, FqOps)
 ZKFL_MSM_DECLARE(g2, Fq2Ops)

@@ -147,20 +147,18 @@ __global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h)
   h[j] = fp_from_mont(v);
 }
 
-// Augmented scalar slots: A: [.., 1, r], B: [.., 1, s], C: [.., -r s].  plain -> zeros.
-__global__ void k_set_rs(const Fr* __restrict__ rs, Fr* __restrict__ wA, Fr* __restrict__ wB, Fr* __restrict__ wC,
-                         size_t nVars, size_t nC, int plain) {
+// Blinding scalar slots referenced by the compacted bases' index maps (std form):
+// extra = [1, r, s, -r*s].  plain -> all zero (parity hook: pure MSMs).
+__global__ void k_set_extra(const Fr* __restrict__ rs, Fr* __restrict__ extra, int plain) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Fr one = fp_zero<FrP>();
   one.v[0] = plain ? 0u : 1u;
   Fr r = plain ? fp_zero<FrP>() : rs[0];
   Fr s = plain ? fp_zero<FrP>() : rs[1];
-  wA[nVars] = one;
-  wA[nVars + 1] = r;
-  wB[nVars] = one;
-  wB[nVars + 1] = s;
-  Fr mrs = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
-  wC[nC] = mrs;
+  extra[0] = one;
+  extra[1] = r;
+  extra[2] = s;
+  extra[3] = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
 }
 
 template <class F>
@@ -297,9 +295,7 @@ struct ProofSlot {
   hipEvent_t ev_ready = nullptr, ev_ab = nullptr, ev_b2 = nullptr, ev_t = nullptr, ev_done = nullptr;
   MsmScratch<FqOps> g1s;
   MsmScratch<Fq2Ops> g2s;
-  Fr* wA = nullptr;   // [nVars+2]
-  Fr* wB = nullptr;   // [nVars+2]
-  Fr* wC = nullptr;   // [nC+1]
+  Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs
   Fr* abc = nullptr;  // [3n]
   Fr* h = nullptr;    // [n]
   G1P* res = nullptr;     // [5]: A', B1', C', H, T
@@ -342,7 +338,7 @@ void slot_release(ProofSlot* s) {
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s);
   msm_scratch_free_g2(s->g2s);
-  void* ptrs[] = {s->wA, s->wB, s->wC, s->abc, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
+  void* ptrs[] = {s->extra, s->abc, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -357,7 +353,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ProofSlot* s = new ProofSlot();
   *out = s;
   const size_t nV = k->nVars, n = k->n;
-  const size_t cap1 = std::max<size_t>({nV + 2, k->nC + 1, (size_t)n});
+  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
@@ -365,10 +361,9 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
-  ZK_CHECK(msm_scratch_alloc_g2(s->g2s, nV + 2, st));
-  ZK_CHECK(hipMalloc(&s->wA, (nV + 2) * 32));
-  ZK_CHECK(hipMalloc(&s->wB, (nV + 2) * 32));
-  ZK_CHECK(hipMalloc(&s->wC, (k->nC + 1) * 32));
+  ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
+  (void)nV;
+  ZK_CHECK(hipMalloc(&s->extra, 4 * 32));
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
   ZK_CHECK(hipMalloc(&s->h, n * 32));
   ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
@@ -443,19 +438,19 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   memcpy(s->pinned + 256, rs_host, 64);
   int pp = prof->begin("prove", st);
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
-  HIP_TRY(hipMemcpyAsync(s->wA, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wA");
-  HIP_TRY(hipMemcpyAsync(s->wB, d_w, nV * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wB");
-  if (k->nC) HIP_TRY(hipMemcpyAsync(s->wC, d_w + k->nPub + 1, k->nC * sizeof(Fr), hipMemcpyDeviceToDevice, st), "wC");
-  hipLaunchKernelGGL(k_set_rs, dim3(1), dim3(1), 0, st, s->d_rs, s->wA, s->wB, s->wC, nV, k->nC, plain);
+  hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain);
+  (void)nV;
+  const uint32_t* W = (const uint32_t*)d_w;
+  const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   // G2 stream
   HIP_TRY(hipStreamWaitEvent(s->st_g2, s->ev_ready, 0), "wait");
-  HIP_TRY(msm_run_g2(k->bB2, s->g2s, (const uint32_t*)s->wB, s->resB2, s->st_g2, prof, "msm_accumulate_g2"), "msm B2");
+  HIP_TRY(msm_run_g2(k->bB2, s->g2s, W, E, s->resB2, s->st_g2, prof, "msm_accumulate_g2"), "msm B2");
   if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, s->st_g2, s->resB2, s->d_proof);
   HIP_TRY(hipEventRecord(s->ev_b2, s->st_g2), "event");
   // main: A, B1 first so the assembly chain can start early
-  HIP_TRY(msm_run_g1(k->bA, s->g1s, (const uint32_t*)s->wA, s->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
-  HIP_TRY(msm_run_g1(k->bB1, s->g1s, (const uint32_t*)s->wB, s->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(msm_run_g1(k->bA, s->g1s, W, E, s->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
+  HIP_TRY(msm_run_g1(k->bB1, s->g1s, W, E, s->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
   HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
   if (!plain) {
     HIP_TRY(hipStreamWaitEvent(s->st_asm, s->ev_ab, 0), "wait");
@@ -470,8 +465,8 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
   prof->end(pi, st, 3.0 * (double)n);
   hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
-  HIP_TRY(msm_run_g1(k->bH, s->g1s, (const uint32_t*)s->h, s->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
-  HIP_TRY(msm_run_g1(k->bC, s->g1s, (const uint32_t*)s->wC, s->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
+  HIP_TRY(msm_run_g1(k->bH, s->g1s, (const uint32_t*)s->h, nullptr, s->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
+  HIP_TRY(msm_run_g1(k->bC, s->g1s, W, E, s->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (!plain) {
     HIP_TRY(hipStreamWaitEvent(st, s->ev_t, 0), "wait");
@@ -493,16 +488,26 @@ int wait_slot(ProofSlot* s, uint8_t* proof_out) {
 
 hipError_t msm_run_any(const MsmBases<FqOps>& b, MsmScratch<FqOps>& s, const uint32_t* sc, G1P* o, hipStream_t st,
                        Profiler* p) {
-  return msm_run_g1(b, s, sc, o, st, p, "msm_accumulate_g1");
+  return msm_run_g1(b, s, sc, nullptr, o, st, p, "msm_accumulate_g1");
 }
 hipError_t msm_run_any(const MsmBases<Fq2Ops>& b, MsmScratch<Fq2Ops>& s, const uint32_t* sc, G2P* o, hipStream_t st,
                        Profiler* p) {
-  return msm_run_g2(b, s, sc, o, st, p, "msm_accumulate_g2");
+  return msm_run_g2(b, s, sc, nullptr, o, st, p, "msm_accumulate_g2");
 }
 hipError_t bases_alloc_any(MsmBases<FqOps>& b, size_t n) { return msm_bases_alloc_g1(b, n); }
 hipError_t bases_alloc_any(MsmBases<Fq2Ops>& b, size_t n) { return msm_bases_alloc_g2(b, n); }
-hipError_t bases_set_any(MsmBases<FqOps>& b, const G1Aff* src, hipStream_t st) { return msm_bases_set_g1(b, src, st); }
-hipError_t bases_set_any(MsmBases<Fq2Ops>& b, const G2Aff* src, hipStream_t st) { return msm_bases_set_g2(b, src, st); }
+hipError_t bases_set_any(MsmBases<FqOps>& b, const G1Aff* src, hipStream_t st) {
+  return msm_bases_set_g1(b, src, nullptr, 0xFFFFFFFFu, st);
+}
+hipError_t bases_set_any(MsmBases<Fq2Ops>& b, const G2Aff* src, hipStream_t st) {
+  return msm_bases_set_g2(b, src, nullptr, 0xFFFFFFFFu, st);
+}
+hipError_t bases_set_map_any(MsmBases<FqOps>& b, const void* src, const uint32_t* hs, uint32_t x, hipStream_t st) {
+  return msm_bases_set_g1(b, (const G1Aff*)src, hs, x, st);
+}
+hipError_t bases_set_map_any(MsmBases<Fq2Ops>& b, const void* src, const uint32_t* hs, uint32_t x, hipStream_t st) {
+  return msm_bases_set_g2(b, (const G2Aff*)src, hs, x, st);
+}
 void bases_free_any(MsmBases<FqOps>& b) { msm_bases_free_g1(b); }
 void bases_free_any(MsmBases<Fq2Ops>& b) { msm_bases_free_g2(b); }
 hipError_t scratch_alloc_any(MsmScratch<FqOps>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g1(s, n, st); }
@@ -747,42 +752,59 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
     KTRY(hipMemcpyAsync(k->coefs, coefs.data(), (size_t)ncoef * 32, hipMemcpyHostToDevice, st), "upload");
   }
-  // MSM bases with augmentation slots (alpha1/delta1 on A, beta1/delta1 on B1, beta2/delta2 on B2,
-  // delta1 on C), expanded per window
-  KTRY(msm_bases_alloc_g1(k->bA, (size_t)nVars + 2), "bases A");
-  KTRY(msm_bases_alloc_g1(k->bB1, (size_t)nVars + 2), "bases B1");
-  KTRY(msm_bases_alloc_g2(k->bB2, (size_t)nVars + 2), "bases B2");
-  KTRY(msm_bases_alloc_g1(k->bC, nC + 1), "bases C");
-  KTRY(msm_bases_alloc_g1(k->bH, dom), "bases H");
+  // MSM bases: infinity points dropped (e.g. ~1/3 of B1/B2 for Poseidon-heavy circuits: x^4
+  // wires never appear in B), plus augmentation slots alpha1/delta1 (A), beta1/delta1 (B1),
+  // beta2/delta2 (B2), delta1 (C) whose scalars are the proof's extra = [1, r, s, -rs]
+  // (index map: extra_start = nVars).
   {
     const uint8_t* alpha1 = pts;
     const uint8_t* beta1 = pts + 64;
     const uint8_t* beta2 = pts + 128;
     const uint8_t* delta1 = pts + 384;
     const uint8_t* delta2 = pts + 448;
-    size_t maxb = ((size_t)nVars + 2) * 128;
-    if ((size_t)dom * 64 > maxb) maxb = (size_t)dom * 64;
-    uint8_t* d_tmp = nullptr;
-    KTRY(hipMalloc(&d_tmp, maxb), "alloc tmp");
-    auto upload_g1 = [&](MsmBases<FqOps>& mb, const uint8_t* sec, size_t cnt, const uint8_t* x0,
-                         const uint8_t* x1) -> hipError_t {
-      hipError_t e = hipMemcpyAsync(d_tmp, sec, cnt * 64, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess && x0) e = hipMemcpyAsync(d_tmp + cnt * 64, x0, 64, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess && x1) e = hipMemcpyAsync(d_tmp + (cnt + 1) * 64, x1, 64, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) e = msm_bases_set_g1(mb, (const G1Aff*)d_tmp, st);
+    const uint32_t X = nVars;  // extra_start
+    auto nonzero = [](const uint8_t* p, size_t len) {
+      for (size_t i = 0; i < len; i++)
+        if (p[i]) return true;
+      return false;
+    };
+    struct Aug {
+      const uint8_t* pt;
+      uint32_t sidx;
+    };
+    // Build the compacted (host) base image + index map, upload, expand.
+    auto build = [&](auto& mb, size_t psz, const uint8_t* sec, size_t cnt, uint32_t scalar_off,
+                     std::initializer_list<Aug> aug, bool identity) -> hipError_t {
+      std::vector<uint8_t> img;
+      std::vector<uint32_t> sidx;
+      img.reserve((cnt + aug.size()) * psz);
+      sidx.reserve(cnt + aug.size());
+      for (size_t i = 0; i < cnt; i++) {
+        const uint8_t* p = sec + i * psz;
+        if (!identity && !nonzero(p, psz)) continue;
+        img.insert(img.end(), p, p + psz);
+        sidx.push_back(scalar_off + (uint32_t)i);
+      }
+      for (const Aug& a : aug) {
+        img.insert(img.end(), a.pt, a.pt + psz);
+        sidx.push_back(a.sidx);
+      }
+      hipError_t e = bases_alloc_any(mb, sidx.size());
+      if (e != hipSuccess || sidx.empty()) return e;
+      void* d_img = nullptr;
+      e = hipMalloc(&d_img, img.size());
+      if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
+      const uint32_t* hs = identity ? nullptr : sidx.data();
+      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, X, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (d_img) (void)hipFree(d_img);
       return e;
     };
-    hipError_t e = upload_g1(k->bA, buf + s[5].off, nVars, alpha1, delta1);
-    if (e == hipSuccess) e = upload_g1(k->bB1, buf + s[6].off, nVars, beta1, delta1);
-    if (e == hipSuccess) e = upload_g1(k->bC, buf + s[8].off, nC, delta1, nullptr);
-    if (e == hipSuccess) e = upload_g1(k->bH, buf + s[9].off, dom, nullptr, nullptr);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp, buf + s[7].off, (size_t)nVars * 128, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + (size_t)nVars * 128, beta2, 128, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_tmp + ((size_t)nVars + 1) * 128, delta2, 128, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = msm_bases_set_g2(k->bB2, (const G2Aff*)d_tmp, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(d_tmp);
+    hipError_t e = build(k->bA, 64, buf + s[5].off, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
+    if (e == hipSuccess) e = build(k->bB1, 64, buf + s[6].off, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false);
+    if (e == hipSuccess) e = build(k->bB2, 128, buf + s[7].off, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false);
+    if (e == hipSuccess) e = build(k->bC, 64, buf + s[8].off, nC, nPub + 1, {{delta1, X + 3}}, false);
+    if (e == hipSuccess) e = build(k->bH, 64, buf + s[9].off, dom, 0, {}, true);
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
