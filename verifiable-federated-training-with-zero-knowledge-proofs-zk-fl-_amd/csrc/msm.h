@@ -223,7 +223,8 @@ void msm_bases_free(MsmBases<F>& b) {
 template <class F>
 hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_t* h_sidx, uint32_t extra_start,
                          hipStream_t st) {
-  b.extra_start = extra_start;
+  // identity maps never address the extra slots (H has domainSize > nVars entries on small circuits)
+  b.extra_start = h_sidx ? extra_start : 0xFFFFFFFFu;
   if (h_sidx && b.n) {
     ZK_CHECK(hipMalloc(&b.sidx, b.n * sizeof(uint32_t)));
     ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));

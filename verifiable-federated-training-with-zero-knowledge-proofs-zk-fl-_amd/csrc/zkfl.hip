@@ -795,7 +795,7 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       e = hipMalloc(&d_img, img.size());
       if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
       const uint32_t* hs = identity ? nullptr : sidx.data();
-      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, X, st);
+      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, identity ? 0xFFFFFFFFu : X, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (d_img) (void)hipFree(d_img);
       return e;
