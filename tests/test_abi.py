@@ -33,3 +33,21 @@ def test_version_and_error_paths_without_device():
     # null-argument paths return ZKFL_E_ARG without touching a device
     assert L.zkfl_key_info(None, None, None, None) == -1
     assert L.zkfl_ctx_set_profiling(None, 1) == -1
+
+
+def test_node_addon_loads():
+    """N-API addon (node/zkfl.node) loads in Node and exposes the binding (no GPU calls)."""
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    addon = os.path.join(os.path.dirname(native.LIB_PATH), "node", "zkfl.node")
+    if not node or not os.path.exists(addon):
+        import pytest
+        pytest.skip("node or addon not available")
+    js = ("const a=require(process.argv[1]);"
+          "const k=['version','deviceCount','createContext','loadKey','keyInfo','prove'];"
+          "for (const f of k) if (typeof a[f] !== 'function') throw new Error(f);"
+          "console.log(a.version());")
+    out = subprocess.run([node, "-e", js, addon], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "1"

@@ -285,3 +285,28 @@ def test_resident_batch_and_errors(gpu_ctx):
     for w in ws:
         w.close()
     key.close()
+
+
+def test_node_snarkjs_cli_prove(gpu_ctx, tmp_path):
+    """`node snarkjs_shim.js groth16 prove zkey wtns proof.json public.json` — the reference's
+    execSync line (tests/full_system_simulation.mjs:773-776) through N-API -> C ABI -> HIP."""
+    import shutil
+    import subprocess
+    from zkfl import native, zkey
+    node = shutil.which("node")
+    shim = os.path.join(os.path.dirname(native.LIB_PATH), "node", "snarkjs_shim.js")
+    if not node or not os.path.exists(os.path.join(os.path.dirname(shim), "zkfl.node")):
+        pytest.skip("node / addon not available")
+    b, zk = _setup(gpu_ctx, "poseidon_hash2")
+    w = b.witness({"left": 11, "right": 22})
+    (tmp_path / "c_final.zkey").write_bytes(zk)
+    (tmp_path / "w.wtns").write_bytes(zkey.wtns_bytes(w))
+    out = subprocess.run([node, shim, "groth16", "prove", "c_final.zkey", "w.wtns", "proof.json", "public.json"],
+                         cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    proof = json.load(open(tmp_path / "proof.json"))
+    pub = json.load(open(tmp_path / "public.json"))
+    assert proof["protocol"] == "groth16" and proof["curve"] == "bn128"
+    assert pub == [str(w[1])]
+    from zkfl.groth16 import proof_from_json
+    assert _verify_bytes(og.parse_zkey(zk), proof_from_json(proof), [int(x) for x in pub])

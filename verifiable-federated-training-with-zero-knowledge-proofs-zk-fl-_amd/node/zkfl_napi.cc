@@ -1,0 +1,192 @@
+// N-API binding of libzkfl (include/zkfl.h) for a Node.js host.
+//
+// Replaces the child-process boundary of the reference harness
+// (`execSync("npx snarkjs groth16 prove ...")`, tests/full_system_simulation.mjs:773-776):
+// a Node process loads the proving key once and proves in-process.  Proving runs on a libuv
+// worker thread (napi_create_async_work) so the event loop is not blocked, and resolves a
+// Promise like snarkjs's `groth16.prove`.
+//
+// JS surface (see snarkjs_shim.js):
+//   version() -> number
+//   deviceCount() -> number
+//   createContext(device) -> ctx
+//   loadKey(ctx, zkeyBuffer) -> key                       (zkfl_zkey_load)
+//   keyInfo(key) -> {nVars, nPublic, domainSize}
+//   prove(ctx, key, wtnsBuffer[, rsBuffer]) -> Promise<{proof: Buffer(256), publicSignals: Buffer}>
+#include <node_api.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "zkfl.h"
+
+namespace {
+
+napi_value throw_err(napi_env env, int rc) {
+  std::string msg = std::string("zkfl error ") + std::to_string(rc) + ": " + zkfl_last_error();
+  napi_throw_error(env, nullptr, msg.c_str());
+  return nullptr;
+}
+
+napi_value Version(napi_env env, napi_callback_info) {
+  napi_value v;
+  napi_create_int32(env, zkfl_version(), &v);
+  return v;
+}
+
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+  int c = 0;
+  zkfl_device_count(&c);
+  napi_value v;
+  napi_create_int32(env, c, &v);
+  return v;
+}
+
+void ctx_finalize(napi_env, void* data, void*) { zkfl_ctx_destroy(static_cast<zkfl_ctx*>(data)); }
+void key_finalize(napi_env, void* data, void*) { zkfl_key_free(static_cast<zkfl_key*>(data)); }
+
+napi_value CreateContext(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  int32_t dev = 0;
+  if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
+  zkfl_ctx* ctx = nullptr;
+  int rc = zkfl_ctx_create(dev, &ctx);
+  if (rc) return throw_err(env, rc);
+  napi_value ext;
+  napi_create_external(env, ctx, ctx_finalize, nullptr, &ext);
+  return ext;
+}
+
+napi_value LoadKey(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void* ctx = nullptr;
+  void* data = nullptr;
+  size_t len = 0;
+  if (argc < 2 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &data, &len) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "loadKey(ctx, zkeyBuffer)");
+    return nullptr;
+  }
+  zkfl_key* key = nullptr;
+  int rc = zkfl_zkey_load(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(data), len, &key);
+  if (rc) return throw_err(env, rc);
+  napi_value ext;
+  napi_create_external(env, key, key_finalize, nullptr, &ext);
+  return ext;
+}
+
+napi_value KeyInfo(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void* key = nullptr;
+  if (argc < 1 || napi_get_value_external(env, argv[0], &key) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "keyInfo(key)");
+    return nullptr;
+  }
+  uint32_t nv = 0, np = 0, dom = 0;
+  int rc = zkfl_key_info(static_cast<zkfl_key*>(key), &nv, &np, &dom);
+  if (rc) return throw_err(env, rc);
+  napi_value obj, a, b, c;
+  napi_create_object(env, &obj);
+  napi_create_uint32(env, nv, &a);
+  napi_create_uint32(env, np, &b);
+  napi_create_uint32(env, dom, &c);
+  napi_set_named_property(env, obj, "nVars", a);
+  napi_set_named_property(env, obj, "nPublic", b);
+  napi_set_named_property(env, obj, "domainSize", c);
+  return obj;
+}
+
+struct ProveWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  zkfl_ctx* ctx = nullptr;
+  zkfl_key* key = nullptr;
+  std::vector<uint8_t> wtns, rs;
+  uint8_t proof[256];
+  std::vector<uint8_t> pub;
+  size_t npub = 0;
+  int rc = 0;
+  std::string err;
+};
+
+void prove_execute(napi_env, void* data) {
+  ProveWork* w = static_cast<ProveWork*>(data);
+  uint32_t nv = 0, np = 0, dom = 0;
+  zkfl_key_info(w->key, &nv, &np, &dom);
+  w->pub.resize((size_t)np * 32 + 32);
+  w->rc = zkfl_groth16_prove(w->ctx, w->key, w->wtns.data(), w->wtns.size(), w->rs.empty() ? nullptr : w->rs.data(),
+                             w->proof, w->pub.data(), &w->npub);
+  if (w->rc) w->err = zkfl_last_error();
+}
+
+void prove_complete(napi_env env, napi_status, void* data) {
+  ProveWork* w = static_cast<ProveWork*>(data);
+  if (w->rc) {
+    napi_value msg, err;
+    std::string m = "zkfl prove failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_reject_deferred(env, w->deferred, err);
+  } else {
+    napi_value obj, proof, pub;
+    void* p;
+    napi_create_buffer_copy(env, 256, w->proof, &p, &proof);
+    napi_create_buffer_copy(env, w->npub * 32, w->pub.data(), &p, &pub);
+    napi_create_object(env, &obj);
+    napi_set_named_property(env, obj, "proof", proof);
+    napi_set_named_property(env, obj, "publicSignals", pub);
+    napi_resolve_deferred(env, w->deferred, obj);
+  }
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value Prove(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *key = nullptr, *wt = nullptr, *rs = nullptr;
+  size_t wlen = 0, rslen = 0;
+  if (argc < 3 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_value_external(env, argv[1], &key) != napi_ok ||
+      napi_get_buffer_info(env, argv[2], &wt, &wlen) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "prove(ctx, key, wtnsBuffer[, rsBuffer])");
+    return nullptr;
+  }
+  ProveWork* w = new ProveWork();
+  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->key = static_cast<zkfl_key*>(key);
+  w->wtns.assign(static_cast<uint8_t*>(wt), static_cast<uint8_t*>(wt) + wlen);
+  if (argc >= 4 && napi_get_buffer_info(env, argv[3], &rs, &rslen) == napi_ok && rslen == 64)
+    w->rs.assign(static_cast<uint8_t*>(rs), static_cast<uint8_t*>(rs) + 64);
+  napi_value promise, name;
+  napi_create_promise(env, &w->deferred, &promise);
+  napi_create_string_utf8(env, "zkfl_prove", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, nullptr, name, prove_execute, prove_complete, w, &w->work);
+  napi_queue_async_work(env, w->work);
+  return promise;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"loadKey", nullptr, LoadKey, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"keyInfo", nullptr, KeyInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)
