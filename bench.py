@@ -48,6 +48,64 @@ def cpu_baseline_leg(zk: bytes, wt: bytes, seconds_budget=20.0):
     return cbaseline.time_prove(zk, wt, seconds_budget)
 
 
+def timed_run(key, warm_w, steps_w, ctx, dist):
+    """W untimed proofs, then exactly K timed proofs bracketed by barrier + synchronize on both
+    sides; returns (max-over-ranks elapsed seconds, proofs, per-kernel profile)."""
+
+    def barrier_sync():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            dist.barrier()
+
+    if warm_w:
+        key.prove_batch(warm_w)
+    ctx.profile_reset()
+    ctx.set_profiling(True)
+    barrier_sync()
+    t_start = time.perf_counter()
+    proofs = key.prove_batch(steps_w)          # K proofs, `slots` in flight
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    ctx.set_profiling(False)
+    prof = {k: ctx.profile(k) for k in ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")}
+    if dist is not None:
+        import torch
+        dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, proofs, prof
+
+
+def report(args, world, elapsed, prof, config, cpu):
+    """The one JSON line (rank 0)."""
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.steps / elapsed
+    cand = {k: v for k, v in prof.items() if k in BYTES_PER_ENTRY and v[1] > 0}
+    roofline = None
+    if cand:
+        dom = max(cand, key=lambda k: cand[k][0])
+        ms_tot, launches, units = prof[dom]
+        avg_s = ms_tot / launches / 1e3
+        bytes_per_launch = units / launches * BYTES_PER_ENTRY[dom]
+        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
+                    "entries_per_launch": round(units / launches)}
+    stage_ms = {k: round(v[0] / max(1, args.steps), 3) for k, v in prof.items()}
+    return {
+        "metric": METRIC, "value": round(value, 4), "unit": "proofs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (reference harness seeded client generator)",
+        "config": config, "roofline": roofline, "stage_ms_per_proof": stage_ms, "cpu_baseline": cpu,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,64 +158,18 @@ def main():
     steps_w = [res[i % len(res)] for i in range(args.steps)]
     warm_w = [res[i % len(res)] for i in range(max(args.warmup, args.slots) if args.warmup else 0)]
 
-    def barrier_sync():
-        ctx.synchronize()
-        if dist is not None:
-            import torch
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            dist.barrier()
-
-    if warm_w:
-        key.prove_batch(warm_w)
-    ctx.profile_reset()
-    ctx.set_profiling(True)
-    barrier_sync()
-    t_start = time.perf_counter()
-    proofs = key.prove_batch(steps_w)          # K proofs, `slots` in flight
-    barrier_sync()
-    elapsed = time.perf_counter() - t_start
-    ctx.set_profiling(False)
-
-    prof = {k: ctx.profile(k) for k in ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")}
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed, proofs, prof = timed_run(key, warm_w, steps_w, ctx, dist)
     if rank == 0:
-        ms_per_step = elapsed / args.steps * 1e3
-        value = world * args.steps / elapsed
-        # roofline for the dominant instrumented kernel
-        cand = {k: v for k, v in prof.items() if k in BYTES_PER_ENTRY and v[1] > 0}
-        dom = max(cand, key=lambda k: cand[k][0])
-        ms_tot, launches, units = prof[dom]
-        avg_s = ms_tot / launches / 1e3
-        bytes_per_launch = units / launches * BYTES_PER_ENTRY[dom]
-        achieved = bytes_per_launch / avg_s / 1e9
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
-                    "entries_per_launch": round(units / launches)}
-        stage_ms = {k: round(v[0] / max(1, args.steps), 3) for k, v in prof.items()}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
                 cpu = cpu_baseline_leg(zk, wts[0])
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
-        out = {
-            "metric": METRIC, "value": round(value, 4), "unit": "proofs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (reference harness seeded client generator)",
-            "config": {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
-                       "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
-                       "global_batch": world, "parallelism": f"replicas{world}", "slots_in_flight": args.slots},
-            "roofline": roofline, "stage_ms_per_proof": stage_ms, "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
+        config = {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
+                  "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
+                  "global_batch": world, "parallelism": f"replicas{world}", "slots_in_flight": args.slots}
+        print(json.dumps(report(args, world, elapsed, prof, config, cpu)), flush=True)
     assert len(proofs) == args.steps and all(len(p) == 256 for p in proofs)
     for r_ in res:
         r_.close()

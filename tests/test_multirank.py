@@ -1,0 +1,76 @@
+"""bench.py's N>1 path (barrier, max-over-ranks timing, weak-scaling value, rank-0 report) on
+2 gloo ranks with a stub prover (CPU).  The GPU prover itself is covered by -m gpu tests; the
+multi-GPU path has no data-path collective (independent proofs per rank)."""
+import json
+import os
+import socket
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _StubKey:
+    """Stands in for native.ProvingKey: 'proves' by sleeping a rank-dependent time."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def prove_batch(self, ws):
+        time.sleep(0.01 * (1 + self.rank) * len(ws))
+        return [bytes(256)] * len(ws)
+
+
+class _StubCtx:
+    def synchronize(self):
+        pass
+
+    def profile_reset(self):
+        pass
+
+    def set_profiling(self, on):
+        pass
+
+    def profile(self, name):
+        return (0.0, 0, 0.0)
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    key = _StubKey(rank)
+    elapsed, proofs, prof = bench.timed_run(key, [0], list(range(8)), _StubCtx(), dist)
+
+    class A:
+        steps, warmup, slots = 8, 1, 1
+    if rank == 0:
+        rep = bench.report(A, world, elapsed, prof, {"workload": "stub"}, None)
+        with open(out_path, "w") as f:
+            json.dump(rep, f)
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_gloo_report(tmp_path):
+    torch = pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rep.json")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    rep = json.load(open(out))
+    # the slowest rank (rank 1: 8 * 20 ms) bounds the job; value counts both ranks' proofs
+    assert rep["n_gpus"] == 2 and rep["steps"] == 8 and rep["scaling"] == "weak"
+    assert rep["ms_per_step"] >= 8 * 20 / 8 * 0.9
+    assert abs(rep["value"] - 2 * 8 / (rep["ms_per_step"] * 8 / 1e3)) < 1e-3 * rep["value"] + 1e-6
+    assert rep["metric"].startswith("Groth16 proofs/sec")
