@@ -5,6 +5,40 @@
 #include "field.h"
 using namespace zkfl;
 
+// the original compiler-lowered CIOS (baseline)
+template <class PR>
+__device__ __forceinline__ Fp<PR> cios_mul(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t t[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+    const uint32_t bi = b.v[i];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c = (uint64_t)a.v[j] * bi + t[j] + c;
+      t[j] = (uint32_t)c;
+      c >>= 32;
+    }
+    uint32_t t8 = t[8] + (uint32_t)c;
+    const uint32_t m = t[0] * PR::INV;
+    c = ((uint64_t)m * PR::P[0] + t[0]) >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      c = (uint64_t)m * PR::P[j] + t[j] + c;
+      t[j - 1] = (uint32_t)c;
+      c >>= 32;
+    }
+    c += t8;
+    t[7] = (uint32_t)c;
+    t[8] = (uint32_t)(c >> 32);
+  }
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, t);
+  return r;
+}
+
 template <class PR>
 __device__ __forceinline__ Fp<PR> fips_mul(const Fp<PR>& a, const Fp<PR>& b) {
   uint32_t m[8], u[9];
@@ -73,9 +107,10 @@ __global__ void __launch_bounds__(256) kbench(Fq* data, int iters) {
   Fq x0 = data[i], x1 = data[i + 1], x2 = data[i + 2], x3 = data[i + 3];
   const Fq y = data[0];
   for (int k = 0; k < iters; k++) {
-    if (V == 0) { x0 = fp_mul(x0, y); x1 = fp_mul(x1, y); x2 = fp_mul(x2, y); x3 = fp_mul(x3, y); }
+    if (V == 0) { x0 = cios_mul(x0, y); x1 = cios_mul(x1, y); x2 = cios_mul(x2, y); x3 = cios_mul(x3, y); }
     else if (V == 1) { x0 = fips_mul(x0, y); x1 = fips_mul(x1, y); x2 = fips_mul(x2, y); x3 = fips_mul(x3, y); }
-    else { x0 = fips_mul_vcc(x0, y); x1 = fips_mul_vcc(x1, y); x2 = fips_mul_vcc(x2, y); x3 = fips_mul_vcc(x3, y); }
+    else if (V == 2) { x0 = fips_mul_vcc(x0, y); x1 = fips_mul_vcc(x1, y); x2 = fips_mul_vcc(x2, y); x3 = fips_mul_vcc(x3, y); }
+    else { x0 = fp_mul(x0, y); x1 = fp_mul(x1, y); x2 = fp_mul(x2, y); x3 = fp_mul(x3, y); }
   }
   data[i] = fp_add(fp_add(x0, x1), fp_add(x2, x3));
 }
@@ -85,16 +120,17 @@ template <int V>
 __global__ void klat(Fq* data, int iters) {
   Fq x = data[1];
   const Fq y = data[0];
-  for (int k = 0; k < iters; k++) x = V == 0 ? fp_mul(x, y) : (V == 1 ? fips_mul(x, y) : fips_mul_vcc(x, y));
+  for (int k = 0; k < iters; k++) x = V == 0 ? cios_mul(x, y) : (V == 1 ? fips_mul(x, y) : (V == 2 ? fips_mul_vcc(x, y) : fp_mul(x, y)));
   data[1] = x;
 }
 
 __global__ void kcheck(const Fq* a, const Fq* b, int n, int* bad) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Fq r0 = fp_mul(a[i], b[i]), r1 = fips_mul(a[i], b[i]), r2 = fips_mul_vcc(a[i], b[i]);
+  Fq r0 = cios_mul(a[i], b[i]), r1 = fips_mul(a[i], b[i]), r2 = fips_mul_vcc(a[i], b[i]), r3 = fp_mul(a[i], b[i]);
   if (!fp_eq(r0, r1)) atomicAdd(bad, 1);
   if (!fp_eq(r0, r2)) atomicAdd(bad + 1, 1);
+  if (!fp_eq(r0, r3)) atomicAdd(bad + 2, 1);
 }
 
 int main() {
@@ -113,22 +149,23 @@ int main() {
         st ^= st << 13; st ^= st >> 7; st ^= st << 17;
         h[i].v[j] = (uint32_t)st & (j == 7 ? 0x1fffffffu : 0xffffffffu);
       }
-    Fq* dd; int* bad; int hb[2] = {0, 0};
-    hipMalloc(&dd, 2 * m * sizeof(Fq)); hipMalloc(&bad, 8);
-    hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, 8);
+    Fq* dd; int* bad; int hb[3] = {0, 0, 0};
+    hipMalloc(&dd, 2 * m * sizeof(Fq)); hipMalloc(&bad, 12);
+    hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, 12);
     hipLaunchKernelGGL(kcheck, dim3(m / 256), dim3(256), 0, 0, dd, dd + m, m, bad);
-    hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(hb, bad, 12, hipMemcpyDeviceToHost);
     printf("mismatches vs CIOS: fips_sgpr=%d fips_vcc=%d (of %d)\n", hb[0], hb[1], m);
   }
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int v = 0; v < 3; v++) {
+  for (int v = 0; v < 4; v++) {
     for (int rep = 0; rep < 2; rep++) {
       hipEventRecord(a);
       if (v == 0) hipLaunchKernelGGL(kbench<0>, dim3(blocks), dim3(threads), 0, 0, d, iters);
       else if (v == 1) hipLaunchKernelGGL(kbench<1>, dim3(blocks), dim3(threads), 0, 0, d, iters);
-      else hipLaunchKernelGGL(kbench<2>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      else if (v == 2) hipLaunchKernelGGL(kbench<2>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      else hipLaunchKernelGGL(kbench<3>, dim3(blocks), dim3(threads), 0, 0, d, iters);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
@@ -139,7 +176,8 @@ int main() {
     hipEventRecord(a);
     if (v == 0) hipLaunchKernelGGL(klat<0>, dim3(1), dim3(1), 0, 0, d, 10000);
     else if (v == 1) hipLaunchKernelGGL(klat<1>, dim3(1), dim3(1), 0, 0, d, 10000);
-    else hipLaunchKernelGGL(klat<2>, dim3(1), dim3(1), 0, 0, d, 10000);
+    else if (v == 2) hipLaunchKernelGGL(klat<2>, dim3(1), dim3(1), 0, 0, d, 10000);
+    else hipLaunchKernelGGL(klat<3>, dim3(1), dim3(1), 0, 0, d, 10000);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
