@@ -22,9 +22,10 @@ import sys
 import time
 
 # Each in-flight proof slot drives 3 HIP streams; HIP maps a process's streams onto
-# GPU_MAX_HW_QUEUES hardware queues (default 4), and streams sharing a queue serialize.  Raise it
-# before anything initializes HIP (measured: 4 queues, 3 slots 95 proofs/s -> 24 queues, 8 slots 164 proofs/s).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "24")
+# GPU_MAX_HW_QUEUES hardware queues (HIP default 4, which the GPU boxes also export), and streams
+# sharing a queue serialize.  Set it before anything initializes HIP (measured: 4 queues 87-95
+# proofs/s -> 24 queues, 8 slots 164 proofs/s).  ZKFL_HW_QUEUES overrides the value used here.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "24")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd")

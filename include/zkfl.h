@@ -107,6 +107,27 @@ int zkfl_msm_g2(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, siz
  * (snarkjs ifft + batchApplyKey(inc) + fft). */
 int zkfl_ntt_coset(zkfl_ctx* ctx, uint8_t* data, uint32_t logn);
 
+/* Verification (replaces `snarkjs groth16 verify <vkey> <public> <proof>`,
+ * tests/full_system_simulation.mjs:865-868; snarkjs groth16_verify, restated in
+ * oracle/groth16.py::verify).  vk image (see zkfl/groth16.py::vk_bytes for vkey.json -> bytes):
+ *   nPublic u32 LE | alpha1 (64) | beta2 (128) | gamma2 (128) | delta2 (128) | IC[nPublic+1] (64 each),
+ * standard-form affine LE, G2 as x.c0|x.c1|y.c0|y.c1 (the proof's encoding).  pub: npub x 32 B std.
+ * Returns 1 (valid), 0 (invalid: pairing check fails, a public signal >= r, a proof coordinate
+ * >= q, a point off its curve, pi_b outside the order-r subgroup) or a negative ZKFL_E_* code
+ * (malformed vk, npub != nPublic).  The prepared key is cached in the context. */
+int zkfl_groth16_verify(zkfl_ctx* ctx, const uint8_t* vk, size_t vk_len, const uint8_t* pub, size_t npub,
+                        const uint8_t proof[256]);
+/* n proofs against one key, one GPU lane each: pubs n x npub x 32 B, proofs n x 256 B,
+ * results[i] = 1 / 0.  Returns ZKFL_OK or an error code. */
+int zkfl_groth16_verify_batch(zkfl_ctx* ctx, const uint8_t* vk, size_t vk_len, size_t n, const uint8_t* pubs,
+                              size_t npub, const uint8_t* proofs, int32_t* results);
+/* Optimal-ate pairing e(P_i, Q_i) for n pairs (g1: n x 64 B, g2: n x 128 B, std affine; all-zero
+ * = infinity).  gt_out: n x 384 B, 12 std-form Fq in the ffjavascript Fq12 toObject order
+ * (c0.c0.a, c0.c0.b, c0.c1.a, ... c1.c2.b) -- the layout of vkey.json's vk_alphabeta_12. */
+int zkfl_pairing(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt_out);
+/* Parity hook: the Miller-loop value before the final exponentiation, same layout. */
+int zkfl_debug_miller_loop(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* out);
+
 /* Dev-ceremony fixed-base multiplications: out[i] = scalars[i] * generator, mont affine. */
 int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
 int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);

@@ -47,7 +47,7 @@ def test_wtns_roundtrip():
 def test_vkey_export_fields():
     from zkfl import groth16
     _, zk, tx = _tiny_zkey()
-    vk = groth16.export_verification_key(zk)
+    vk = groth16.export_verification_key(zk, alphabeta=False)
     a = bn.mul(bn.G1_GEN, tx.alpha)
     assert vk["vk_alpha_1"][:2] == [str(a[0]), str(a[1])]
     assert vk["nPublic"] == 1 and len(vk["IC"]) == 2

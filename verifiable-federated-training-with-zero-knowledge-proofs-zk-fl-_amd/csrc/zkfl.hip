@@ -30,6 +30,7 @@
 #include "msm_api.h"
 #include "ntt.h"
 #include "prof.h"
+#include "verify.h"
 #include "zkfl.h"
 
 using namespace zkfl;
@@ -285,8 +286,9 @@ __global__ void k_g2_gen_mont(G2Aff* out) {
 // ---------------------------------------------------------------------------
 struct zkfl_ctx {
   int device = 0;
-  hipStream_t st = nullptr;  // primitives, key loading
+  hipStream_t st = nullptr;  // primitives, key loading, verification
   Profiler prof;
+  VkDev* vk = nullptr;       // last prepared verification key (reused while the vk bytes repeat)
 };
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
@@ -630,6 +632,7 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->st);
   ctx->prof.reset();
+  vk_free(ctx->vk);
   (void)hipStreamDestroy(ctx->st);
   delete ctx;
   return ZKFL_OK;
@@ -1013,6 +1016,59 @@ int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8
 
 int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out) {
   return run_gen_mul<Fq2Ops>(ctx, scalars, n, out, true);
+}
+
+// ---------------------------------------------------------------------------
+// Verification (csrc/verify.hip)
+// ---------------------------------------------------------------------------
+static int vk_get(zkfl_ctx* ctx, const uint8_t* vk, size_t vk_len, size_t npub) {
+  if (!vk_same(ctx->vk, vk, vk_len)) {
+    vk_free(ctx->vk);
+    ctx->vk = nullptr;
+    std::string err;
+    VkDev* p = nullptr;
+    int rc = vk_prepare(vk, vk_len, ctx->st, &p, err);
+    if (rc != ZKFL_OK) return fail(rc, err);
+    ctx->vk = p;
+  }
+  if (vk_npub(ctx->vk) != npub)
+    return fail(ZKFL_E_MISMATCH, "verify: " + std::to_string(npub) + " public signals, key expects " +
+                                     std::to_string(vk_npub(ctx->vk)));
+  return ZKFL_OK;
+}
+
+int zkfl_groth16_verify_batch(zkfl_ctx* ctx, const uint8_t* vk, size_t vk_len, size_t n, const uint8_t* pubs,
+                              size_t npub, const uint8_t* proofs, int32_t* results) {
+  if (!ctx || !vk || (n && (!proofs || !results || (npub && !pubs)))) return fail(ZKFL_E_ARG, "verify: bad args");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  int rc = vk_get(ctx, vk, vk_len, npub);
+  if (rc != ZKFL_OK) return rc;
+  std::string err;
+  rc = verify_batch(ctx->vk, n, pubs, proofs, results, ctx->st, err);
+  return rc == ZKFL_OK ? rc : fail(rc, err);
+}
+
+int zkfl_groth16_verify(zkfl_ctx* ctx, const uint8_t* vk, size_t vk_len, const uint8_t* pub, size_t npub,
+                        const uint8_t proof[256]) {
+  int32_t res = 0;
+  int rc = zkfl_groth16_verify_batch(ctx, vk, vk_len, 1, pub, npub, proof, &res);
+  return rc == ZKFL_OK ? res : rc;
+}
+
+static int pairing_common(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* out, int fe) {
+  if (!ctx || (n && (!g1 || !g2 || !out))) return fail(ZKFL_E_ARG, "pairing: bad args");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  std::string err;
+  int rc = pairing_batch(n, g1, g2, fe, out, ctx->st, err);
+  return rc == ZKFL_OK ? rc : fail(rc, err);
+}
+
+int zkfl_pairing(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt_out) {
+  return pairing_common(ctx, n, g1, g2, gt_out, 1);
+}
+
+int zkfl_debug_miller_loop(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
+  return pairing_common(ctx, n, g1, g2, out, 0);
 }
 
 }  // extern "C"

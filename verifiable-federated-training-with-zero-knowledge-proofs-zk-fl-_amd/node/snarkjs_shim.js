@@ -4,9 +4,12 @@
 // CLI (same argument order and files as the reference's execSync strings,
 // tests/full_system_simulation.mjs:773-776):
 //   node snarkjs_shim.js groth16 prove <circuit_final.zkey> <witness.wtns> <proof.json> <public.json>
+//   node snarkjs_shim.js groth16 verify <verification_key.json> <public.json> <proof.json>
+//     (:865-868; exit 0 + "OK!" when valid, exit 1 + "Invalid proof" otherwise)
 // API (snarkjs shape):
 //   const { groth16 } = require('./snarkjs_shim.js');
 //   const { proof, publicSignals } = await groth16.prove(zkeyFileOrBuffer, wtnsFileOrBuffer);
+//   const ok = await groth16.verify(vKeyObject, publicSignals, proof);
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -50,7 +53,40 @@ async function prove(zkey, wtns) {
   return { proof: proofToJson(r.proof), publicSignals: pub };
 }
 
-module.exports = { groth16: { prove }, addon, proofToJson };
+function decToLe(x) {
+  let v = BigInt(x);
+  const b = Buffer.alloc(32);
+  for (let i = 0; i < 32; i++) { b[i] = Number(v & BigInt(255)); v >>= BigInt(8); }
+  if (v !== BigInt(0)) throw new Error('value does not fit in 256 bits: ' + x);
+  return b;
+}
+
+function g1Buf(p) {
+  if (BigInt(p[2]) === BigInt(0)) return Buffer.alloc(64);
+  return Buffer.concat([decToLe(p[0]), decToLe(p[1])]);
+}
+
+function g2Buf(p) {
+  if (BigInt(p[2][0]) === BigInt(0) && BigInt(p[2][1]) === BigInt(0)) return Buffer.alloc(128);
+  return Buffer.concat([decToLe(p[0][0]), decToLe(p[0][1]), decToLe(p[1][0]), decToLe(p[1][1])]);
+}
+
+// vkey.json -> the C-ABI vk image (include/zkfl.h, zkfl_groth16_verify)
+function vkBuffer(vk) {
+  const n = Buffer.alloc(4);
+  n.writeUInt32LE(vk.nPublic, 0);
+  return Buffer.concat([n, g1Buf(vk.vk_alpha_1), g2Buf(vk.vk_beta_2), g2Buf(vk.vk_gamma_2), g2Buf(vk.vk_delta_2),
+    ...vk.IC.map(g1Buf)]);
+}
+
+async function verify(vk, publicSignals, proof) {
+  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
+  const pr = Buffer.concat([g1Buf(proof.pi_a), g2Buf(proof.pi_b), g1Buf(proof.pi_c)]);
+  const pub = Buffer.concat(publicSignals.map(decToLe).concat([Buffer.alloc(0)]));
+  return addon.verify(ctx, vkBuffer(vk), pub, pr);
+}
+
+module.exports = { groth16: { prove, verify }, addon, proofToJson, vkBuffer };
 
 if (require.main === module) {
   const [cmd, sub, zkeyF, wtnsF, proofF, publicF] = process.argv.slice(2);
@@ -60,10 +96,20 @@ if (require.main === module) {
       fs.writeFileSync(publicF, JSON.stringify(publicSignals, null, 1));
       process.exit(0);
     }).catch((e) => { console.error(e.message); process.exit(1); });
+  } else if (cmd === 'groth16' && sub === 'verify' && proofF) {
+    // argument order: verify <vkey.json> <public.json> <proof.json>
+    const [vkF, pubF, prF] = [zkeyF, wtnsF, proofF];
+    const rd = (f) => JSON.parse(fs.readFileSync(f, 'utf8'));
+    verify(rd(vkF), rd(pubF), rd(prF)).then((ok) => {
+      if (ok) { console.log('[INFO]  snarkJS: OK!'); process.exit(0); }
+      console.error('[ERROR] snarkJS: Invalid proof');
+      process.exit(1);
+    }).catch((e) => { console.error(e.message); process.exit(1); });
   } else if (cmd === 'version') {
     console.log('zkfl ' + addon.version());
   } else {
-    console.error('usage: snarkjs_shim.js groth16 prove <zkey> <wtns> <proof.json> <public.json>');
+    console.error('usage: snarkjs_shim.js groth16 prove <zkey> <wtns> <proof.json> <public.json>\n' +
+                  '       snarkjs_shim.js groth16 verify <vkey.json> <public.json> <proof.json>');
     process.exit(99);
   }
 }

@@ -13,6 +13,7 @@
 //   loadKey(ctx, zkeyBuffer) -> key                       (zkfl_zkey_load)
 //   keyInfo(key) -> {nVars, nPublic, domainSize}
 //   prove(ctx, key, wtnsBuffer[, rsBuffer]) -> Promise<{proof: Buffer(256), publicSignals: Buffer}>
+//   verify(ctx, vkBuffer, publicBuffer, proofBuffer) -> Promise<boolean>   (zkfl_groth16_verify)
 #include <node_api.h>
 
 #include <cstring>
@@ -174,6 +175,67 @@ napi_value Prove(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+struct VerifyWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  zkfl_ctx* ctx = nullptr;
+  std::vector<uint8_t> vk, pub, proof;
+  int rc = 0;
+  std::string err;
+};
+
+void verify_execute(napi_env, void* data) {
+  VerifyWork* w = static_cast<VerifyWork*>(data);
+  w->rc = zkfl_groth16_verify(w->ctx, w->vk.data(), w->vk.size(), w->pub.data(), w->pub.size() / 32,
+                              w->proof.data());
+  if (w->rc < 0) w->err = zkfl_last_error();
+}
+
+void verify_complete(napi_env env, napi_status, void* data) {
+  VerifyWork* w = static_cast<VerifyWork*>(data);
+  if (w->rc < 0) {
+    napi_value msg, err;
+    std::string m = "zkfl verify failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_reject_deferred(env, w->deferred, err);
+  } else {
+    napi_value b;
+    napi_get_boolean(env, w->rc == 1, &b);
+    napi_resolve_deferred(env, w->deferred, b);
+  }
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value Verify(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *vk = nullptr, *pub = nullptr, *pr = nullptr;
+  size_t vlen = 0, plen = 0, prlen = 0;
+  if (argc < 4 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &vk, &vlen) != napi_ok ||
+      napi_get_buffer_info(env, argv[2], &pub, &plen) != napi_ok ||
+      napi_get_buffer_info(env, argv[3], &pr, &prlen) != napi_ok || prlen != 256 || plen % 32) {
+    napi_throw_type_error(env, nullptr, "verify(ctx, vkBuffer, publicBuffer(n x 32), proofBuffer(256))");
+    return nullptr;
+  }
+  VerifyWork* w = new VerifyWork();
+  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->vk.assign(static_cast<uint8_t*>(vk), static_cast<uint8_t*>(vk) + vlen);
+  w->pub.assign(static_cast<uint8_t*>(pub), static_cast<uint8_t*>(pub) + plen);
+  w->pub.resize(plen + 32);  // never empty (data() of an empty vector may be null)
+  w->pub.resize(plen);
+  w->proof.assign(static_cast<uint8_t*>(pr), static_cast<uint8_t*>(pr) + 256);
+  napi_value promise, name;
+  napi_create_promise(env, &w->deferred, &promise);
+  napi_create_string_utf8(env, "zkfl_verify", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, nullptr, name, verify_execute, verify_complete, w, &w->work);
+  napi_queue_async_work(env, w->work);
+  return promise;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -182,6 +244,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"loadKey", nullptr, LoadKey, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"keyInfo", nullptr, KeyInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -49,6 +49,11 @@ SIGNATURES = {
     "zkfl_ntt_coset": (C.c_int, [_P, _U8P, C.c_uint32]),
     "zkfl_setup_g1_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_setup_g2_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_groth16_verify": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p]),
+    "zkfl_groth16_verify_batch": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_size_t, C.c_char_p, C.c_size_t,
+                                            C.c_char_p, C.POINTER(C.c_int32)]),
+    "zkfl_pairing": (C.c_int, [_P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
+    "zkfl_debug_miller_loop": (C.c_int, [_P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
 }
 
 
@@ -159,6 +164,31 @@ class Context:
         out = _buf(128 * n if n else 1)
         check(lib().zkfl_setup_g2_gen_mul(self.h, scalars, n, out))
         return bytes(out)[:128 * n]
+
+    # verification (snarkjs groth16 verify)
+    def verify(self, vk: bytes, public: bytes, proof: bytes) -> bool:
+        """vk image (zkfl.groth16.vk_bytes), public signals npub x 32 B std LE, proof 256 B."""
+        assert len(proof) == 256 and len(public) % 32 == 0
+        rc = lib().zkfl_groth16_verify(self.h, vk, len(vk), public, len(public) // 32, proof)
+        if rc < 0:
+            check(rc)
+        return rc == 1
+
+    def verify_batch(self, vk: bytes, publics: bytes, proofs: bytes, npub: int) -> list:
+        n = len(proofs) // 256
+        assert len(proofs) == 256 * n and len(publics) == 32 * npub * n
+        res = (C.c_int32 * max(1, n))()
+        check(lib().zkfl_groth16_verify_batch(self.h, vk, len(vk), n, publics, npub, proofs, res))
+        return [bool(res[i]) for i in range(n)]
+
+    def pairing(self, g1: bytes, g2: bytes, final_exp: bool = True) -> bytes:
+        """e(P_i, Q_i) for n pairs (std affine); 384 B std Fq12 each (toObject order)."""
+        n = len(g1) // 64
+        assert len(g1) == 64 * n and len(g2) == 128 * n
+        out = _buf(384 * n if n else 1)
+        fn = lib().zkfl_pairing if final_exp else lib().zkfl_debug_miller_loop
+        check(fn(self.h, n, g1, g2, out))
+        return bytes(out)[:384 * n]
 
 
 class ProvingKey:
