@@ -35,6 +35,17 @@ METRIC = "Groth16 proofs/sec (training-step circuit, ~2^18 constraints) at 1/8 M
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # algorithmic bytes per accumulated (base, window) entry: 4 B sorted index + affine base
 BYTES_PER_ENTRY = {"msm_accumulate_g1": 4 + 64, "msm_accumulate_g2": 4 + 128}
+# Fq multiplications per entry: XYZZ mixed addition madd-2008-s = 8M + 2S over Fq (G1), over Fq2
+# (G2: 3 Fq products per Fq2 product, Karatsuba)
+FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
+# the integer-VALU ceiling: Fq Montgomery multiplications/s of the library's fp_mul at full
+# occupancy, measured on MI355X by tools/fp_microbench.hip (tools/README.md)
+FQMUL_PEAK_GPS = 125.1
+# rocprofv3 kernel names of the instrumented kernels (profiles/pmc_traffic.json keys)
+KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps>",
+                 "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2Ops>"}
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")
 
 CIRCUITS = {
     "M": ("sgd_verified", (128, 4, 7, 1000)),
@@ -56,7 +67,7 @@ def cpu_baseline_leg(zk: bytes, wt: bytes, seconds_budget=20.0):
 
 def timed_run(key, warm_w, steps_w, ctx, dist):
     """W untimed proofs, then exactly K timed proofs bracketed by barrier + synchronize on both
-    sides; returns (max-over-ranks elapsed seconds, proofs, per-kernel profile)."""
+    sides; returns (max-over-ranks elapsed seconds, proofs)."""
 
     def barrier_sync():
         ctx.synchronize()
@@ -68,25 +79,49 @@ def timed_run(key, warm_w, steps_w, ctx, dist):
 
     if warm_w:
         key.prove_batch(warm_w)
-    ctx.profile_reset()
-    ctx.set_profiling(True)
     barrier_sync()
     t_start = time.perf_counter()
     proofs = key.prove_batch(steps_w)          # K proofs, `slots` in flight
     barrier_sync()
     elapsed = time.perf_counter() - t_start
-    ctx.set_profiling(False)
-    prof = {k: ctx.profile(k) for k in ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")}
     if dist is not None:
         import torch
         dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, proofs, prof
+    return elapsed, proofs
 
 
-def report(args, world, elapsed, prof, config, cpu):
+def roofline_pass(key, ctx, ws, slots, n=6):
+    """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's three
+    streams serialized onto one), after the timed region: the roofline's average launch time."""
+    key.set_slots(1)
+    key.prove_batch(ws[:1])
+    ctx.profile_reset()
+    ctx.set_profiling(True, serialize=True)
+    key.prove_batch([ws[i % len(ws)] for i in range(n)])
+    ctx.set_profiling(False)
+    prof = {k: ctx.profile(k) for k in PROFILED}
+    ctx.profile_reset()
+    key.set_slots(slots)
+    return prof, n
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/rocpd_summary.py)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, v in d.get("kernels", {}).items():
+        if KERNEL_SYMBOL[kernel] in name:
+            return v["traffic"]
+    return None
+
+
+def report(args, world, elapsed, prof, config, cpu, prof_proofs=1):
     """The one JSON line (rank 0)."""
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
@@ -94,29 +129,34 @@ def report(args, world, elapsed, prof, config, cpu):
     roofline = None
     if cand:
         dom = max(cand, key=lambda k: cand[k][0])
-        ms_tot, launches, units = prof[dom]
-        avg_s = ms_tot / launches / 1e3
-        bytes_per_launch = units / launches * BYTES_PER_ENTRY[dom]
-        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        ms_tot, launches, units, med_ms = prof[dom]
+        avg_s = med_ms / 1e3        # median launch: robust to a one-off stalled dispatch
+        entries = units / launches
+        achieved = entries * BYTES_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
+        fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
-                    "entries_per_launch": round(units / launches)}
-    stage_ms = {k: round(v[0] / max(1, args.steps), 3) for k, v in prof.items()}
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": _pmc_traffic(dom),
+                    "algorithmic_bytes": round(entries * BYTES_PER_ENTRY[dom]),
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "mean_launch_ms": round(ms_tot / launches, 4),
+                    "launches": launches,
+                    "entries_per_launch": round(entries),
+                    "valu": {"achieved": round(fq, 2), "peak": FQMUL_PEAK_GPS, "unit": "G Fq-mul/s",
+                             "frac": round(fq / FQMUL_PEAK_GPS, 4)}}
+    stage_ms = {k: round(v[3] * v[1] / max(1, prof_proofs), 3) for k, v in prof.items()}  # median x launches
     return {
         "metric": METRIC, "value": round(value, 4), "unit": "proofs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (reference harness seeded client generator)",
-        "config": config, "roofline": roofline, "stage_ms_per_proof": stage_ms, "cpu_baseline": cpu,
+        "config": config, "roofline": roofline, "stage_ms_isolated_per_proof": stage_ms, "cpu_baseline": cpu,
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slots", type=int, default=8, help="proofs in flight per GPU (HIP stream sets)")
@@ -164,7 +204,8 @@ def main():
     steps_w = [res[i % len(res)] for i in range(args.steps)]
     warm_w = [res[i % len(res)] for i in range(max(args.warmup, args.slots) if args.warmup else 0)]
 
-    elapsed, proofs, prof = timed_run(key, warm_w, steps_w, ctx, dist)
+    elapsed, proofs = timed_run(key, warm_w, steps_w, ctx, dist)
+    prof, nprof = roofline_pass(key, ctx, res, args.slots)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -176,7 +217,7 @@ def main():
                   "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
                   "global_batch": world, "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}
-        print(json.dumps(report(args, world, elapsed, prof, config, cpu)), flush=True)
+        print(json.dumps(report(args, world, elapsed, prof, config, cpu, nprof)), flush=True)
     assert len(proofs) == args.steps and all(len(p) == 256 for p in proofs)
     for r_ in res:
         r_.close()

@@ -60,10 +60,15 @@ int zkfl_device_count(int* count);
 
 int zkfl_ctx_create(int device, zkfl_ctx** out);
 int zkfl_ctx_destroy(zkfl_ctx* ctx);
-/* Per-kernel timing with HIP events on the context's stream (used by bench.py roofline). */
+/* Per-kernel timing with HIP events on the stream each kernel runs on (bench.py roofline).
+ * enabled: 0 off, 1 on, 2 on + serialized (a proof's G2 and assembly work is put on its main
+ * stream, so with one slot every kernel runs alone and its events time it in isolation). */
 int zkfl_ctx_set_profiling(zkfl_ctx* ctx, int enabled);
-/* name: "msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove".  Synchronises. */
-int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units);
+/* name: "msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove".  Synchronises the device.
+ * total_ms: summed event time; units: summed algorithmic units (MSM entries, NTT elements...);
+ * median_ms (nullable): median single-launch time, robust to a one-off stalled dispatch. */
+int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units,
+                     double* median_ms);
 int zkfl_ctx_profile_reset(zkfl_ctx* ctx);
 int zkfl_ctx_synchronize(zkfl_ctx* ctx);
 

@@ -34,7 +34,7 @@ class _StubCtx:
         pass
 
     def profile(self, name):
-        return (0.0, 0, 0.0)
+        return (0.0, 0, 0.0, 0.0)
 
 
 def _worker(rank, world, port, out_path):
@@ -44,7 +44,8 @@ def _worker(rank, world, port, out_path):
     import bench
     dist.init_process_group("gloo", rank=rank, world_size=world)
     key = _StubKey(rank)
-    elapsed, proofs, prof = bench.timed_run(key, [0], list(range(8)), _StubCtx(), dist)
+    elapsed, proofs = bench.timed_run(key, [0], list(range(8)), _StubCtx(), dist)
+    prof = {k: (0.0, 0, 0.0, 0.0) for k in bench.PROFILED}
 
     class A:
         steps, warmup, slots = 8, 1, 1

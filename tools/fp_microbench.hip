@@ -101,16 +101,65 @@ __device__ __forceinline__ Fp<PR> fips_mul_vcc(const Fp<PR>& a, const Fp<PR>& b)
   return r;
 }
 
+
+// V3: library form plus one explicit s_nop per MAC (what does a wait state cost?)
+// V4: both products of one FIPS step in ONE asm statement (half the asm boundaries)
+#define MAC_NOP_V(x, y) asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\ts_nop 0" : "+v"(lo), "+v"(hi) : "v"(x), "v"(y) : "vcc");
+#define MAC_NOP_S(x, y) asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\ts_nop 0" : "+v"(lo), "+v"(hi) : "v"(x), "s"(y) : "vcc");
+#define MAC_PAIR(x1, y1, x2, y2) asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t" \
+                                     "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" \
+                                     : "+v"(lo), "+v"(hi) : "v"(x1), "v"(y1), "v"(x2), "s"(y2) : "vcc");
+
+template <class PR, int MODE>
+__device__ __forceinline__ Fp<PR> fips_mul_x(const Fp<PR>& a, const Fp<PR>& b) {
+  uint32_t m[8], u[9];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      if (MODE == 0) { MAC_NOP_V(a.v[j], b.v[i - j]); MAC_NOP_S(m[j], PR::P[i - j]); }
+      else { MAC_PAIR(a.v[j], b.v[i - j], m[j], PR::P[i - j]); }
+    }
+    if (MODE == 0) { MAC_NOP_V(a.v[i], b.v[0]); } else { MACV2(a.v[i], b.v[0]); }
+    m[i] = (uint32_t)lo * PR::INV;
+    if (MODE == 0) { MAC_NOP_S(m[i], PR::P[0]); } else { MACS2(m[i], PR::P[0]); }
+    SHIFT2();
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) {
+      if (MODE == 0) { MAC_NOP_V(a.v[j], b.v[i - j]); MAC_NOP_S(m[j], PR::P[i - j]); }
+      else { MAC_PAIR(a.v[j], b.v[i - j], m[j], PR::P[i - j]); }
+    }
+    u[i - 8] = (uint32_t)lo;
+    SHIFT2();
+  }
+  u[8] = (uint32_t)lo;
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, u);
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ Fq vmul(const Fq& x, const Fq& y) {
+  if (V == 0) return cios_mul(x, y);
+  if (V == 1) return fips_mul(x, y);
+  if (V == 2) return fips_mul_vcc(x, y);
+  if (V == 3) return fips_mul_x<FqP, 0>(x, y);
+  if (V == 4) return fips_mul_x<FqP, 1>(x, y);
+  return fp_mul(x, y);
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) kbench(Fq* data, int iters) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   Fq x0 = data[i], x1 = data[i + 1], x2 = data[i + 2], x3 = data[i + 3];
   const Fq y = data[0];
   for (int k = 0; k < iters; k++) {
-    if (V == 0) { x0 = cios_mul(x0, y); x1 = cios_mul(x1, y); x2 = cios_mul(x2, y); x3 = cios_mul(x3, y); }
-    else if (V == 1) { x0 = fips_mul(x0, y); x1 = fips_mul(x1, y); x2 = fips_mul(x2, y); x3 = fips_mul(x3, y); }
-    else if (V == 2) { x0 = fips_mul_vcc(x0, y); x1 = fips_mul_vcc(x1, y); x2 = fips_mul_vcc(x2, y); x3 = fips_mul_vcc(x3, y); }
-    else { x0 = fp_mul(x0, y); x1 = fp_mul(x1, y); x2 = fp_mul(x2, y); x3 = fp_mul(x3, y); }
+    x0 = vmul<V>(x0, y); x1 = vmul<V>(x1, y); x2 = vmul<V>(x2, y); x3 = vmul<V>(x3, y);
   }
   data[i] = fp_add(fp_add(x0, x1), fp_add(x2, x3));
 }
@@ -120,17 +169,19 @@ template <int V>
 __global__ void klat(Fq* data, int iters) {
   Fq x = data[1];
   const Fq y = data[0];
-  for (int k = 0; k < iters; k++) x = V == 0 ? cios_mul(x, y) : (V == 1 ? fips_mul(x, y) : (V == 2 ? fips_mul_vcc(x, y) : fp_mul(x, y)));
+  for (int k = 0; k < iters; k++) x = vmul<V>(x, y);
   data[1] = x;
 }
 
 __global__ void kcheck(const Fq* a, const Fq* b, int n, int* bad) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Fq r0 = cios_mul(a[i], b[i]), r1 = fips_mul(a[i], b[i]), r2 = fips_mul_vcc(a[i], b[i]), r3 = fp_mul(a[i], b[i]);
-  if (!fp_eq(r0, r1)) atomicAdd(bad, 1);
-  if (!fp_eq(r0, r2)) atomicAdd(bad + 1, 1);
-  if (!fp_eq(r0, r3)) atomicAdd(bad + 2, 1);
+  Fq r0 = cios_mul(a[i], b[i]);
+  if (!fp_eq(r0, vmul<1>(a[i], b[i]))) atomicAdd(bad, 1);
+  if (!fp_eq(r0, vmul<2>(a[i], b[i]))) atomicAdd(bad + 1, 1);
+  if (!fp_eq(r0, vmul<3>(a[i], b[i]))) atomicAdd(bad + 2, 1);
+  if (!fp_eq(r0, vmul<4>(a[i], b[i]))) atomicAdd(bad + 3, 1);
+  if (!fp_eq(r0, vmul<5>(a[i], b[i]))) atomicAdd(bad + 4, 1);
 }
 
 int main() {
@@ -149,23 +200,21 @@ int main() {
         st ^= st << 13; st ^= st >> 7; st ^= st << 17;
         h[i].v[j] = (uint32_t)st & (j == 7 ? 0x1fffffffu : 0xffffffffu);
       }
-    Fq* dd; int* bad; int hb[3] = {0, 0, 0};
-    hipMalloc(&dd, 2 * m * sizeof(Fq)); hipMalloc(&bad, 12);
-    hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, 12);
+    Fq* dd; int* bad; int hb[5] = {0, 0, 0, 0, 0};
+    hipMalloc(&dd, 2 * m * sizeof(Fq)); hipMalloc(&bad, 20);
+    hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, 20);
     hipLaunchKernelGGL(kcheck, dim3(m / 256), dim3(256), 0, 0, dd, dd + m, m, bad);
-    hipMemcpy(hb, bad, 12, hipMemcpyDeviceToHost);
-    printf("mismatches vs CIOS: fips_sgpr=%d fips_vcc=%d (of %d)\n", hb[0], hb[1], m);
+    hipMemcpy(hb, bad, 20, hipMemcpyDeviceToHost);
+    printf("mismatches vs CIOS (variants 1..5): %d %d %d %d %d (of %d)\n", hb[0], hb[1], hb[2], hb[3], hb[4], m);
   }
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int v = 0; v < 4; v++) {
+  for (int v = 0; v < 6; v++) {
     for (int rep = 0; rep < 2; rep++) {
       hipEventRecord(a);
-      if (v == 0) hipLaunchKernelGGL(kbench<0>, dim3(blocks), dim3(threads), 0, 0, d, iters);
-      else if (v == 1) hipLaunchKernelGGL(kbench<1>, dim3(blocks), dim3(threads), 0, 0, d, iters);
-      else if (v == 2) hipLaunchKernelGGL(kbench<2>, dim3(blocks), dim3(threads), 0, 0, d, iters);
-      else hipLaunchKernelGGL(kbench<3>, dim3(blocks), dim3(threads), 0, 0, d, iters);
+      void (*kb[6])(Fq*, int) = {kbench<0>, kbench<1>, kbench<2>, kbench<3>, kbench<4>, kbench<5>};
+      hipLaunchKernelGGL(kb[v], dim3(blocks), dim3(threads), 0, 0, d, iters);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
@@ -174,10 +223,8 @@ int main() {
       if (rep) printf("variant %d throughput: %.1f G Fq-mul/s (%.2f ms)\n", v, muls / ms / 1e6, ms);
     }
     hipEventRecord(a);
-    if (v == 0) hipLaunchKernelGGL(klat<0>, dim3(1), dim3(1), 0, 0, d, 10000);
-    else if (v == 1) hipLaunchKernelGGL(klat<1>, dim3(1), dim3(1), 0, 0, d, 10000);
-    else if (v == 2) hipLaunchKernelGGL(klat<2>, dim3(1), dim3(1), 0, 0, d, 10000);
-    else hipLaunchKernelGGL(klat<3>, dim3(1), dim3(1), 0, 0, d, 10000);
+    void (*kl[6])(Fq*, int) = {klat<0>, klat<1>, klat<2>, klat<3>, klat<4>, klat<5>};
+    hipLaunchKernelGGL(kl[v], dim3(1), dim3(1), 0, 0, d, 10000);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;

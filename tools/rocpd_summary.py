@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summaries of rocprofv3 (ROCm 7.2, rocpd SQLite output) runs for profiles/.
+
+  rocpd_summary.py kernels RUN.db OUT.csv
+      per-kernel calls / total / avg / min / max duration from --kernel-trace
+  rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json
+      per-kernel average FETCH_SIZE / WRITE_SIZE per launch (separate --pmc passes, as
+      MI355X_MICROARCH.md §rocprofv3 PMC slots requires), plus the FETCH_SIZE calibration of the
+      MSM gather pattern from tools/pmc_calib.hip (CALIB.db: --pmc FETCH_SIZE of pmc_calib):
+      factor = known bytes / reported bytes for 64-B (G1) and 128-B (G2) records.
+      bench.py reads OUT.json (profiles/pmc_traffic.json) for the roofline "traffic" field.
+"""
+import csv
+import json
+import sqlite3
+import sys
+
+CALIB_LANES = 4 << 20  # tools/pmc_calib.hip
+
+
+def kernels(db, out):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
+                     "from kernels group by name order by sum(end-start) desc").fetchall()
+    tot = sum(r[2] for r in rows) or 1
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_ms", "avg_us", "min_us", "max_us", "pct"])
+        for r in rows:
+            w.writerow([r[0], r[1], round(r[2] / 1e6, 3), round(r[3] / 1e3, 2), round(r[4] / 1e3, 2),
+                        round(r[5] / 1e3, 2), round(100 * r[2] / tot, 2)])
+
+
+def _pmc(db, counter):
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, count(*), avg(value) from counters_collection where counter_name=? "
+                     "group by kernel_name", (counter,)).fetchall()
+    return {r[0]: (r[1], r[2]) for r in rows}  # KiB per launch
+
+
+def pmc(fetch_db, write_db, calib_db, out):
+    fetch, write = _pmc(fetch_db, "FETCH_SIZE"), _pmc(write_db, "WRITE_SIZE")
+    calib = _pmc(calib_db, "FETCH_SIZE")
+    factors = {}
+    for rb in (64, 128):
+        k = [v for n, v in calib.items() if f"k_gather<{rb}>" in n]
+        factors[rb] = (CALIB_LANES * rb) / (k[0][1] * 1024) if k else None
+    res = {"unit": "bytes per launch", "fetch_calibration": {
+        "g1_64B_records": factors[64], "g2_128B_records": factors[128],
+        "method": "tools/pmc_calib.hip: 4 Mi lanes each gather one random record from a 4 GiB table; "
+                  "factor = known bytes / FETCH_SIZE bytes"}, "kernels": {}}
+    for name, (n, f_kib) in fetch.items():
+        w_kib = write.get(name, (0, 0.0))[1]
+        rb = 128 if "Fq2Ops" in name else 64
+        fac = factors[rb] if "k_msm_accumulate" in name and factors[rb] else 1.0
+        res["kernels"][name] = {"launches": n, "fetch_raw": round(f_kib * 1024), "write": round(w_kib * 1024),
+                                "fetch_factor": round(fac, 4),
+                                "traffic": round(f_kib * 1024 * fac + w_kib * 1024)}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "kernels":
+        kernels(sys.argv[2], sys.argv[3])
+    else:
+        pmc(*sys.argv[2:6])

@@ -145,12 +145,20 @@ __global__ void __launch_bounds__(64) k_msm_accumulate(const uint32_t* __restric
   const uint32_t s = bstart[b] + k * MSM_L;
   uint32_t e = s + MSM_L;
   if (e > bend[b]) e = bend[b];
+  // Software-pipelined: the base of entry p+1 and the index of entry p+2 are in flight while
+  // entry p is added, so the dependent index -> base gather overlaps the field arithmetic.
   XYZZ<F> acc = xyzz_inf<F>();
+  uint32_t v0 = vals[s];
+  uint32_t v1 = (s + 1 < e) ? vals[s + 1] : 0u;
+  Affine<F> a = bases[v0 & 0x7FFFFFFFu];
   for (uint32_t p = s; p < e; p++) {
-    uint32_t v = vals[p];
-    Affine<F> a = bases[v & 0x7FFFFFFFu];
-    if (v & 0x80000000u) a = aff_neg<F>(a);
-    acc = xyzz_madd<F>(acc, a);
+    Affine<F> an;
+    if (p + 1 < e) an = bases[v1 & 0x7FFFFFFFu];
+    const uint32_t v2 = (p + 2 < e) ? vals[p + 2] : 0u;
+    acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
+    v0 = v1;
+    v1 = v2;
+    a = an;
   }
   partials[t] = acc;
 }

@@ -11,7 +11,7 @@ namespace zkfl {
 constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
-constexpr int MSM_L = 32;                  // entries per accumulation task
+constexpr int MSM_L = 16;                  // entries per accumulation task (lanes >> SIMDs x waves)
 constexpr int MSM_RG = 8;                  // running-sum group size in the bucket reduction
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -17,6 +18,7 @@ struct ProfRec {
 
 struct Profiler {
   bool on = false;
+  bool serialize = false;  // run every proof stream on the slot's main stream (isolated kernel timings)
   std::vector<ProfRec> recs;
   std::vector<uint32_t*> dev_counters;  // pinned host slots for device-counted units
 
@@ -52,20 +54,24 @@ struct Profiler {
     }
     recs.clear();
   }
-  // Sum over records with this name.  Caller synchronises first.
-  void query(const std::string& name, double* ms, uint64_t* launches, double* units) {
+  // Sum (and median launch time) over records with this name.  Caller synchronises first.
+  void query(const std::string& name, double* ms, uint64_t* launches, double* units, double* median_ms) {
     double t = 0, u = 0;
-    uint64_t c = 0;
+    std::vector<double> d;
     for (auto& r : recs) {
       if (r.name != name) continue;
       float e = 0;
       if (hipEventElapsedTime(&e, r.a, r.b) == hipSuccess) t += e;
+      d.push_back(e);
       u += r.units_dev ? (double)*r.units_dev : r.units;
-      c++;
     }
     *ms = t;
-    *launches = c;
+    *launches = d.size();
     if (units) *units = u;
+    if (median_ms) {
+      std::sort(d.begin(), d.end());
+      *median_ms = d.empty() ? 0.0 : (d.size() & 1 ? d[d.size() / 2] : 0.5 * (d[d.size() / 2 - 1] + d[d.size() / 2]));
+    }
   }
 };
 

@@ -436,6 +436,8 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
+  hipStream_t st_g2 = prof->serialize ? st : s->st_g2;
+  hipStream_t st_asm = prof->serialize ? st : s->st_asm;
   const size_t nV = k->nVars, n = k->n;
   memcpy(s->pinned + 256, rs_host, 64);
   int pp = prof->begin("prove", st);
@@ -446,18 +448,18 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   // G2 stream
-  HIP_TRY(hipStreamWaitEvent(s->st_g2, s->ev_ready, 0), "wait");
-  HIP_TRY(msm_run_g2(k->bB2, s->g2s, W, E, s->resB2, s->st_g2, prof, "msm_accumulate_g2"), "msm B2");
-  if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, s->st_g2, s->resB2, s->d_proof);
-  HIP_TRY(hipEventRecord(s->ev_b2, s->st_g2), "event");
+  HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
+  HIP_TRY(msm_run_g2(k->bB2, s->g2s, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
+  if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, st_g2, s->resB2, s->d_proof);
+  HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   // main: A, B1 first so the assembly chain can start early
   HIP_TRY(msm_run_g1(k->bA, s->g1s, W, E, s->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
   HIP_TRY(msm_run_g1(k->bB1, s->g1s, W, E, s->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
   HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
   if (!plain) {
-    HIP_TRY(hipStreamWaitEvent(s->st_asm, s->ev_ab, 0), "wait");
-    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, s->st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
-    HIP_TRY(hipEventRecord(s->ev_t, s->st_asm), "event");
+    HIP_TRY(hipStreamWaitEvent(st_asm, s->ev_ab, 0), "wait");
+    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
+    HIP_TRY(hipEventRecord(s->ev_t, st_asm), "event");
   }
   int pi = prof->begin("abc", st);
   hipLaunchKernelGGL(k_abc, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rowA, k->rowB, k->cols, k->coefs, d_w, n,
@@ -641,14 +643,16 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
 int zkfl_ctx_set_profiling(zkfl_ctx* ctx, int enabled) {
   if (!ctx) return fail(ZKFL_E_ARG, "null ctx");
   ctx->prof.on = enabled != 0;
+  ctx->prof.serialize = enabled == 2;
   return ZKFL_OK;
 }
 
-int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units) {
+int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units,
+                     double* median_ms) {
   if (!ctx || !name || !total_ms || !launches) return fail(ZKFL_E_ARG, "null");
   (void)hipSetDevice(ctx->device);
-  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
-  ctx->prof.query(name, total_ms, launches, units);
+  HIP_TRY(hipDeviceSynchronize(), "sync");
+  ctx->prof.query(name, total_ms, launches, units, median_ms);
   return ZKFL_OK;
 }
 

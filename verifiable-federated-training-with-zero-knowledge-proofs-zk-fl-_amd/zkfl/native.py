@@ -30,7 +30,7 @@ SIGNATURES = {
     "zkfl_ctx_destroy": (C.c_int, [_P]),
     "zkfl_ctx_set_profiling": (C.c_int, [_P, C.c_int]),
     "zkfl_ctx_profile": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
-                                   C.POINTER(C.c_double)]),
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "zkfl_ctx_profile_reset": (C.c_int, [_P]),
     "zkfl_ctx_synchronize": (C.c_int, [_P]),
     "zkfl_zkey_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
@@ -116,13 +116,14 @@ class Context:
         self.close()
 
     # profiling (bench.py roofline)
-    def set_profiling(self, on: bool):
-        check(lib().zkfl_ctx_set_profiling(self.h, 1 if on else 0))
+    def set_profiling(self, on, serialize: bool = False):
+        check(lib().zkfl_ctx_set_profiling(self.h, (2 if serialize else 1) if on else 0))
 
     def profile(self, name: str):
-        ms, n, u = C.c_double(), C.c_uint64(), C.c_double()
-        check(lib().zkfl_ctx_profile(self.h, name.encode(), C.byref(ms), C.byref(n), C.byref(u)))
-        return ms.value, n.value, u.value
+        """-> (total ms, launches, units, median launch ms)"""
+        ms, n, u, med = C.c_double(), C.c_uint64(), C.c_double(), C.c_double()
+        check(lib().zkfl_ctx_profile(self.h, name.encode(), C.byref(ms), C.byref(n), C.byref(u), C.byref(med)))
+        return ms.value, n.value, u.value, med.value
 
     def profile_reset(self):
         check(lib().zkfl_ctx_profile_reset(self.h))
