@@ -176,7 +176,7 @@ def main():
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)
 
-    from zkfl import circuits, clients, native, zkey
+    from zkfl import circuits, clients, native, wprog, zkey
 
     name, params = CIRCUITS[args.circuit]
     t0 = time.perf_counter()
@@ -185,10 +185,9 @@ def main():
     inputs = []
     for c in range(args.clients):
         client = clients.Client(rank * args.clients + c + 1, batch, dim, depth, clients.JsLcg(12345 + c))
-        inputs.append(client.training_input(batch, precision, 100000000)[0])
-    wits = [b.witness(inp) for inp in inputs]
-    log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires, "
-        f"{len(wits)} client witnesses ({time.perf_counter() - t0:.1f} s)")
+        inputs.append(wprog.input_bytes(b, client.training_input(batch, precision, 100000000)[0]))
+    log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires "
+        f"({time.perf_counter() - t0:.1f} s)")
 
     ctx = native.Context(local_rank)
     t0 = time.perf_counter()
@@ -197,10 +196,12 @@ def main():
     t0 = time.perf_counter()
     key = native.ProvingKey(ctx, zk)
     key.set_slots(args.slots)
-    wts = [zkey.wtns_bytes(w) for w in wits]
-    res = [key.upload(wt) for wt in wts]
-    log(f"[bench r{rank}] key load + witness upload ({time.perf_counter() - t0:.1f} s), domain {key.domain_size}, "
+    wp = native.WitnessProgram(ctx, wprog.compile_program(b))
+    log(f"[bench r{rank}] key + witness program load ({time.perf_counter() - t0:.1f} s), domain {key.domain_size}, "
         f"slots {args.slots}")
+    t0 = time.perf_counter()
+    res = wp.compute_resident(key, inputs)      # GPU witness generation straight into HBM
+    log(f"[bench r{rank}] {len(res)} client witnesses on the GPU ({(time.perf_counter() - t0) * 1e3:.1f} ms)")
     steps_w = [res[i % len(res)] for i in range(args.steps)]
     warm_w = [res[i % len(res)] for i in range(max(args.warmup, args.slots) if args.warmup else 0)]
 
@@ -210,7 +211,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline_leg(zk, wts[0])
+                cpu = cpu_baseline_leg(zk, wp.compute(inputs[:1])[0])
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
         config = {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
@@ -221,6 +222,7 @@ def main():
     assert len(proofs) == args.steps and all(len(p) == 256 for p in proofs)
     for r_ in res:
         r_.close()
+    wp.close()
     key.close()
     ctx.close()
     if dist is not None:

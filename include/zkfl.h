@@ -53,6 +53,7 @@ extern "C" {
 typedef struct zkfl_ctx zkfl_ctx;
 typedef struct zkfl_key zkfl_key;
 typedef struct zkfl_witness zkfl_witness;
+typedef struct zkfl_wprog zkfl_wprog;
 
 int zkfl_version(void);
 const char* zkfl_last_error(void);
@@ -111,6 +112,24 @@ int zkfl_msm_g2(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, siz
 /* In place: 2^logn std-form evaluations on the domain -> evaluations on the odd coset
  * (snarkjs ifft + batchApplyKey(inc) + fft). */
 int zkfl_ntt_coset(zkfl_ctx* ctx, uint8_t* data, uint32_t logn);
+
+/* Witness generation on the GPU (replaces circom's WASM witness calculator:
+ * `node <c>_js/generate_witness.cjs <c>.wasm input.json out.wtns`, tests/full_system_simulation.mjs:758-767,
+ * and `snarkjs wtns calculate`, tests/test_secureagg.cjs:108-118).  The circuit is a witness
+ * program image compiled once per circuit by zkfl/wprog.py (the .wasm's role); inputs are the
+ * circuit's input signals in declaration order, flattened, reduced mod r, 32 B std form each
+ * (zkfl/wprog.py::input_bytes does the input.json -> bytes step).  An unsatisfied assert returns
+ * ZKFL_E_CONSTRAINT (circom: "Assert Failed"); an input >= r returns ZKFL_E_ARG. */
+int zkfl_wprog_load(zkfl_ctx* ctx, const uint8_t* prog, size_t len, zkfl_wprog** out);
+int zkfl_wprog_free(zkfl_wprog* prog);
+int zkfl_wprog_info(const zkfl_wprog* prog, uint32_t* n_wires, uint32_t* n_inputs, uint32_t* n_public);
+/* Byte size of one .wtns image for this program (snarkjs wtns v2: 76 + 32 x n_wires). */
+size_t zkfl_wtns_size(const zkfl_wprog* prog);
+/* n witnesses -> n .wtns images at wtns_out + i * zkfl_wtns_size(prog). */
+int zkfl_witness_compute(zkfl_ctx* ctx, const zkfl_wprog* prog, size_t n, const uint8_t* inputs, uint8_t* wtns_out);
+/* n witnesses computed straight into device-resident witnesses for `key` (no host round trip). */
+int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const zkfl_key* key, size_t n,
+                                  const uint8_t* inputs, zkfl_witness** out);
 
 /* Verification (replaces `snarkjs groth16 verify <vkey> <public> <proof>`,
  * tests/full_system_simulation.mjs:865-868; snarkjs groth16_verify, restated in

@@ -5,6 +5,8 @@ import subprocess
 
 import pytest
 
+from oracle import witness as ow
+
 from oracle import bn254 as bn
 from oracle import groth16 as og
 
@@ -33,10 +35,10 @@ def test_c_prove_matches_python(cb, circ):
     from zkfl import circuits, clients, zkey
     b = circuits.build(*circ)
     if circ[0] == "poseidon_hash2":
-        w = b.witness({"left": 3, "right": 4})
+        w = ow.evaluate(b, {"left": 3, "right": 4})
     else:
         inp, _ = clients.Client(1, 8, 4, 3, clients.JsLcg(12345)).training_input(8, 1000, 100000000)
-        w = b.witness(inp)
+        w = ow.evaluate(b, inp)
     backend = OraclePoints() if circ[0] == "poseidon_hash2" else COraclePoints()
     zk = zkey.groth16_setup(b, backend, zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
     rs = (777).to_bytes(32, "little") + (888).to_bytes(32, "little")

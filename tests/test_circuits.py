@@ -5,11 +5,12 @@ import random
 
 import pytest
 
+from oracle import witness as ow
+
 from oracle import groth16 as og
 from oracle import poseidon as op
 from zkfl import circuits, clients
 from zkfl.field import R, poseidon_hash
-from zkfl.r1cs import ConstraintError
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -29,7 +30,7 @@ def test_poseidon_gadget_witness(n):
     xs = b.input("x", (n,))
     b.bind_output(out, b.poseidon(xs))
     vals = [random.Random(n).randrange(R) for _ in range(n)]
-    w = b.witness({"x": vals})
+    w = ow.evaluate(b, {"x": vals})
     assert w[1] == op.poseidon(vals)
     assert b.check_all(w)
 
@@ -37,7 +38,7 @@ def test_poseidon_gadget_witness(n):
 def test_fixture_v5_satisfies_circuit():
     d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
     b = circuits.build("sgd_step_v5", 8, 16, 7)
-    w = b.witness(d)
+    w = ow.evaluate(b, d)
     assert b.check_all(w)
     # public.json order = [client_id, round, root_D, root_G, tauSquared]
     assert [str(x) for x in w[1:6]] == [d["client_id"], d["round"], d["root_D"], d["root_G"], d["tauSquared"]]
@@ -47,15 +48,15 @@ def test_fixture_v5_satisfies_circuit():
 def test_fixture_tampered_rejected(field, val):
     d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
     d[field] = val
-    with pytest.raises(ConstraintError):
-        circuits.build("sgd_step_v5", 8, 16, 7).witness(d)
+    with pytest.raises(ow.AssertFailed):
+        ow.evaluate(circuits.build("sgd_step_v5", 8, 16, 7), d)
 
 
 def test_fixture_non_boolean_path_rejected():
     d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
     d["pathIndices"][0][0] = "2"
-    with pytest.raises(ConstraintError):
-        circuits.build("sgd_step_v5", 8, 16, 7).witness(d)
+    with pytest.raises(ow.AssertFailed):
+        ow.evaluate(circuits.build("sgd_step_v5", 8, 16, 7), d)
 
 
 def test_input_shape_errors():
@@ -63,7 +64,7 @@ def test_input_shape_errors():
     d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
     del d["labels"]
     with pytest.raises(ValueError):
-        b.witness(d)
+        ow.evaluate(b, d)
 
 
 def _client(n=8, dim=4, depth=3, cid=1):
@@ -84,7 +85,7 @@ def test_sgd_verified_reference_instance():
     b = circuits.build("sgd_verified", 8, 4, 3, 1000)
     c = _client()
     inp, grad = c.training_input(8, 1000, 100000000)
-    w = b.witness(inp)
+    w = ow.evaluate(b, inp)
     assert b.check_all(w)
     assert b.n_public == 6
     pub = [str(x) for x in w[1:7]]
@@ -96,30 +97,30 @@ def test_sgd_verified_wrong_gradient_rejected():
     b = circuits.build("sgd_verified", 8, 4, 3, 1000)
     inp, _ = _client().training_input(8, 1000, 100000000)
     inp["remainder"][0] = str(int(inp["remainder"][0]) + 1)
-    with pytest.raises(ConstraintError):
-        b.witness(inp)
+    with pytest.raises(ow.AssertFailed):
+        ow.evaluate(b, inp)
 
 
 def test_sgd_verified_clipping_bound_enforced():
     b = circuits.build("sgd_verified", 8, 4, 3, 1000)
     inp, grad = _client().training_input(8, 1000, 100000000)
     inp["tauSquared"] = str(sum(g * g for g in grad) - 1)
-    with pytest.raises(ConstraintError):
-        b.witness(inp)
+    with pytest.raises(ow.AssertFailed):
+        ow.evaluate(b, inp)
 
 
 def test_balance_and_secagg():
     c = _client()
     bb = circuits.build("balance_unified", 8, 3, 4)
-    assert bb.check_all(bb.witness(c.balance_input()))
+    assert bb.check_all(ow.evaluate(bb, c.balance_input()))
     bad = c.balance_input()
     bad["c1"] = str(int(bad["c1"]) + 1)
-    with pytest.raises(ConstraintError):
-        bb.witness(bad)
+    with pytest.raises(ow.AssertFailed):
+        ow.evaluate(bb, bad)
     _, grad = c.training_input(8, 1000, 100000000)
     sa = circuits.build("secure_masked_update", 4, 2)
     inp = clients.secagg_input(1, [2, 3], grad, 1, 100000000, c.root_D, 0)
-    w = sa.witness(inp)
+    w = ow.evaluate(sa, inp)
     assert sa.check_all(w) and sa.n_public == 13
 
 

@@ -10,6 +10,8 @@ import random
 
 import pytest
 
+from oracle import witness as ow
+
 from oracle import bn254 as bn
 from oracle import groth16 as og
 
@@ -194,7 +196,7 @@ def test_gpu_setup_zkey_identical_to_oracle_backend(gpu_ctx):
 def test_proof_poseidon_hash2_bit_exact(gpu_ctx):
     from zkfl import native, zkey
     b, zk = _setup(gpu_ctx, "poseidon_hash2")
-    w = b.witness({"left": 1, "right": 2})
+    w = ow.evaluate(b, {"left": 1, "right": 2})
     key = native.ProvingKey(gpu_ctx, zk)
     proof, pub = key.prove(zkey.wtns_bytes(w), RS)
     z = og.parse_zkey(zk)
@@ -226,7 +228,7 @@ def test_proof_sgd_verified_reference_instance(gpu_ctx):
     b, zk = _setup(gpu_ctx, "sgd_verified", 8, 4, 3, 1000)
     c = clients.Client(1, 8, 4, 3, clients.JsLcg(12345))
     inp, _ = c.training_input(8, 1000, 100000000)
-    w = b.witness(inp)
+    w = ow.evaluate(b, inp)
     key = native.ProvingKey(gpu_ctx, zk)
     proof, pub = key.prove(zkey.wtns_bytes(w), RS)
     z = og.parse_zkey(zk)
@@ -249,7 +251,7 @@ def test_fixture_v5_proof_verifies(gpu_ctx):
     d = json.load(open(os.path.join(GOLDEN, "test_input_v5.json")))
     b, zk = _setup(gpu_ctx, "sgd_step_v5", 8, 16, 7)
     key = native.ProvingKey(gpu_ctx, zk)
-    proof, pub = key.prove(zkey.wtns_bytes(b.witness(d)))
+    proof, pub = key.prove(zkey.wtns_bytes(ow.evaluate(b, d)))
     assert [str(x) for x in pub] == [d["client_id"], d["round"], d["root_D"], d["root_G"], d["tauSquared"]]
     assert _verify_bytes(og.parse_zkey(zk), proof, pub)
     key.close()
@@ -262,7 +264,7 @@ def test_resident_batch_and_errors(gpu_ctx):
     wt = []
     for cid in (1, 2, 3):
         c = clients.Client(cid, 8, 4, 3, clients.JsLcg(12345 + cid))
-        wt.append(zkey.wtns_bytes(b.witness(c.balance_input())))
+        wt.append(zkey.wtns_bytes(ow.evaluate(b, c.balance_input())))
     ws = [key.upload(x) for x in wt]
     rs = b"".join(_le(11 + i) + _le(22 + i) for i in range(3))
     batch = key.prove_batch(ws, rs)
@@ -298,7 +300,7 @@ def test_node_snarkjs_cli_prove(gpu_ctx, tmp_path):
     if not node or not os.path.exists(os.path.join(os.path.dirname(shim), "zkfl.node")):
         pytest.skip("node / addon not available")
     b, zk = _setup(gpu_ctx, "poseidon_hash2")
-    w = b.witness({"left": 11, "right": 22})
+    w = ow.evaluate(b, {"left": 11, "right": 22})
     (tmp_path / "c_final.zkey").write_bytes(zk)
     (tmp_path / "w.wtns").write_bytes(zkey.wtns_bytes(w))
     out = subprocess.run([node, shim, "groth16", "prove", "c_final.zkey", "w.wtns", "proof.json", "public.json"],

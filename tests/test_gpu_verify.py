@@ -13,6 +13,8 @@ import subprocess
 
 import pytest
 
+from oracle import witness as ow
+
 from oracle import bn254 as bn
 from oracle import groth16 as og
 from oracle import pairing_tower as T
@@ -117,7 +119,7 @@ def _setup_and_prove(gpu_ctx, name, *params, inputs, n_proofs=1):
     b = circuits.build(name, *params)
     zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(tau=4242, alpha=9, beta=10, gamma=11, delta=12))
     key = native.ProvingKey(gpu_ctx, zk)
-    w = b.witness(inputs)
+    w = ow.evaluate(b, inputs)
     out = [key.prove(zkey.wtns_bytes(w)) for _ in range(n_proofs)]
     key.close()
     return zk, out

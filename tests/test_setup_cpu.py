@@ -1,3 +1,4 @@
+from oracle import witness as ow
 """Product dev ceremony + zkey writer, checked by the oracle prover/verifier (CPU).
 
 The fixed-base multiplications are delegated to the oracle (test backend) so the zkey
@@ -32,14 +33,14 @@ def test_product_zkey_matches_oracle_setup_and_proves():
                 "IC", "A", "B1", "B2", "C", "H"):
         assert z[key] == ref[key], key
     assert sorted(z["coeffs"]) == sorted(ref["coeffs"])
-    w = b.witness({"left": 1, "right": 2})
+    w = ow.evaluate(b, {"left": 1, "right": 2})
     p = og.prove(z, w, r=3, s=4)
     assert og.verify(z, p["public"], p["pi_a"], p["pi_b"], p["pi_c"])
 
 
 def test_wtns_roundtrip():
     b = circuits.build("poseidon_hash2")
-    w = b.witness({"left": 5, "right": 6})
+    w = ow.evaluate(b, {"left": 5, "right": 6})
     buf = zkey.wtns_bytes(w)
     assert og.parse_wtns(buf) == w == zkey.read_wtns(buf)
 

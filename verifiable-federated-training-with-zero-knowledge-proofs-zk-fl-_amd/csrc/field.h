@@ -139,15 +139,25 @@ ZK_DEV Fp<PR> fp_dbl(const Fp<PR>& a) {
 // Montgomery multiplication, finely integrated product scanning (FIPS).  a, b < p  ->
 // a*b*2^-256 mod p, < p.  Column sums are accumulated in a 3-word register triple
 // (lo:64 | hi:32): each 32x32 product is ONE v_mad_u64_u32 whose 64-bit addend is the running
-// column and whose carry-out goes through VCC into `hi` (v_addc_co_u32).  The compiler's own
-// lowering of the same C++ needs a v_cmp + v_cndmask per product and ~270 v_mov per multiply
-// for 64-bit zero-extension; measured on MI355X (tools/fp_microbench.hip): 124 vs 94 G Fq-mul/s
-// at full occupancy, 0.86 vs 1.34 us single-lane latency.  Both moduli are 254-bit so the
-// column accumulator never exceeds 3 words.
-#define ZK_MAC_VV(lo, hi, x, y) \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "v"(y) : "vcc")
-#define ZK_MAC_VS(lo, hi, x, y) \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(x), "s"(y) : "vcc")
+// column and whose carry-out goes, through an SGPR pair the compiler allocates, into `hi`
+// (v_addc_co_u32).  The compiler's own lowering of the same C++ needs a v_cmp + v_cndmask per
+// product and ~270 v_mov per multiply for 64-bit zero-extension; measured on MI355X
+// (tools/fp_microbench.hip, tools/ilp_bench.hip): 125 vs 94 G Fq-mul/s at full occupancy, and at
+// the MSM kernel's 4 waves/SIMD 118 G/s with the SGPR carry vs 109 G/s with the carry pinned
+// to VCC (a fixed VCC clobber serializes independent multiplications).  Both moduli are 254-bit
+// so the column accumulator never exceeds 3 words.
+#define ZK_MAC_VV(lo, hi, x, y)                                                                             \
+  do {                                                                                                      \
+    uint64_t cc_;                                                                                           \
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1" : "+v"(lo), "=&s"(cc_), "+v"(hi) \
+        : "v"(x), "v"(y));                                                                                  \
+  } while (0)
+#define ZK_MAC_VS(lo, hi, x, y)                                                                             \
+  do {                                                                                                      \
+    uint64_t cc_;                                                                                           \
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1" : "+v"(lo), "=&s"(cc_), "+v"(hi) \
+        : "v"(x), "s"(y));                                                                                  \
+  } while (0)
 
 template <class PR>
 ZK_DEV Fp<PR> fp_mul(const Fp<PR>& a, const Fp<PR>& b) {

@@ -1,0 +1,26 @@
+// Host interface of the GPU witness engine (csrc/witness.hip), used by the C ABI in csrc/zkfl.hip.
+// Replaces circom's WASM witness calculator (tests/full_system_simulation.mjs:758-767).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "field.h"
+
+namespace zkfl {
+
+struct WProg;  // a loaded witness program (zkfl/wprog.py image), device-resident
+
+int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std::string& err);
+void wprog_free(WProg* p);
+void wprog_info(const WProg* p, uint32_t* n_wires, uint32_t* n_inputs, uint32_t* n_public);
+
+// n witnesses; inputs: n x n_inputs x 32 B std form (host); outs_host[j]: device buffer of
+// n_wires std-form Fr for witness j.  ZKFL_E_CONSTRAINT when an assert fails, ZKFL_E_ARG when
+// an input is not < r.
+int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_host, hipStream_t st,
+              std::string& err);
+
+}  // namespace zkfl

@@ -31,6 +31,7 @@
 #include "ntt.h"
 #include "prof.h"
 #include "verify.h"
+#include "witness.h"
 #include "zkfl.h"
 
 using namespace zkfl;
@@ -330,6 +331,11 @@ struct zkfl_witness {
   const zkfl_key* key = nullptr;
   Fr* d = nullptr;  // nVars std-form elements
   std::vector<uint8_t> pub;  // nPub x 32 B
+};
+
+struct zkfl_wprog {
+  zkfl_ctx* ctx = nullptr;
+  WProg* p = nullptr;
 };
 
 namespace {
@@ -1073,6 +1079,127 @@ int zkfl_pairing(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, 
 
 int zkfl_debug_miller_loop(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
   return pairing_common(ctx, n, g1, g2, out, 0);
+}
+
+// ---------------------------------------------------------------------------
+// Witness generation (csrc/witness.hip)
+// ---------------------------------------------------------------------------
+int zkfl_wprog_load(zkfl_ctx* ctx, const uint8_t* prog, size_t len, zkfl_wprog** out) {
+  if (!ctx || !prog || !out) return fail(ZKFL_E_ARG, "wprog_load: null argument");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  std::string err;
+  WProg* p = nullptr;
+  int rc = wprog_load(prog, len, ctx->st, &p, err);
+  if (rc != ZKFL_OK) return fail(rc, err);
+  zkfl_wprog* w = new zkfl_wprog();
+  w->ctx = ctx;
+  w->p = p;
+  *out = w;
+  return ZKFL_OK;
+}
+
+int zkfl_wprog_free(zkfl_wprog* prog) {
+  if (!prog) return ZKFL_OK;
+  (void)hipSetDevice(prog->ctx->device);
+  wprog_free(prog->p);
+  delete prog;
+  return ZKFL_OK;
+}
+
+int zkfl_wprog_info(const zkfl_wprog* prog, uint32_t* n_wires, uint32_t* n_inputs, uint32_t* n_public) {
+  if (!prog) return fail(ZKFL_E_ARG, "null program");
+  wprog_info(prog->p, n_wires, n_inputs, n_public);
+  return ZKFL_OK;
+}
+
+size_t zkfl_wtns_size(const zkfl_wprog* prog) {
+  uint32_t nw = 0;
+  if (prog) wprog_info(prog->p, &nw, nullptr, nullptr);
+  return 76 + 32 * (size_t)nw;
+}
+
+static void wtns_header(uint8_t* dst, uint32_t nw) {
+  const uint32_t h1[3] = {0x736e7477u /* "wtns" */, 2, 2};
+  memcpy(dst, h1, 12);
+  uint32_t t = 1;
+  uint64_t sz = 40;
+  memcpy(dst + 12, &t, 4);
+  memcpy(dst + 16, &sz, 8);
+  uint32_t n8 = 32;
+  memcpy(dst + 24, &n8, 4);
+  memcpy(dst + 28, R_LIMBS, 32);
+  memcpy(dst + 60, &nw, 4);
+  t = 2;
+  sz = 32ull * nw;
+  memcpy(dst + 64, &t, 4);
+  memcpy(dst + 68, &sz, 8);
+}
+
+int zkfl_witness_compute(zkfl_ctx* ctx, const zkfl_wprog* prog, size_t n, const uint8_t* inputs, uint8_t* wtns_out) {
+  if (!ctx || !prog || (n && (!wtns_out || !inputs))) return fail(ZKFL_E_ARG, "witness_compute: null argument");
+  if (n == 0) return ZKFL_OK;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  uint32_t nw = 0;
+  wprog_info(prog->p, &nw, nullptr, nullptr);
+  const size_t img = 76 + 32 * (size_t)nw;
+  Fr* d = nullptr;
+  HIP_TRY(hipMalloc(&d, n * (size_t)nw * 32), "witness buffer");
+  std::vector<Fr*> outs(n);
+  for (size_t j = 0; j < n; j++) outs[j] = d + j * nw;
+  std::string err;
+  int rc = wprog_run(prog->p, n, inputs, outs.data(), ctx->st, err);
+  hipError_t e = hipSuccess;
+  for (size_t j = 0; rc == ZKFL_OK && e == hipSuccess && j < n; j++) {
+    wtns_header(wtns_out + j * img, nw);
+    e = hipMemcpyAsync(wtns_out + j * img + 76, outs[j], 32ull * nw, hipMemcpyDeviceToHost, ctx->st);
+  }
+  if (rc == ZKFL_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->st);
+  (void)hipFree(d);
+  if (rc != ZKFL_OK) return fail(rc, err);
+  if (e != hipSuccess) return hip_fail(e, "witness download");
+  return ZKFL_OK;
+}
+
+int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const zkfl_key* key, size_t n,
+                                  const uint8_t* inputs, zkfl_witness** out) {
+  if (!ctx || !prog || !key || (n && (!out || !inputs))) return fail(ZKFL_E_ARG, "witness_compute: null argument");
+  uint32_t nw = 0, npub = 0;
+  wprog_info(prog->p, &nw, nullptr, &npub);
+  if (nw != key->nVars || npub != key->nPub)
+    return fail(ZKFL_E_MISMATCH, "witness program does not match the proving key (nVars / nPublic)");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  std::vector<zkfl_witness*> ws(n, nullptr);
+  std::vector<Fr*> outs(n, nullptr);
+  hipError_t e = hipSuccess;
+  for (size_t j = 0; j < n && e == hipSuccess; j++) {
+    ws[j] = new zkfl_witness();
+    ws[j]->key = key;
+    e = hipMalloc(&ws[j]->d, 32ull * nw);
+    outs[j] = ws[j]->d;
+  }
+  std::string err;
+  int rc = e == hipSuccess ? wprog_run(prog->p, n, inputs, outs.data(), ctx->st, err) : hip_fail(e, "witness alloc");
+  if (rc == ZKFL_OK) {
+    // public signals (witness[1..nPub]) for the prove call's public.json
+    for (size_t j = 0; j < n && e == hipSuccess; j++) {
+      ws[j]->pub.resize(32ull * npub);
+      if (npub) e = hipMemcpyAsync(ws[j]->pub.data(), ws[j]->d + 1, 32ull * npub, hipMemcpyDeviceToHost, ctx->st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->st);
+    if (e != hipSuccess) rc = hip_fail(e, "public signals");
+  } else if (!err.empty()) {
+    rc = fail(rc, err);
+  }
+  if (rc != ZKFL_OK) {
+    for (zkfl_witness* w : ws)
+      if (w) {
+        if (w->d) (void)hipFree(w->d);
+        delete w;
+      }
+    return rc;
+  }
+  for (size_t j = 0; j < n; j++) out[j] = ws[j];
+  return ZKFL_OK;
 }
 
 }  // extern "C"

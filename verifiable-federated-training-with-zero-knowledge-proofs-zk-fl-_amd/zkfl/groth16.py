@@ -16,9 +16,9 @@ from __future__ import annotations
 import hashlib
 import os
 
-from . import native
+from . import native, wprog
 from .field import Q
-from .zkey import read_wtns, wtns_bytes, zkey_header
+from .zkey import read_wtns, zkey_header
 
 _RINV_Q = pow(2 ** 256, Q - 2, Q)
 
@@ -112,8 +112,9 @@ def public_bytes(public) -> bytes:
 
 
 def wtns_calculate(circuit, inputs: dict) -> bytes:
-    """Witness generation (circom WASM replacement); raises ConstraintError on bad inputs."""
-    return wtns_bytes(circuit.witness(inputs))
+    """Witness generation on the GPU (circom WASM + generate_witness.cjs replacement) -> .wtns
+    bytes; an unsatisfied assert raises ZkflError with code ZKFL_E_CONSTRAINT (-7)."""
+    return _prover().wtns_calculate(circuit, inputs)
 
 
 def r1cs_info(circuit) -> dict:
@@ -131,6 +132,18 @@ class Prover:
     def __init__(self, device: int = 0):
         self.ctx = native.Context(device)
         self._keys = {}
+        self._progs = {}
+
+    def program(self, circuit) -> native.WitnessProgram:
+        """The circuit's compiled witness program, loaded once (the .wasm's role)."""
+        p = self._progs.get(id(circuit))
+        if p is None:
+            p = (circuit, native.WitnessProgram(self.ctx, wprog.compile_program(circuit)))
+            self._progs[id(circuit)] = p
+        return p[1]
+
+    def wtns_calculate(self, circuit, inputs: dict) -> bytes:
+        return self.program(circuit).compute([wprog.input_bytes(circuit, inputs)])[0]
 
     def key(self, zkey) -> native.ProvingKey:
         buf = _read(zkey)
@@ -147,7 +160,7 @@ class Prover:
         return proof_to_json(proof), [str(x) for x in pub]
 
     def full_prove(self, inputs: dict, circuit, zkey, rs: bytes | None = None):
-        return self.prove(zkey, wtns_calculate(circuit, inputs), rs)
+        return self.prove(zkey, self.wtns_calculate(circuit, inputs), rs)
 
     def verify(self, vk: dict, public, proof: dict) -> bool:
         return self.ctx.verify(vk_bytes(vk), public_bytes(public), proof_from_json(proof))
@@ -161,6 +174,9 @@ class Prover:
         for k in self._keys.values():
             k.close()
         self._keys.clear()
+        for _, p in self._progs.values():
+            p.close()
+        self._progs.clear()
         self.ctx.close()
 
 

@@ -54,6 +54,12 @@ SIGNATURES = {
                                             C.c_char_p, C.POINTER(C.c_int32)]),
     "zkfl_pairing": (C.c_int, [_P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
     "zkfl_debug_miller_loop": (C.c_int, [_P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
+    "zkfl_wprog_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "zkfl_wprog_free": (C.c_int, [_P]),
+    "zkfl_wprog_info": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "zkfl_wtns_size": (C.c_size_t, [_P]),
+    "zkfl_witness_compute": (C.c_int, [_P, _P, C.c_size_t, C.c_char_p, _U8P]),
+    "zkfl_witness_compute_resident": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_char_p, C.POINTER(_P)]),
 }
 
 
@@ -256,7 +262,10 @@ class ProvingKey:
 
 
 class ResidentWitness:
-    def __init__(self, key: ProvingKey, wtns: bytes):
+    def __init__(self, key: ProvingKey, wtns: bytes | None = None, handle=None):
+        if handle is not None:
+            self.h = handle
+            return
         h = _P()
         check(lib().zkfl_witness_upload(key.ctx.h, key.h, wtns, len(wtns), C.byref(h)))
         self.h = h
@@ -271,3 +280,49 @@ class ResidentWitness:
             self.close()
         except Exception:
             pass
+
+
+class WitnessProgram:
+    """A compiled circuit witness program (zkfl.wprog image) loaded on the device: the
+    replacement of circom's <circuit>.wasm + generate_witness.cjs."""
+
+    def __init__(self, ctx: Context, image: bytes):
+        h = _P()
+        check(lib().zkfl_wprog_load(ctx.h, image, len(image), C.byref(h)))
+        self.h, self.ctx = h, ctx
+        nw, ni, npub = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().zkfl_wprog_info(h, C.byref(nw), C.byref(ni), C.byref(npub)))
+        self.n_wires, self.n_inputs, self.n_public = nw.value, ni.value, npub.value
+        self.wtns_size = lib().zkfl_wtns_size(h)
+
+    def close(self):
+        if self.h:
+            lib().zkfl_wprog_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _inputs(self, inputs) -> bytes:
+        buf = b"".join(inputs)
+        if len(buf) != 32 * self.n_inputs * len(inputs):
+            raise ZkflError(-1, f"expected {self.n_inputs} input values (32 B each) per witness")
+        return buf
+
+    def compute(self, inputs) -> list:
+        """inputs: list of per-witness input byte strings (zkfl.wprog.input_bytes) -> .wtns images."""
+        n = len(inputs)
+        out = _buf(self.wtns_size * max(1, n))
+        check(lib().zkfl_witness_compute(self.ctx.h, self.h, n, self._inputs(inputs), out))
+        ob = bytes(out)
+        return [ob[i * self.wtns_size:(i + 1) * self.wtns_size] for i in range(n)]
+
+    def compute_resident(self, key: ProvingKey, inputs) -> list:
+        """-> ResidentWitness per input, computed in HBM for `key` (no host round trip)."""
+        n = len(inputs)
+        arr = (_P * max(1, n))()
+        check(lib().zkfl_witness_compute_resident(self.ctx.h, self.h, key.h, n, self._inputs(inputs), arr))
+        return [ResidentWitness(key, handle=_P(arr[i])) for i in range(n)]

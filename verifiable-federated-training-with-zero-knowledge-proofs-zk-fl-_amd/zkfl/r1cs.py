@@ -13,8 +13,10 @@ Semantics follow circom 2 with full linear simplification (``--O2``):
     ``assert`` (SURVEY.md §5 failure detection: invalid inputs fail at witness generation).
 
 The witness is produced by a *program* recorded at build time (``Builder.ops``): one op per
-allocated wire group ('m' product, 'bits' Num2Bits hint, 'inv' IsZero hint, 'pos' Poseidon
-permutation).  The structure never depends on input values, so one build serves all inputs.
+allocated wire group ('m' product, 'lc' bound output, 'bits' Num2Bits hint, 'inv' IsZero hint,
+'pos' Poseidon permutation).  The structure never depends on input values, so one build serves
+all inputs.  zkfl/wprog.py compiles it into the image the GPU witness engine executes
+(csrc/witness.hip); oracle/witness.py is the CPU evaluator the tests check the GPU against.
 """
 
 from __future__ import annotations
@@ -22,7 +24,7 @@ from __future__ import annotations
 import struct
 from functools import lru_cache
 
-from .field import POSEIDON_RF, POSEIDON_RP, R, fr, poseidon_params, poseidon_perm_trace
+from .field import POSEIDON_RF, POSEIDON_RP, R, fr, poseidon_params
 
 
 class ConstraintError(ValueError):
@@ -337,48 +339,6 @@ class Builder:
             for i, x in enumerate(flat):
                 out[first + i] = x
         return out
-
-    def witness(self, values: dict, check: bool = True):
-        w = [0] * self.n_wires
-        w[0] = 1
-        for k, v in self.flatten_inputs(values).items():
-            w[k] = v
-        for op in self.ops:
-            kind = op[0]
-            if kind == "m":
-                _, wi, a, b = op
-                w[wi] = evaluate(a, w) * evaluate(b, w) % R
-            elif kind == "pos":
-                _, w0, t, ins, tp = op
-                state = [0] + [evaluate(a, w) for a in ins]
-                _, trace = poseidon_perm_trace(state)
-                k = w0
-                for idx in tp.live:
-                    x2, x4, x5 = trace[idx]
-                    w[k] = x2
-                    w[k + 1] = x4
-                    w[k + 2] = x5
-                    k += 3
-            elif kind == "bits":
-                _, w0, n, x = op
-                v = evaluate(x, w)
-                for i in range(n):
-                    w[w0 + i] = (v >> i) & 1
-            elif kind == "lc":
-                _, wi, x = op
-                w[wi] = evaluate(x, w)
-            elif kind == "inv":
-                _, wi, x = op
-                v = evaluate(x, w)
-                w[wi] = pow(v, R - 2, R) if v else 0
-            else:  # pragma: no cover
-                raise RuntimeError(kind)
-        if check:
-            for ci in self.asserts:
-                A, B, C = self.cons[ci]
-                if evaluate(A, w) * evaluate(B, w) % R != evaluate(C, w):
-                    raise ConstraintError(f"{self.name}: assert constraint {ci} failed")
-        return w
 
     def check_all(self, w) -> bool:
         """Full R1CS satisfaction check (every constraint)."""
