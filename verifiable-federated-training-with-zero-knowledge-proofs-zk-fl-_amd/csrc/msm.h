@@ -15,8 +15,11 @@
 //    2^18-constraint training circuit) free.
 //  * Signed digits in [-2^15, 2^15]; the sign is applied by negating y on the fly.
 //  * (bucket, entry) pairs are radix-sorted (rocPRIM, 16 key bits), bucket ranges found by
-//    adjacent-key compare, and the accumulation is split into tasks of <= L entries so a
-//    skewed bucket (e.g. all bit-valued witness wires) cannot serialise one lane.
+//    adjacent-key compare.  The sorted entries are cut into fixed chunks of L entries, one lane
+//    each, independent of bucket boundaries: every lane does exactly L additions (no idle lanes
+//    behind a short bucket tail, no task->bucket search), emits a partial sum at each bucket
+//    change (first segment -> head[chunk], last -> tail[chunk], a bucket wholly inside the chunk
+//    -> its final sum), and k_msm_bucket_sum stitches each bucket from its chunks' partials.
 //  * Accumulation uses XYZZ + affine mixed additions (10 Fq mul for G1).
 //  * Bucket reduction sum_b (b+1) S_b uses grouped running sums (groups of RG buckets),
 //    recursively on the group sums, then a Horner combination.
@@ -114,62 +117,84 @@ static __global__ void k_msm_bounds(const uint16_t* __restrict__ keys, size_t m,
   if (p == m - 1 || keys[p + 1] == MSM_KEY_NONE) *nnz = (uint32_t)(p + 1);  // non-zero digits
 }
 
-static __global__ void k_msm_task_count(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
-                                 uint32_t* __restrict__ tcount) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= MSM_NB) return;
-  uint32_t len = bend[b] - bstart[b];
-  tcount[b] = (len + MSM_L - 1) / MSM_L;
-}
-
-template <class F>
-__global__ void __launch_bounds__(64) k_msm_accumulate(const uint32_t* __restrict__ vals,
+// Lane c adds the sorted entries [c*L, min(c*L+L, nnz)).  Software-pipelined: the key/index of
+// entry p+1 and its base are in flight while entry p is added.
+// MINW: minimum waves per SIMD the register allocator must allow (G1: 4, keeping the madd
+// working set in <= 128 VGPRs; G2's Fq2 working set does not fit 4 waves without spilling).
+template <class F, int MINW>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
+                                                        const uint16_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ vals,
                                                         const Affine<F>* __restrict__ bases,
-                                                        const uint32_t* __restrict__ bstart,
-                                                        const uint32_t* __restrict__ bend,
-                                                        const uint32_t* __restrict__ toff,
-                                                        size_t max_tasks,
-                                                        XYZZ<F>* __restrict__ partials) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= max_tasks) return;
-  const uint32_t total = toff[MSM_NB];
-  if (t >= total) return;
-  // bucket b: largest b with toff[b] <= t
-  int lo = 0, hi = MSM_NB - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (toff[mid] <= t) lo = mid; else hi = mid - 1;
-  }
-  const int b = lo;
-  const uint32_t k = (uint32_t)t - toff[b];
-  const uint32_t s = bstart[b] + k * MSM_L;
-  uint32_t e = s + MSM_L;
-  if (e > bend[b]) e = bend[b];
-  // Software-pipelined: the base of entry p+1 and the index of entry p+2 are in flight while
-  // entry p is added, so the dependent index -> base gather overlaps the field arithmetic.
+                                                        const uint32_t* __restrict__ nnz_ptr,
+                                                        XYZZ<F>* __restrict__ head,
+                                                        XYZZ<F>* __restrict__ tail,
+                                                        XYZZ<F>* __restrict__ buckets) {
+  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nnz = *nnz_ptr;
+  const size_t p0 = c * MSM_L;
+  if (p0 >= nnz) return;
+  const uint32_t p1 = (uint32_t)(p0 + MSM_L < nnz ? p0 + MSM_L : nnz);
   XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t v0 = vals[s];
-  uint32_t v1 = (s + 1 < e) ? vals[s + 1] : 0u;
+  uint32_t cur = keys[p0];
+  bool first = true;
+  uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
+  if (p0 + 1 < p1) {
+    k1 = keys[p0 + 1];
+    v1 = vals[p0 + 1];
+  }
   Affine<F> a = bases[v0 & 0x7FFFFFFFu];
-  for (uint32_t p = s; p < e; p++) {
+  for (uint32_t p = (uint32_t)p0; p < p1; p++) {
     Affine<F> an;
-    if (p + 1 < e) an = bases[v1 & 0x7FFFFFFFu];
-    const uint32_t v2 = (p + 2 < e) ? vals[p + 2] : 0u;
+    uint32_t k2 = 0, v2 = 0;
+    if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
+    if (p + 2 < p1) {
+      k2 = keys[p + 2];
+      v2 = vals[p + 2];
+    }
     acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
+    if (p + 1 < p1 && k1 != cur) {  // bucket boundary inside the chunk
+      if (first) head[c] = acc;
+      else buckets[cur] = acc;     // starts and ends inside this chunk: complete
+      first = false;
+      acc = xyzz_inf<F>();
+      cur = k1;
+    }
     v0 = v1;
     v1 = v2;
+    k1 = k2;
     a = an;
   }
-  partials[t] = acc;
+  if (first) head[c] = acc;
+  else tail[c] = acc;
 }
 
+// Bucket b = its entries [s, e): stitched from the partials of chunks c0 = s/L .. c1 = (e-1)/L.
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_bucket_sum(const XYZZ<F>* __restrict__ partials, const uint32_t* __restrict__ toff,
-                                 XYZZ<F>* __restrict__ buckets) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(64) k_msm_bucket_sum(const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ bend,
+                                                        const uint32_t* __restrict__ nnz_ptr,
+                                                        const XYZZ<F>* __restrict__ head,
+                                                        const XYZZ<F>* __restrict__ tail,
+                                                        XYZZ<F>* __restrict__ buckets) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= MSM_NB) return;
-  XYZZ<F> acc = xyzz_inf<F>();
-  for (uint32_t t = toff[b]; t < toff[b + 1]; t++) acc = xyzz_add<F>(acc, partials[t]);
+  const uint32_t s = bstart[b], e = bend[b];
+  if (s == e) {
+    buckets[b] = xyzz_inf<F>();
+    return;
+  }
+  const uint32_t c0 = s / MSM_L, c1 = (e - 1) / MSM_L;
+  const bool starts_chunk = (s == c0 * MSM_L);
+  if (c0 == c1) {
+    const uint32_t nnz = *nnz_ptr;
+    const uint32_t cend = (c0 + 1) * MSM_L < nnz ? (c0 + 1) * MSM_L : nnz;
+    if (starts_chunk) buckets[b] = head[c0];
+    else if (e == cend) buckets[b] = tail[c0];
+    return;  // otherwise wholly inside the chunk: written by k_msm_accumulate
+  }
+  XYZZ<F> acc = starts_chunk ? head[c0] : tail[c0];
+  for (uint32_t c = c0 + 1; c <= c1; c++) acc = xyzz_add<F>(acc, head[c]);
   buckets[b] = acc;
 }
 
@@ -254,13 +279,9 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
   ZK_CHECK(hipMalloc(&s.bstart, MSM_NB * sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&s.bend, MSM_NB * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&s.tcount, (MSM_NB + 1) * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&s.toff, (MSM_NB + 1) * sizeof(uint32_t)));
-  ZK_CHECK(rocprim::exclusive_scan(nullptr, s.scan_tmp_bytes, s.tcount, s.toff, 0u, (size_t)MSM_NB + 1,
-                                   rocprim::plus<uint32_t>(), st));
-  ZK_CHECK(hipMalloc(&s.scan_tmp, s.scan_tmp_bytes));
-  s.max_tasks = m / MSM_L + MSM_NB + 1;
-  ZK_CHECK(hipMalloc(&s.partials, s.max_tasks * sizeof(XYZZ<F>)));
+  s.max_chunks = (m + MSM_L - 1) / MSM_L;
+  ZK_CHECK(hipMalloc(&s.head, s.max_chunks * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.tail, s.max_chunks * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&s.buckets, MSM_NB * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&s.red_acc, MSM_NB * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&s.red_run, MSM_NB * sizeof(XYZZ<F>)));
@@ -271,8 +292,8 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
 
 template <class F>
 void msm_scratch_free(MsmScratch<F>& s) {
-  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.scan_tmp, s.bstart, s.bend,
-                  s.tcount, s.toff, s.partials, s.buckets, s.red_acc, s.red_run, s.red_tmp, s.nnz};
+  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.bstart, s.bend,
+                  s.head, s.tail, s.buckets, s.red_acc, s.red_run, s.red_tmp, s.nnz};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s = MsmScratch<F>();
@@ -293,10 +314,10 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
     return hipGetLastError();
   }
   const size_t m = b.n * MSM_W;
-  const size_t max_tasks = m / MSM_L + MSM_NB + 1;
+  const size_t chunks = (m + MSM_L - 1) / MSM_L;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
-  if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
+  if (need > pl.sort_tmp_bytes || chunks > pl.max_chunks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
                      b.extra_start, b.n, pl.keys_in, pl.vals_in);
   ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
@@ -306,17 +327,13 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
   ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_msm_bounds, dim3(zk_grid(m, 256)), dim3(256), 0, st, pl.keys_out, m, pl.bstart, pl.bend,
                      pl.nnz);
-  ZK_CHECK(hipMemsetAsync(pl.tcount + MSM_NB, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_msm_task_count, dim3(zk_grid(MSM_NB, 256)), dim3(256), 0, st, pl.bstart, pl.bend,
-                     pl.tcount);
-  ZK_CHECK(rocprim::exclusive_scan(pl.scan_tmp, pl.scan_tmp_bytes, pl.tcount, pl.toff, 0u, (size_t)MSM_NB + 1,
-                                   rocprim::plus<uint32_t>(), st));
   const int pidx = prof ? prof->begin(tag, st) : -1;
-  hipLaunchKernelGGL(k_msm_accumulate<F>, dim3(zk_grid(max_tasks, 64)), dim3(64), 0, st, pl.vals_out, b.bases_w,
-                     pl.bstart, pl.bend, pl.toff, max_tasks, pl.partials);
+  hipLaunchKernelGGL((k_msm_accumulate<F, sizeof(typename F::T) == 32 ? 4 : 1>), dim3(zk_grid(chunks, 64)), dim3(64), 0,
+                     st, pl.keys_out, pl.vals_out,
+                     b.bases_w, pl.nnz, pl.head, pl.tail, pl.buckets);
   if (prof) prof->end(pidx, st, 0.0, pl.nnz);
-  hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.partials, pl.toff,
-                     pl.buckets);
+  hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.bstart, pl.bend, pl.nnz,
+                     pl.head, pl.tail, pl.buckets);
   // grouped running-sum reduction
   const XYZZ<F>* in = pl.buckets;
   int K = MSM_NB;

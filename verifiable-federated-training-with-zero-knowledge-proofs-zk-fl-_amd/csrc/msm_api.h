@@ -11,7 +11,7 @@ namespace zkfl {
 constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
-constexpr int MSM_L = 16;                  // entries per accumulation task (lanes >> SIMDs x waves)
+constexpr int MSM_L = 16;                  // sorted entries per accumulation lane (fixed-size chunks)
 constexpr int MSM_RG = 8;                  // running-sum group size in the bucket reduction
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
 
@@ -38,14 +38,11 @@ struct MsmScratch {
   uint32_t* vals_out = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  void* scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
   uint32_t* bstart = nullptr;  // [NB]
   uint32_t* bend = nullptr;    // [NB]
-  uint32_t* tcount = nullptr;  // [NB + 1]
-  uint32_t* toff = nullptr;    // [NB + 1]
-  size_t max_tasks = 0;
-  XYZZ<F>* partials = nullptr;  // [max_tasks]
+  size_t max_chunks = 0;        // ceil(cap * W / L)
+  XYZZ<F>* head = nullptr;      // [max_chunks] sum of the chunk's first bucket segment
+  XYZZ<F>* tail = nullptr;      // [max_chunks] sum of its last segment (when it differs)
   XYZZ<F>* buckets = nullptr;   // [NB]
   XYZZ<F>* red_acc = nullptr;   // reduction scratch (all levels), [NB]
   XYZZ<F>* red_run = nullptr;   // [NB]
