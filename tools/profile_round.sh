@@ -13,5 +13,6 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o r
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run -- python3 "$R/bench.py" --steps 8 --warmup 1 --slots 2 --no-cpu-baseline > "$OUT/write.log" 2>&1
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/calib" -o run -- "$R/tools/pmc_calib" > "$OUT/calib.log" 2>&1
 python3 "$R/tools/rocpd_summary.py" kernels "$OUT/ks/run_results.db" "$OUT/kernel_stats.csv"
+python3 "$R/tools/rocpd_summary.py" roofline "$OUT/ks/run_results.db" "$OUT/bench_ks.log" "$OUT/roofline_pass.json"
 python3 "$R/tools/rocpd_summary.py" pmc "$OUT/fetch/run_results.db" "$OUT/write/run_results.db" "$OUT/calib/run_results.db" "$OUT/pmc_traffic.json"
 echo "profiles written to $OUT"

@@ -3,6 +3,10 @@
 
   rocpd_summary.py kernels RUN.db OUT.csv
       per-kernel calls / total / avg / min / max duration from --kernel-trace
+  rocpd_summary.py roofline RUN.db BENCH.log OUT.json
+      the dispatches of bench.py's serialized roofline pass (the last `launches` dispatches of
+      each instrumented kernel in a traced bench.py run): median / mean duration, to compare with
+      the bench line's roofline.avg_launch_ms (median) / mean_launch_ms
   rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json
       per-kernel average FETCH_SIZE / WRITE_SIZE per launch (separate --pmc passes, as
       MI355X_MICROARCH.md §rocprofv3 PMC slots requires), plus the FETCH_SIZE calibration of the
@@ -60,8 +64,34 @@ def pmc(fetch_db, write_db, calib_db, out):
         json.dump(res, f, indent=1, sort_keys=True)
 
 
+ROOFLINE_KERNELS = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps", "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2Ops"}
+
+
+def roofline(db, bench_log, out):
+    line = [ln for ln in open(bench_log) if ln.startswith("{")][-1]
+    rep = json.loads(line)
+    n = rep["roofline"]["launches"]
+    c = sqlite3.connect(db)
+    res = {"bench_roofline": rep["roofline"], "trace": {}}
+    for tag, sym in ROOFLINE_KERNELS.items():
+        d = [r[0] for r in c.execute("select end-start from kernels where name like ? order by start",
+                                     (f"%{sym}%",)).fetchall()]
+        launches = n if tag == rep["roofline"]["kernel"] else n // 4  # 4 G1 MSMs per G2 MSM
+        last = sorted(x / 1e6 for x in d[-launches:])
+        if last:
+            mid = len(last) // 2
+            med = last[mid] if len(last) % 2 else 0.5 * (last[mid - 1] + last[mid])
+            res["trace"][tag] = {"dispatches": len(last), "median_ms": round(med, 4),
+                                 "mean_ms": round(sum(last) / len(last), 4),
+                                 "min_ms": round(last[0], 4), "max_ms": round(last[-1], 4)}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "kernels":
         kernels(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "roofline":
+        roofline(sys.argv[2], sys.argv[3], sys.argv[4])
     else:
         pmc(*sys.argv[2:6])
