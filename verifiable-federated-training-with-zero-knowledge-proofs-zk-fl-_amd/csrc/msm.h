@@ -31,6 +31,22 @@
 
 namespace zkfl {
 
+// Accumulation kernel configuration per curve (measured on MI355X): G1 fits its
+// working set in 128 VGPRs -> 4 waves/SIMD with the pipelined gather; G2's Fq2 working set needs
+// > 256 registers, so it runs at 1 wave/SIMD (2 waves cost 130-280 spills in every schedule tried).
+#ifndef MSM_G1_WAVES
+#define MSM_G1_WAVES 4
+#endif
+#ifndef MSM_G1_PF
+#define MSM_G1_PF true
+#endif
+#ifndef MSM_G2_WAVES
+#define MSM_G2_WAVES 1
+#endif
+#ifndef MSM_G2_PF
+#define MSM_G2_PF true
+#endif
+
 // ---------------------------------------------------------------------------
 // Key-load-time window expansion: out[i*W + j] = 2^(16 j) * in[i]  (affine)
 // ---------------------------------------------------------------------------
@@ -119,9 +135,10 @@ static __global__ void k_msm_bounds(const uint16_t* __restrict__ keys, size_t m,
 
 // Lane c adds the sorted entries [c*L, min(c*L+L, nnz)).  Software-pipelined: the key/index of
 // entry p+1 and its base are in flight while entry p is added.
-// MINW: minimum waves per SIMD the register allocator must allow (G1: 4, keeping the madd
-// working set in <= 128 VGPRs; G2's Fq2 working set does not fit 4 waves without spilling).
-template <class F, int MINW>
+// MINW: minimum waves per SIMD the register allocator must allow; PF: software-pipeline the
+// next entry's key/index/base loads behind the current addition (costs one affine point of
+// registers).  Chosen per curve in msm_run.
+template <class F, int MINW, bool PF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
                                                         const uint16_t* __restrict__ keys,
                                                         const uint32_t* __restrict__ vals,
@@ -138,32 +155,47 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t cur = keys[p0];
   bool first = true;
-  uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
-  if (p0 + 1 < p1) {
-    k1 = keys[p0 + 1];
-    v1 = vals[p0 + 1];
-  }
-  Affine<F> a = bases[v0 & 0x7FFFFFFFu];
-  for (uint32_t p = (uint32_t)p0; p < p1; p++) {
-    Affine<F> an;
-    uint32_t k2 = 0, v2 = 0;
-    if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
-    if (p + 2 < p1) {
-      k2 = keys[p + 2];
-      v2 = vals[p + 2];
+  if (PF) {
+    uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
+    if (p0 + 1 < p1) {
+      k1 = keys[p0 + 1];
+      v1 = vals[p0 + 1];
     }
-    acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
-    if (p + 1 < p1 && k1 != cur) {  // bucket boundary inside the chunk
-      if (first) head[c] = acc;
-      else buckets[cur] = acc;     // starts and ends inside this chunk: complete
-      first = false;
-      acc = xyzz_inf<F>();
-      cur = k1;
+    Affine<F> a = bases[v0 & 0x7FFFFFFFu];
+    for (uint32_t p = (uint32_t)p0; p < p1; p++) {
+      Affine<F> an;
+      uint32_t k2 = 0, v2 = 0;
+      if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
+      if (p + 2 < p1) {
+        k2 = keys[p + 2];
+        v2 = vals[p + 2];
+      }
+      acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
+      if (p + 1 < p1 && k1 != cur) {  // bucket boundary inside the chunk
+        if (first) head[c] = acc;
+        else buckets[cur] = acc;     // starts and ends inside this chunk: complete
+        first = false;
+        acc = xyzz_inf<F>();
+        cur = k1;
+      }
+      v0 = v1;
+      v1 = v2;
+      k1 = k2;
+      a = an;
     }
-    v0 = v1;
-    v1 = v2;
-    k1 = k2;
-    a = an;
+  } else {
+    for (uint32_t p = (uint32_t)p0; p < p1; p++) {
+      const uint32_t k = keys[p], v = vals[p];
+      if (k != cur) {
+        if (first) head[c] = acc;
+        else buckets[cur] = acc;
+        first = false;
+        acc = xyzz_inf<F>();
+        cur = k;
+      }
+      Affine<F> a = bases[v & 0x7FFFFFFFu];
+      acc = xyzz_madd<F>(acc, (v & 0x80000000u) ? aff_neg<F>(a) : a);
+    }
   }
   if (first) head[c] = acc;
   else tail[c] = acc;
@@ -328,8 +360,9 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
   hipLaunchKernelGGL(k_msm_bounds, dim3(zk_grid(m, 256)), dim3(256), 0, st, pl.keys_out, m, pl.bstart, pl.bend,
                      pl.nnz);
   const int pidx = prof ? prof->begin(tag, st) : -1;
-  hipLaunchKernelGGL((k_msm_accumulate<F, sizeof(typename F::T) == 32 ? 4 : 1>), dim3(zk_grid(chunks, 64)), dim3(64), 0,
-                     st, pl.keys_out, pl.vals_out,
+  constexpr bool G1 = sizeof(typename F::T) == 32;
+  hipLaunchKernelGGL((k_msm_accumulate<F, G1 ? MSM_G1_WAVES : MSM_G2_WAVES, G1 ? MSM_G1_PF : MSM_G2_PF>),
+                     dim3(zk_grid(chunks, 64)), dim3(64), 0, st, pl.keys_out, pl.vals_out,
                      b.bases_w, pl.nnz, pl.head, pl.tail, pl.buckets);
   if (prof) prof->end(pidx, st, 0.0, pl.nnz);
   hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.bstart, pl.bend, pl.nnz,
