@@ -73,10 +73,35 @@ ZK_DEV uint32_t g2_load(const uint32_t* s, G2Aff& q) {
   return f2_eq(lhs, rhs) ? 0u : ST_BAD;
 }
 
-// [r]Q == O  (order-r subgroup of the twist; G2 has a large cofactor)
+// psi (untwist-Frobenius-twist) on XYZZ coordinates: conj is a field automorphism, so
+// psi(X, Y, ZZ, ZZZ) = (conj(X) gx, conj(Y) gy, conj(ZZ), conj(ZZZ))
+ZK_DEV G2P g2_psi(const G2P& p) {
+  G2P r;
+  r.X = f2_mul(f2_conj(p.X), load_fq2(TWIST_FROB_X));
+  r.Y = f2_mul(f2_conj(p.Y), load_fq2(TWIST_FROB_Y));
+  r.ZZ = f2_conj(p.ZZ);
+  r.ZZZ = f2_conj(p.ZZZ);
+  return r;
+}
+
+ZK_DEV bool g2_eq(const G2P& a, const G2P& b) {
+  const bool ia = xyzz_is_inf(a), ib = xyzz_is_inf(b);
+  if (ia || ib) return ia && ib;
+  return f2_eq(f2_mul(a.X, b.ZZ), f2_mul(b.X, a.ZZ)) && f2_eq(f2_mul(a.Y, b.ZZZ), f2_mul(b.Y, a.ZZZ));
+}
+
+// Order-r subgroup membership of a twist point (G2 has a large cofactor), by the BN endomorphism
+// criterion [x0+1]P + psi([x0]P) + psi^2([x0]P) == psi^3([2 x0]P), x0 = u (ePrint 2022/348 §5.1):
+// a 63-bit scalar multiplication instead of [r]P.  Checked against [r]P on subgroup and
+// non-subgroup points in tests (tests/test_gpu_verify.py).
 ZK_DEV bool g2_in_subgroup(const G2Aff& q) {
-  G2P acc = xyzz_scalar_mul<Fq2Ops>(xyzz_from_affine<Fq2Ops>(q), FrP::P);
-  return xyzz_is_inf(acc);
+  const uint32_t u[8] = {(uint32_t)BN_U, (uint32_t)(BN_U >> 32), 0, 0, 0, 0, 0, 0};
+  const G2P p = xyzz_from_affine<Fq2Ops>(q);
+  const G2P xp = xyzz_scalar_mul<Fq2Ops>(p, u);
+  const G2P pxp = g2_psi(xp);
+  G2P lhs = xyzz_add<Fq2Ops>(xyzz_add<Fq2Ops>(xyzz_add<Fq2Ops>(xp, p), pxp), g2_psi(pxp));
+  G2P rhs = g2_psi(g2_psi(g2_psi(xyzz_dbl<Fq2Ops>(xp))));
+  return g2_eq(lhs, rhs);
 }
 
 __global__ __launch_bounds__(64) void k_g2_prepare(size_t n, const uint32_t* q_std, size_t q_stride, int subgroup,
