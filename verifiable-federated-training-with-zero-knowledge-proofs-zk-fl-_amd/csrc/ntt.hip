@@ -78,7 +78,8 @@ __global__ void k_ntt_dit_stage(Fr* __restrict__ a, size_t n, size_t half, const
 //   DIT: spans 1 .. T/2 (the first log2 T stages of the forward transform)
 template <bool DIF>
 __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, int logt,
-                                                 const Fr* __restrict__ tw, int nvec, size_t vstride) {
+                                                 const Fr* __restrict__ tw, int nvec, size_t vstride,
+                                                 const Fr* __restrict__ scale) {
   __shared__ Fr tile[NTT_LDS_N];
   const size_t T = (size_t)1 << logt;
   const size_t tiles_per_vec = n >> logt;
@@ -110,7 +111,65 @@ __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, i
     }
     __syncthreads();
   }
-  for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
+  const size_t base = (tile_id - v * tiles_per_vec) * T;
+  if (scale)  // fused coset scale (inverse pass): x[p] *= inc^bitrev(p) / n
+    for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = fp_mul(tile[i], scale[base + i]);
+  else
+    for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
+}
+
+// The top k stages (spans n/2 .. n/2^k) of a DIF (or the last k of a DIT) transform only combine
+// elements that share their low (logn - k) index bits: a "column" of 2^k elements with stride
+// 2^(logn-k).  One workgroup takes NTT_COL_TILE / 2^k consecutive columns (rows of consecutive
+// elements are contiguous in memory), runs the k stages in LDS and writes back: one global pass
+// instead of k radix-2 passes.
+constexpr int NTT_COL_TILE_LOG = 11;
+constexpr int NTT_COL_TILE = 1 << NTT_COL_TILE_LOG;
+template <bool DIF>
+__global__ void __launch_bounds__(256) k_ntt_cols(Fr* __restrict__ a, int logn, int k, const Fr* __restrict__ tw,
+                                                  int nvec, size_t vstride) {
+  __shared__ Fr tile[NTT_COL_TILE];
+  const size_t n = (size_t)1 << logn;
+  const int lowlog = logn - k;                 // column stride 2^lowlog
+  const size_t M = (size_t)1 << k;             // elements per column
+  const size_t C = (size_t)NTT_COL_TILE >> k;  // columns per workgroup (k <= 11)
+  const size_t groups = ((size_t)1 << lowlog) / C;
+  const size_t v = blockIdx.x / groups;
+  if (v >= (size_t)nvec) return;
+  const size_t col0 = (blockIdx.x - v * groups) * C;
+  Fr* x = a + v * vstride;
+  for (size_t q = threadIdx.x; q < NTT_COL_TILE; q += blockDim.x) {
+    const size_t c = q % C, m = q / C;
+    tile[q] = x[col0 + c + (m << lowlog)];
+  }
+  __syncthreads();
+  const size_t nbf = NTT_COL_TILE >> 1;
+  for (int s = 0; s < k; s++) {
+    const size_t mhalf = DIF ? (M >> (s + 1)) : ((size_t)1 << s);  // span in column units
+    const size_t half = mhalf << lowlog;                               // span in global units
+    const size_t twstride = n / (half << 1);
+    for (size_t t = threadIdx.x; t < nbf; t += blockDim.x) {
+      const size_t c = t % C, mt = t / C;  // butterfly mt of column c
+      const size_t mj = mt & (mhalf - 1);
+      const size_t m0 = ((mt - mj) << 1) + mj, m1 = m0 + mhalf;
+      const size_t i0 = m0 * C + c, i1 = m1 * C + c;
+      const Fr tws = tw[(col0 + c + (mj << lowlog)) * twstride];
+      Fr u = tile[i0], w = tile[i1];
+      if (DIF) {
+        tile[i0] = fp_add(u, w);
+        tile[i1] = fp_mul(fp_sub(u, w), tws);
+      } else {
+        w = fp_mul(w, tws);
+        tile[i0] = fp_add(u, w);
+        tile[i1] = fp_sub(u, w);
+      }
+    }
+    __syncthreads();
+  }
+  for (size_t q = threadIdx.x; q < NTT_COL_TILE; q += blockDim.x) {
+    const size_t c = q % C, m = q / C;
+    x[col0 + c + (m << lowlog)] = tile[q];
+  }
 }
 
 __global__ void k_ntt_scale(Fr* __restrict__ a, size_t n, const Fr* __restrict__ tab, int nvec,
@@ -165,19 +224,30 @@ void ntt_plan_free(NttPlan& pl) {
   pl = NttPlan();
 }
 
-// DIF pass of the inverse transform (natural -> bit-reversed), without 1/n.
-static hipError_t ntt_dif(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size_t vstride, hipStream_t st) {
+// DIF pass of the inverse transform (natural -> bit-reversed), 1/n and the coset scale fused
+// into the last (LDS) pass when `scale` is given.  The stages above the LDS tile run as one
+// column pass (logn <= 21) or as radix-2 global passes (larger domains).
+static hipError_t ntt_dif(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size_t vstride, const Fr* scale,
+                          hipStream_t st) {
   const size_t n = pl.n;
   const int logt = pl.logn < NTT_LDS_LOG ? pl.logn : NTT_LDS_LOG;
+  const int top = pl.logn - logt;
+  const int kcol = top <= NTT_COL_TILE_LOG ? top : 0;  // one column pass, or radix-2 passes (logn > 21)
   const size_t nb = (n >> 1) * nvec;
-  for (int s = 0; s < pl.logn - logt; s++) {
+  for (int s = 0; s < top - kcol; s++) {
     size_t half = n >> (s + 1);
     hipLaunchKernelGGL(k_ntt_dif_stage, dim3(zk_grid(nb, 256)), dim3(256), 0, st, d, n, half, tw, n / (2 * half),
                        nvec, vstride);
   }
+  if (kcol > 0) {
+    const unsigned groups = (unsigned)((((size_t)1 << (pl.logn - kcol)) / ((size_t)NTT_COL_TILE >> kcol)) * nvec);
+    hipLaunchKernelGGL(k_ntt_cols<true>, dim3(groups), dim3(256), 0, st, d, pl.logn, kcol, tw, nvec, vstride);
+  }
   if (logt > 0)
     hipLaunchKernelGGL(k_ntt_lds<true>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
-                       nvec, vstride);
+                       nvec, vstride, scale);
+  else if (scale)
+    hipLaunchKernelGGL(k_ntt_scale, dim3(zk_grid(pl.n * nvec, 256)), dim3(256), 0, st, d, pl.n, scale, nvec, vstride);
   return hipGetLastError();
 }
 
@@ -185,11 +255,17 @@ static hipError_t ntt_dif(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size
 static hipError_t ntt_dit(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size_t vstride, hipStream_t st) {
   const size_t n = pl.n;
   const int logt = pl.logn < NTT_LDS_LOG ? pl.logn : NTT_LDS_LOG;
+  const int top = pl.logn - logt;
+  const int kcol = top <= NTT_COL_TILE_LOG ? top : 0;
   const size_t nb = (n >> 1) * nvec;
   if (logt > 0)
     hipLaunchKernelGGL(k_ntt_lds<false>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
-                       nvec, vstride);
-  for (int s = logt; s < pl.logn; s++) {
+                       nvec, vstride, (const Fr*)nullptr);
+  if (kcol > 0) {
+    const unsigned groups = (unsigned)((((size_t)1 << (pl.logn - kcol)) / ((size_t)NTT_COL_TILE >> kcol)) * nvec);
+    hipLaunchKernelGGL(k_ntt_cols<false>, dim3(groups), dim3(256), 0, st, d, pl.logn, kcol, tw, nvec, vstride);
+  }
+  for (int s = logt + kcol; s < pl.logn; s++) {
     size_t half = (size_t)1 << s;
     hipLaunchKernelGGL(k_ntt_dit_stage, dim3(zk_grid(nb, 256)), dim3(256), 0, st, d, n, half, tw, n / (2 * half),
                        nvec, vstride);
@@ -200,9 +276,7 @@ static hipError_t ntt_dit(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size
 // In place: nvec vectors (stride vstride) of evaluations on the domain -> evaluations on
 // the odd coset (snarkjs ifft + batchApplyKey + fft).
 hipError_t ntt_coset_shift(const NttPlan& pl, Fr* d, int nvec, size_t vstride, hipStream_t st) {
-  ZK_CHECK(ntt_dif(pl, d, pl.tw_inv, nvec, vstride, st));
-  hipLaunchKernelGGL(k_ntt_scale, dim3(zk_grid(pl.n * nvec, 256)), dim3(256), 0, st, d, pl.n, pl.coset, nvec,
-                     vstride);
+  ZK_CHECK(ntt_dif(pl, d, pl.tw_inv, nvec, vstride, pl.coset, st));
   return ntt_dit(pl, d, pl.tw_fwd, nvec, vstride, st);
 }
 

@@ -125,17 +125,89 @@ int parse_wtns(const uint8_t* buf, size_t len, WtnsView& out) {
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-// ABC over CSR rows.  coef raw = coef * R^2 mod r (snarkjs zkey section 4), w std form, so
-// mont_mul(coef_raw, w) = (coef * w) in Montgomery form.
-__global__ void k_abc(const uint32_t* __restrict__ rowA, const uint32_t* __restrict__ rowB,
-                      const uint32_t* __restrict__ cols, const Fr* __restrict__ coefs,
-                      const Fr* __restrict__ w, size_t n, Fr* __restrict__ abc) {
-  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// ABC as a segmented sum over the flat term array (A rows then B rows; rp[0..2n] row pointers).
+// coef raw = coef * R^2 mod r (snarkjs zkey section 4), w std form, so
+// mont_mul(coef_raw, w) = coef * w * R = Montgomery form of coef*w.  Rows range from 1 to ~130
+// terms (Poseidon S-box inputs carry ~61-term combinations), so one lane per row leaves ~2/3 of
+// the lanes idle; instead lane c takes the ABC_L terms [c*L, c*L+L), emitting the sum of its
+// first row segment to head[c], of its last to tail[c], and rows wholly inside the chunk
+// straight to abc[row]; k_abc_rows stitches rows j and n+j and forms c = a*b.
+constexpr uint32_t ABC_L = 16;
+
+__global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ rp, uint32_t nrows,
+                                                   const uint32_t* __restrict__ cols, const Fr* __restrict__ coefs,
+                                                   const Fr* __restrict__ w, uint32_t K, Fr* __restrict__ head,
+                                                   Fr* __restrict__ tail, Fr* __restrict__ abc) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t p0 = c * ABC_L;
+  if (p0 >= K) return;
+  const uint32_t p1 = p0 + ABC_L < K ? p0 + ABC_L : K;
+  // row containing p0: largest r with rp[r] <= p0 (empty rows share their start with the next)
+  uint32_t lo = 0, hi = nrows - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (rp[mid] <= p0) lo = mid;
+    else hi = mid - 1;
+  }
+  uint32_t r = lo, rend = rp[r + 1];
+  Fr acc = fp_zero<FrP>();
+  bool first = true;
+  // software-pipelined: term p+1's witness gather (and p+2's column index) are in flight while
+  // term p is multiplied
+  uint32_t col1 = (p0 + 1 < p1) ? cols[p0 + 1] : 0u;
+  Fr wv = w[cols[p0]], cf = coefs[p0];
+  for (uint32_t p = p0; p < p1; p++) {
+    Fr wn, cn;
+    uint32_t col2 = 0;
+    if (p + 1 < p1) {
+      wn = w[col1];
+      cn = coefs[p + 1];
+    }
+    if (p + 2 < p1) col2 = cols[p + 2];
+    if (p == rend) {  // row boundary inside the chunk
+      if (first) head[c] = acc;
+      else abc[r] = acc;
+      first = false;
+      acc = fp_zero<FrP>();
+      do {
+        r++;
+        rend = rp[r + 1];
+      } while (rend == p);
+    }
+    acc = fp_add(acc, fp_mul(cf, wv));
+    wv = wn;
+    cf = cn;
+    col1 = col2;
+  }
+  if (first) head[c] = acc;
+  else tail[c] = acc;
+}
+
+__device__ __forceinline__ Fr abc_row(const uint32_t* __restrict__ rp, uint32_t r, uint32_t K,
+                                      const Fr* __restrict__ head, const Fr* __restrict__ tail,
+                                      const Fr* __restrict__ abc) {
+  const uint32_t s = rp[r], e = rp[r + 1];
+  if (s == e) return fp_zero<FrP>();
+  const uint32_t c0 = s / ABC_L, c1 = (e - 1) / ABC_L;
+  const bool starts = (s == c0 * ABC_L);
+  if (c0 == c1) {
+    const uint32_t cend = (c0 + 1) * ABC_L < K ? (c0 + 1) * ABC_L : K;
+    if (starts) return head[c0];
+    if (e == cend) return tail[c0];
+    return abc[r];  // wholly inside the chunk: written by k_abc_chunks
+  }
+  Fr acc = starts ? head[c0] : tail[c0];
+  for (uint32_t c = c0 + 1; c <= c1; c++) acc = fp_add(acc, head[c]);
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) k_abc_rows(const uint32_t* __restrict__ rp, size_t n, uint32_t K,
+                                                  const Fr* __restrict__ head, const Fr* __restrict__ tail,
+                                                  Fr* __restrict__ abc) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  Fr a = fp_zero<FrP>();
-  for (uint32_t k = rowA[j]; k < rowA[j + 1]; k++) a = fp_add(a, fp_mul(coefs[k], w[cols[k]]));
-  Fr b = fp_zero<FrP>();
-  for (uint32_t k = rowB[j]; k < rowB[j + 1]; k++) b = fp_add(b, fp_mul(coefs[k], w[cols[k]]));
+  const Fr a = abc_row(rp, (uint32_t)j, K, head, tail, abc);
+  const Fr b = abc_row(rp, (uint32_t)(n + j), K, head, tail, abc);
   abc[j] = a;
   abc[n + j] = b;
   abc[2 * n + j] = fp_mul(a, b);
@@ -300,6 +372,8 @@ struct ProofSlot {
   MsmScratch<Fq2Ops> g2s;
   Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs
   Fr* abc = nullptr;  // [3n]
+  Fr* abc_head = nullptr;  // [ceil(K / ABC_L)] ABC segmented-sum partials
+  Fr* abc_tail = nullptr;
   Fr* h = nullptr;    // [n]
   G1P* res = nullptr;     // [5]: A', B1', C', H, T
   G2P* resB2 = nullptr;   // [1]
@@ -316,8 +390,7 @@ struct zkfl_key {
   int logn = 0;
   size_t nC = 0;  // C query length
   size_t K = 0;
-  uint32_t* rowA = nullptr;  // [n+1]
-  uint32_t* rowB = nullptr;  // [n+1]
+  uint32_t* rows = nullptr;  // [2n+1]: A rows then B rows over one term array
   uint32_t* cols = nullptr;  // [K]
   Fr* coefs = nullptr;       // [K]
   MsmBases<FqOps> bA, bB1, bC, bH;
@@ -346,7 +419,7 @@ void slot_release(ProofSlot* s) {
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s);
   msm_scratch_free_g2(s->g2s);
-  void* ptrs[] = {s->extra, s->abc, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
+  void* ptrs[] = {s->extra, s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -373,6 +446,9 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   (void)nV;
   ZK_CHECK(hipMalloc(&s->extra, 4 * 32));
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
+  const size_t abc_chunks = (k->K + ABC_L - 1) / ABC_L + 1;
+  ZK_CHECK(hipMalloc(&s->abc_head, abc_chunks * 32));
+  ZK_CHECK(hipMalloc(&s->abc_tail, abc_chunks * 32));
   ZK_CHECK(hipMalloc(&s->h, n * 32));
   ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
@@ -407,7 +483,7 @@ void key_release(zkfl_key* k) {
   msm_bases_free_g1(k->bH);
   msm_bases_free_g2(k->bB2);
   ntt_plan_free(k->ntt);
-  void* ptrs[] = {k->rowA, k->rowB, k->cols, k->coefs};
+  void* ptrs[] = {k->rows, k->cols, k->coefs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete k;
@@ -468,8 +544,13 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(hipEventRecord(s->ev_t, st_asm), "event");
   }
   int pi = prof->begin("abc", st);
-  hipLaunchKernelGGL(k_abc, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rowA, k->rowB, k->cols, k->coefs, d_w, n,
-                     s->abc);
+  if (k->K) {
+    const uint32_t K = (uint32_t)k->K;
+    hipLaunchKernelGGL(k_abc_chunks, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                       (uint32_t)(2 * n), k->cols, k->coefs, d_w, K, s->abc_head, s->abc_tail, s->abc);
+  }
+  hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
+                     s->abc_tail, s->abc);
   prof->end(pi, st, (double)k->K);
   pi = prof->begin("ntt", st);
   HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
@@ -755,12 +836,13 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     hipError_t _e = (x);                                \
     if (_e != hipSuccess) return cleanup(hip_fail(_e, where)); \
   } while (0)
-  KTRY(hipMalloc(&k->rowA, ((size_t)dom + 1) * 4), "alloc rows");
-  KTRY(hipMalloc(&k->rowB, ((size_t)dom + 1) * 4), "alloc rows");
+  KTRY(hipMalloc(&k->rows, (2 * (size_t)dom + 1) * 4), "alloc rows");
   KTRY(hipMalloc(&k->cols, (size_t)(ncoef ? ncoef : 1) * 4), "alloc cols");
   KTRY(hipMalloc(&k->coefs, (size_t)(ncoef ? ncoef : 1) * 32), "alloc coefs");
-  KTRY(hipMemcpyAsync(k->rowA, rowptr.data(), ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st), "upload");
-  KTRY(hipMemcpyAsync(k->rowB, rowptr.data() + dom + 1, ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st), "upload");
+  // combined row pointers: A rows [0, dom), B rows [dom, 2 dom) over one term array (rowA[dom] == rowB[0])
+  KTRY(hipMemcpyAsync(k->rows, rowptr.data(), (size_t)dom * 4, hipMemcpyHostToDevice, st), "upload");
+  KTRY(hipMemcpyAsync(k->rows + dom, rowptr.data() + dom + 1, ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st),
+       "upload");
   if (ncoef) {
     KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
     KTRY(hipMemcpyAsync(k->coefs, coefs.data(), (size_t)ncoef * 32, hipMemcpyHostToDevice, st), "upload");
