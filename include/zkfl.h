@@ -125,6 +125,14 @@ int zkfl_wprog_free(zkfl_wprog* prog);
 int zkfl_wprog_info(const zkfl_wprog* prog, uint32_t* n_wires, uint32_t* n_inputs, uint32_t* n_public);
 /* Byte size of one .wtns image for this program (snarkjs wtns v2: 76 + 32 x n_wires). */
 size_t zkfl_wtns_size(const zkfl_wprog* prog);
+/* circom's input.json (one object of signal name -> number | decimal/0x string | nested arrays;
+ * negatives reduced mod r) -> the flattened input vector, using the signal table of a program
+ * image.  Host only (no device needed).  inputs_out: room for `cap` values of 32 B; *n_inputs
+ * receives the count.  Missing signal / wrong shape / non-integer -> ZKFL_E_ARG. */
+int zkfl_wprog_parse_inputs(const uint8_t* prog, size_t len, const char* input_json, uint8_t* inputs_out, size_t cap,
+                            size_t* n_inputs);
+/* One witness from input.json -> one .wtns image (the generate_witness.cjs call, :758-767). */
+int zkfl_witness_compute_json(zkfl_ctx* ctx, const zkfl_wprog* prog, const char* input_json, uint8_t* wtns_out);
 /* n witnesses -> n .wtns images at wtns_out + i * zkfl_wtns_size(prog). */
 int zkfl_witness_compute(zkfl_ctx* ctx, const zkfl_wprog* prog, size_t n, const uint8_t* inputs, uint8_t* wtns_out);
 /* n witnesses computed straight into device-resident witnesses for `key` (no host round trip). */

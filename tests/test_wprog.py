@@ -22,7 +22,7 @@ def interpret(img: bytes, inputs: bytes):
     """Run a program image on one input vector (pure Python; mirrors csrc/witness.hip)."""
     f = struct.unpack_from("<4s13I", img, 0)
     _, ver, nw, npo, npi, npv, in_first, n_ops, n_lv, n_lcs, n_terms, n_as, n_tm, n_wd = f
-    assert ver == 1
+    assert ver == 2
     o = struct.calcsize("<4s13I")
 
     def u32s(n):
@@ -50,6 +50,12 @@ def interpret(img: bytes, inputs: bytes):
         C = frs((8 + rp) * t)
         M = frs(t * t)
         widths[t] = (rp, C, M)
+    (n_sig,) = u32s(1)
+    for _ in range(n_sig):
+        (ln,) = u32s(1)
+        o += (ln + 3) // 4 * 4
+        (nd,) = u32s(1)
+        u32s(nd + 2)
     assert o == len(img)
 
     w = [0] * nw
@@ -141,3 +147,35 @@ def test_failed_assert_detected():
     bad["remainder"][0] = str(int(bad["remainder"][0]) + 1)
     _, ok = interpret(wprog.compile_program(bb), wprog.input_bytes(bb, bad))
     assert not ok
+
+
+# ---------------------------------------------------------------------------
+# input.json parsing in libzkfl (host-only C ABI: no GPU needed)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name,params,inp", list(_cases()), ids=lambda x: x if isinstance(x, str) else "")
+def test_c_input_json_parser_matches_python(name, params, inp):
+    from zkfl import native
+    b = circuits.build(name, *params)
+    img = wprog.compile_program(b)
+    assert native.parse_inputs(img, json.dumps(inp)) == wprog.input_bytes(b, inp)
+
+
+def test_c_input_json_parser_values_and_errors():
+    from zkfl import native
+    b = circuits.build("poseidon_hash2")
+    img = wprog.compile_program(b)
+    enc = lambda *v: b"".join((x % R).to_bytes(32, "little") for x in v)  # noqa: E731
+    cases = [('{"left": 1, "right": 2}', enc(1, 2)),
+             ('{"right": "-5", "left": "0x10"}', enc(16, -5)),
+             (' {"left":%d,"right":%d,"extra":[1,2]} ' % (R + 3, -R), enc(3, 0)),
+             ('{"left": "%d", "right": "-%d"}' % (2 ** 300, 2 ** 300), enc(2 ** 300, -2 ** 300))]
+    for text, want in cases:
+        assert native.parse_inputs(img, text) == want, text
+    for bad in ('{"left": 1}', '{"left": [1], "right": 2}', '{"left": 1.5, "right": 2}', '[1, 2]',
+                '{"left": 1, "right": 2', '{"left": "a", "right": 2}'):
+        with pytest.raises(native.ZkflError) as e:
+            native.parse_inputs(img, bad)
+        assert e.value.code == -1, bad
+    with pytest.raises(native.ZkflError) as e:
+        native.parse_inputs(img[:-8], '{"left": 1, "right": 2}')
+    assert e.value.code == -2

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "field.h"
+#include "fp_mul_asm.h"
 using namespace zkfl;
 
 #define MACV_S(x, y) asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1" : "+v"(lo), "=&s"(cc), "+v"(hi) : "v"(x), "v"(y));
@@ -37,8 +38,32 @@ __device__ __forceinline__ Fp<PR> mul_sgpr(const Fp<PR>& a, const Fp<PR>& b) {
   return r;
 }
 
+__device__ __forceinline__ Fq mul_whole(const Fq& a, const Fq& b) {
+  uint32_t u[8];
+  ZK_FP_MUL_ASM(u, a.v, b.v, FqP::P, FqP::INV);
+  Fq r;
+  fp_reduce_once<FqP>(r.v, u);
+  return r;
+}
+
 template <int V>
-__device__ __forceinline__ Fq mulv(const Fq& a, const Fq& b) { return V == 0 ? fp_mul(a, b) : mul_sgpr(a, b); }
+__device__ __forceinline__ Fq mulv(const Fq& a, const Fq& b) {
+  return V == 0 ? fp_mul(a, b) : (V == 1 ? mul_sgpr(a, b) : mul_whole(a, b));
+}
+
+__global__ void kcheck2(const Fq* a, const Fq* b, int n, int* bad) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (!fp_eq(mul_whole(a[i], b[i]), fp_mul(a[i], b[i]))) atomicAdd(bad, 1);
+}
+
+__global__ void klat1(Fq* data, int iters, int v) {
+  Fq x = data[1];
+  const Fq y = data[0];
+  if (v == 0) for (int k = 0; k < iters; k++) x = fp_mul(x, y);
+  else for (int k = 0; k < iters; k++) x = mul_whole(x, y);
+  data[1] = x;
+}
 
 template <int V, int CH>
 __global__ __launch_bounds__(64) void kchain(Fq* data, int iters) {
@@ -59,13 +84,30 @@ int main() {
   Fq* d;
   (void)hipMalloc(&d, (size_t)(blocks * threads + 8) * sizeof(Fq));
   (void)hipMemset(d, 0x11, (size_t)(blocks * threads + 8) * sizeof(Fq));
-  void (*ks[4])(Fq*, int) = {kchain<0, 1>, kchain<0, 2>, kchain<1, 1>, kchain<1, 2>};
-  const char* names[4] = {"vcc  1 chain ", "vcc  2 chains", "sgpr 1 chain ", "sgpr 2 chains"};
+  void (*ks[6])(Fq*, int) = {kchain<0, 1>, kchain<0, 2>, kchain<1, 1>, kchain<1, 2>, kchain<2, 1>, kchain<2, 2>};
+  const char* names[6] = {"lib   1 chain ", "lib   2 chains", "sgpr  1 chain ", "sgpr  2 chains", "whole 1 chain ",
+                          "whole 2 chains"};
+  {
+    const int m = 1 << 20;
+    Fq* h = (Fq*)malloc(2 * m * sizeof(Fq));
+    uint64_t st = 88172645463325252ull;
+    for (int i = 0; i < 2 * m; i++)
+      for (int j = 0; j < 8; j++) {
+        st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+        h[i].v[j] = (uint32_t)st & (j == 7 ? 0x1fffffffu : 0xffffffffu);
+      }
+    Fq* dd; int* bad; int hb = 0;
+    (void)hipMalloc(&dd, 2 * m * sizeof(Fq)); (void)hipMalloc(&bad, 4);
+    (void)hipMemcpy(dd, h, 2 * m * sizeof(Fq), hipMemcpyHostToDevice); (void)hipMemset(bad, 0, 4);
+    hipLaunchKernelGGL(kcheck2, dim3(m / 256), dim3(256), 0, 0, dd, dd + m, m, bad);
+    (void)hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+    printf("whole-asm mismatches vs library: %d of %d\n", hb, m);
+  }
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   for (int lds_kib : {10, 0}) {
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 6; v++) {
       float ms = 0;
       for (int rep = 0; rep < 2; rep++) {
         (void)hipEventRecord(a);
@@ -77,6 +119,15 @@ int main() {
       double muls = (double)blocks * threads * iters * ((v & 1) ? 2 : 1);
       printf("LDS %2d KiB/block  %s: %6.1f G Fq-mul/s\n", lds_kib, names[v], muls / ms / 1e6);
     }
+  }
+  for (int v = 0; v < 2; v++) {
+    float ms = 0;
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(klat1, dim3(1), dim3(1), 0, 0, d, 10000, v);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    printf("%s single-lane latency: %.1f ns / mul\n", v ? "whole" : "lib  ", ms * 1e6 / 10000);
   }
   return 0;
 }

@@ -17,6 +17,12 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
 void wprog_free(WProg* p);
 void wprog_info(const WProg* p, uint32_t* n_wires, uint32_t* n_inputs, uint32_t* n_public);
 
+// input.json (circom's input format) -> flattened input signals, n_inputs x 8 u32 std form.
+int wprog_inputs_json(const WProg* p, const char* json, std::vector<uint32_t>& out, std::string& err);
+// same from the image bytes alone (host only, no device)
+int wprog_image_inputs_json(const uint8_t* img, size_t len, const char* json, std::vector<uint32_t>& out,
+                            std::string& err);
+
 // n witnesses; inputs: n x n_inputs x 32 B std form (host); outs_host[j]: device buffer of
 // n_wires std-form Fr for witness j.  ZKFL_E_CONSTRAINT when an assert fails, ZKFL_E_ARG when
 // an input is not < r.

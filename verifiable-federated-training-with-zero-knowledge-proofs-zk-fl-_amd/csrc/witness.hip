@@ -16,7 +16,10 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <cctype>
 #include <cstdio>
+#include <string>
+#include <vector>
 
 #include "common.h"
 #include "field.h"
@@ -195,9 +198,237 @@ struct Reader {
   }
 };
 
+
+struct WSignal {  // one declared input signal (input.json key)
+  std::string name;
+  std::vector<uint32_t> dims;
+  uint32_t first = 0;
+  uint32_t pub = 0;
+};
+
+bool read_signals(Reader& R, std::vector<WSignal>& out) {
+  const uint32_t n = R.u32();
+  if (!R.ok || n > (1u << 20)) return false;
+  for (uint32_t i = 0; i < n; i++) {
+    WSignal sg;
+    const uint32_t len = R.u32();
+    if (!R.ok || len > 4096) return false;
+    const uint8_t* nm = R.take((len + 3) & ~3u);
+    if (!nm) return false;
+    sg.name.assign(reinterpret_cast<const char*>(nm), len);
+    const uint32_t nd = R.u32();
+    if (!R.ok || nd > 16) return false;
+    for (uint32_t d = 0; d < nd; d++) sg.dims.push_back(R.u32());
+    sg.first = R.u32();
+    sg.pub = R.u32();
+    if (!R.ok) return false;
+    out.push_back(std::move(sg));
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// input.json -> flattened input signals (host).  The subset circom's witness calculator accepts
+// for these circuits: one object mapping signal names to a number, a decimal (or 0x hex) string,
+// or nested arrays of those; negatives are reduced mod r as circom does.  Extra keys are
+// ignored (as zkfl/r1cs.py::flatten_inputs does).
+// ---------------------------------------------------------------------------
+struct JVal {
+  enum Kind { SCALAR, ARRAY, OBJECT } kind = SCALAR;
+  std::string text;  // scalar literal (string contents or number text)
+  std::vector<JVal> items;
+  std::vector<std::string> keys;
+};
+
+struct JParser {
+  const char* s;
+  const char* e;
+  std::string err;
+  void ws() {
+    while (s < e && (*s == ' ' || *s == '\n' || *s == '\r' || *s == '\t')) s++;
+  }
+  bool fail(const char* m) {
+    if (err.empty()) err = m;
+    return false;
+  }
+  bool str(std::string& out) {
+    if (s >= e || *s != '"') return fail("expected a string");
+    s++;
+    while (s < e && *s != '"') {
+      if (*s == '\\') return fail("escapes are not supported in input strings");
+      out.push_back(*s++);
+    }
+    if (s >= e) return fail("unterminated string");
+    s++;
+    return true;
+  }
+  bool value(JVal& v, int depth) {
+    if (depth > 32) return fail("nesting too deep");
+    ws();
+    if (s >= e) return fail("unexpected end of input");
+    if (*s == '{' || *s == '[') {
+      const bool obj = *s == '{';
+      const char close = obj ? '}' : ']';
+      v.kind = obj ? JVal::OBJECT : JVal::ARRAY;
+      s++;
+      ws();
+      if (s < e && *s == close) {
+        s++;
+        return true;
+      }
+      for (;;) {
+        ws();
+        std::string k;
+        if (obj) {
+          if (!str(k)) return false;
+          ws();
+          if (s >= e || *s != ':') return fail("expected ':'");
+          s++;
+        }
+        JVal c;
+        if (!value(c, depth + 1)) return false;
+        if (obj) v.keys.push_back(k);
+        v.items.push_back(std::move(c));
+        ws();
+        if (s < e && *s == ',') {
+          s++;
+          continue;
+        }
+        if (s < e && *s == close) {
+          s++;
+          return true;
+        }
+        return fail(obj ? "expected ',' or '}'" : "expected ',' or ']'");
+      }
+    }
+    v.kind = JVal::SCALAR;
+    if (*s == '"') return str(v.text);
+    while (s < e && (isalnum((unsigned char)*s) || *s == '-' || *s == '+' || *s == '.')) v.text.push_back(*s++);
+    if (v.text.empty()) return fail("unexpected character");
+    return true;
+  }
+};
+
+// decimal / 0x-hex integer literal (optional sign) -> std-form Fr limbs (mod r)
+bool literal_to_fr(const std::string& t, uint32_t out[8]) {
+  static const uint64_t RL[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                                 0x30644e72e131a029ull};
+  size_t i = 0;
+  bool neg = false;
+  if (i < t.size() && (t[i] == '-' || t[i] == '+')) neg = t[i++] == '-';
+  unsigned base = 10;
+  if (i + 1 < t.size() && t[i] == '0' && (t[i + 1] == 'x' || t[i + 1] == 'X')) {
+    base = 16;
+    i += 2;
+  }
+  if (i >= t.size()) return false;
+  uint64_t acc[5] = {0, 0, 0, 0, 0};  // < 16 r + 15 < 2^259 before reduction
+  for (; i < t.size(); i++) {
+    const char ch = t[i];
+    unsigned d;
+    if (ch >= '0' && ch <= '9') d = ch - '0';
+    else if (base == 16 && ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+    else if (base == 16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+    else return false;  // fractions / exponents are not field elements
+    unsigned __int128 c = d;
+    for (int k = 0; k < 5; k++) {
+      c += (unsigned __int128)acc[k] * base;
+      acc[k] = (uint64_t)c;
+      c >>= 64;
+    }
+    for (;;) {  // reduce below r
+      bool ge = acc[4] != 0;
+      if (!ge) {
+        ge = true;
+        for (int k = 3; k >= 0; k--)
+          if (acc[k] != RL[k]) {
+            ge = acc[k] > RL[k];
+            break;
+          }
+      }
+      if (!ge) break;
+      uint64_t borrow = 0;
+      for (int k = 0; k < 5; k++) {
+        const unsigned __int128 sub = (unsigned __int128)(k < 4 ? RL[k] : 0) + borrow;
+        borrow = (unsigned __int128)acc[k] < sub ? 1 : 0;
+        acc[k] = (uint64_t)((unsigned __int128)acc[k] - sub);
+      }
+    }
+  }
+  const bool zero = !(acc[0] | acc[1] | acc[2] | acc[3]);
+  if (neg && !zero) {  // r - v
+    uint64_t borrow = 0;
+    for (int k = 0; k < 4; k++) {
+      const unsigned __int128 sub = (unsigned __int128)acc[k] + borrow;
+      borrow = (unsigned __int128)RL[k] < sub ? 1 : 0;
+      acc[k] = (uint64_t)((unsigned __int128)RL[k] - sub);
+    }
+  }
+  for (int k = 0; k < 4; k++) {
+    out[2 * k] = (uint32_t)acc[k];
+    out[2 * k + 1] = (uint32_t)(acc[k] >> 32);
+  }
+  return true;
+}
+
+bool flatten(const JVal& v, const WSignal& sg, size_t dim, std::vector<uint32_t>& out, std::string& err) {
+  if (dim == sg.dims.size()) {
+    if (v.kind != JVal::SCALAR) {
+      err = "input '" + sg.name + "' has too many dimensions";
+      return false;
+    }
+    uint32_t fr[8];
+    if (!literal_to_fr(v.text, fr)) {
+      err = "input '" + sg.name + "': '" + v.text + "' is not an integer";
+      return false;
+    }
+    out.insert(out.end(), fr, fr + 8);
+    return true;
+  }
+  if (v.kind != JVal::ARRAY || v.items.size() != sg.dims[dim]) {
+    std::string shape;
+    for (uint32_t d : sg.dims) shape += (shape.empty() ? "" : ", ") + std::to_string(d);
+    err = "input '" + sg.name + "' has wrong shape, expected (" + shape + ")";
+    return false;
+  }
+  for (const JVal& c : v.items)
+    if (!flatten(c, sg, dim + 1, out, err)) return false;
+  return true;
+}
+
+int inputs_from_json(const std::vector<WSignal>& sigs, const char* json, std::vector<uint32_t>& out,
+                     std::string& err) {
+  if (!json) {
+    err = "null input json";
+    return ZKFL_E_ARG;
+  }
+  JParser P{json, json + strlen(json), ""};
+  JVal root;
+  if (!P.value(root, 0)) {
+    err = "input json: " + P.err;
+    return ZKFL_E_ARG;
+  }
+  P.ws();
+  if (P.s != P.e || root.kind != JVal::OBJECT) {
+    err = "input json: expected one object of signal names";
+    return ZKFL_E_ARG;
+  }
+  for (const WSignal& sg : sigs) {
+    size_t k = 0;
+    while (k < root.keys.size() && root.keys[k] != sg.name) k++;
+    if (k == root.keys.size()) {
+      err = "missing input signal '" + sg.name + "'";
+      return ZKFL_E_ARG;
+    }
+    if (!flatten(root.items[k], sg, 0, out, err)) return ZKFL_E_ARG;
+  }
+  return ZKFL_OK;
+}
+
 }  // namespace
 
 struct WProg {
+  std::vector<WSignal> signals;
   uint32_t n_wires = 0, n_pub_out = 0, n_pub_in = 0, n_prv_in = 0, in_first = 0;
   uint32_t n_ops = 0, n_levels = 0, n_asserts = 0;
   std::vector<uint32_t> level_ptr;
@@ -211,6 +442,42 @@ void wprog_free(WProg* p) {
   delete p;
 }
 
+int wprog_inputs_json(const WProg* p, const char* json, std::vector<uint32_t>& out, std::string& err) {
+  return inputs_from_json(p->signals, json, out, err);
+}
+
+int wprog_image_inputs_json(const uint8_t* img, size_t len, const char* json, std::vector<uint32_t>& out,
+                            std::string& err) {
+  // walk the image to its signal table without touching the device
+  Reader R{img, len};
+  const uint8_t* magic = R.take(4);
+  if (!magic || memcmp(magic, "zkwp", 4) != 0 || R.u32() != 2) {
+    err = "witness program: bad magic/version";
+    return ZKFL_E_FORMAT;
+  }
+  uint32_t h[12];
+  for (int i = 0; i < 12; i++) h[i] = R.u32();
+  const uint32_t n_ops = h[5], n_levels = h[6], n_lcs = h[7], n_terms = h[8], n_asserts = h[9], n_tmpl = h[10],
+                 n_widths = h[11];
+  R.take(4ull * (n_levels + 1));
+  R.take(16ull * n_ops);
+  R.take(4ull * (n_lcs + 1));
+  R.take(36ull * n_terms);
+  R.take(4ull * n_asserts);
+  R.take(32ull * n_tmpl);
+  for (uint32_t k = 0; k < n_widths && R.ok; k++) {
+    const uint32_t t = R.u32(), rp = R.u32();
+    if (t > (uint32_t)MAX_T || rp > 128) R.ok = false;
+    else R.take(32ull * ((8 + rp) * t + (size_t)t * t));
+  }
+  std::vector<WSignal> sigs;
+  if (!R.ok || !read_signals(R, sigs)) {
+    err = "witness program: truncated or inconsistent image";
+    return ZKFL_E_FORMAT;
+  }
+  return inputs_from_json(sigs, json, out, err);
+}
+
 void wprog_info(const WProg* p, uint32_t* nw, uint32_t* n_in, uint32_t* n_pub) {
   if (nw) *nw = p->n_wires;
   if (n_in) *n_in = p->n_pub_in + p->n_prv_in;
@@ -220,7 +487,7 @@ void wprog_info(const WProg* p, uint32_t* nw, uint32_t* n_in, uint32_t* n_pub) {
 int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std::string& err) {
   Reader R{img, len};
   const uint8_t* magic = R.take(4);
-  if (!magic || memcmp(magic, "zkwp", 4) != 0 || R.u32() != 1) {
+  if (!magic || memcmp(magic, "zkwp", 4) != 0 || R.u32() != 2) {
     err = "witness program: bad magic/version";
     return ZKFL_E_FORMAT;
   }
@@ -259,6 +526,17 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
     }
     p->view.width[t] = {rp, (uint32_t)(consts.size() / 32), (uint32_t)(consts.size() / 32 + nc)};
     consts.insert(consts.end(), c, c + 32 * (nc + nm));
+  }
+  if (ok && !read_signals(R, p->signals)) ok = false;
+  if (ok) {  // the signal table must tile the input range exactly, in declaration order
+    uint64_t next = p->in_first;
+    for (const WSignal& sg : p->signals) {
+      uint64_t cnt = 1;
+      for (uint32_t d : sg.dims) cnt *= d;
+      ok = ok && sg.first == next;
+      next += cnt;
+    }
+    ok = ok && next == (uint64_t)p->in_first + p->n_pub_in + p->n_prv_in && R.left == 0;
   }
   if (ok) {
     // structural validation (device code trusts these indices)

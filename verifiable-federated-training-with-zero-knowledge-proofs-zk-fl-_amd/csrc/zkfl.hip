@@ -1242,6 +1242,28 @@ int zkfl_witness_compute(zkfl_ctx* ctx, const zkfl_wprog* prog, size_t n, const 
   return ZKFL_OK;
 }
 
+int zkfl_wprog_parse_inputs(const uint8_t* prog, size_t len, const char* input_json, uint8_t* inputs_out, size_t cap,
+                            size_t* n_inputs) {
+  if (!prog || !input_json || !n_inputs || (cap && !inputs_out)) return fail(ZKFL_E_ARG, "parse_inputs: null argument");
+  std::vector<uint32_t> v;
+  std::string err;
+  int rc = wprog_image_inputs_json(prog, len, input_json, v, err);
+  if (rc != ZKFL_OK) return fail(rc, err);
+  *n_inputs = v.size() / 8;
+  if (*n_inputs > cap) return fail(ZKFL_E_ARG, "parse_inputs: output buffer too small");
+  memcpy(inputs_out, v.data(), v.size() * 4);
+  return ZKFL_OK;
+}
+
+int zkfl_witness_compute_json(zkfl_ctx* ctx, const zkfl_wprog* prog, const char* input_json, uint8_t* wtns_out) {
+  if (!ctx || !prog || !input_json || !wtns_out) return fail(ZKFL_E_ARG, "witness_compute_json: null argument");
+  std::vector<uint32_t> v;
+  std::string err;
+  int rc = wprog_inputs_json(prog->p, input_json, v, err);
+  if (rc != ZKFL_OK) return fail(rc, err);
+  return zkfl_witness_compute(ctx, prog, 1, reinterpret_cast<const uint8_t*>(v.data()), wtns_out);
+}
+
 int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const zkfl_key* key, size_t n,
                                   const uint8_t* inputs, zkfl_witness** out) {
   if (!ctx || !prog || !key || (n && (!out || !inputs))) return fail(ZKFL_E_ARG, "witness_compute: null argument");

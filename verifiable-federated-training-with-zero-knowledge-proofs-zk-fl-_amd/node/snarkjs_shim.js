@@ -5,11 +5,15 @@
 // tests/full_system_simulation.mjs:773-776):
 //   node snarkjs_shim.js groth16 prove <circuit_final.zkey> <witness.wtns> <proof.json> <public.json>
 //   node snarkjs_shim.js groth16 verify <verification_key.json> <public.json> <proof.json>
+//   node snarkjs_shim.js wtns calculate <circuit.zkwp> <input.json> <witness.wtns>
+//     (snarkjs wtns calculate / generate_witness.cjs, :758-767; the .zkwp witness program image
+//      from `python -m zkfl compile` plays the role of the circuit's .wasm)
 //     (:865-868; exit 0 + "OK!" when valid, exit 1 + "Invalid proof" otherwise)
 // API (snarkjs shape):
 //   const { groth16 } = require('./snarkjs_shim.js');
 //   const { proof, publicSignals } = await groth16.prove(zkeyFileOrBuffer, wtnsFileOrBuffer);
 //   const ok = await groth16.verify(vKeyObject, publicSignals, proof);
+//   const wtnsBuffer = await wtns.calculate(inputObject, zkwpFileOrBuffer);
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -86,7 +90,21 @@ async function verify(vk, publicSignals, proof) {
   return addon.verify(ctx, vkBuffer(vk), pub, pr);
 }
 
-module.exports = { groth16: { prove, verify }, addon, proofToJson, vkBuffer };
+const progs = new Map();
+
+async function wtnsCalculate(input, zkwp) {
+  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
+  const id = Buffer.isBuffer(zkwp) ? zkwp : path.resolve(zkwp);
+  let prog = progs.get(id);
+  if (!prog) {
+    prog = addon.loadProgram(ctx, read(zkwp));
+    progs.set(id, prog);
+  }
+  const text = typeof input === 'string' ? input : JSON.stringify(input, (k, v) => (typeof v === 'bigint' ? v.toString() : v));
+  return addon.witness(ctx, prog, text);
+}
+
+module.exports = { groth16: { prove, verify }, wtns: { calculate: wtnsCalculate }, addon, proofToJson, vkBuffer };
 
 if (require.main === module) {
   const [cmd, sub, zkeyF, wtnsF, proofF, publicF] = process.argv.slice(2);
@@ -105,11 +123,19 @@ if (require.main === module) {
       console.error('[ERROR] snarkJS: Invalid proof');
       process.exit(1);
     }).catch((e) => { console.error(e.message); process.exit(1); });
+  } else if (cmd === 'wtns' && sub === 'calculate' && proofF) {
+    // argument order: wtns calculate <circuit.zkwp> <input.json> <out.wtns>
+    const [progF, inputF, outF] = [zkeyF, wtnsF, proofF];
+    wtnsCalculate(fs.readFileSync(inputF, 'utf8'), progF).then((w) => {
+      fs.writeFileSync(outF, w);
+      process.exit(0);
+    }).catch((e) => { console.error(e.message); process.exit(1); });
   } else if (cmd === 'version') {
     console.log('zkfl ' + addon.version());
   } else {
     console.error('usage: snarkjs_shim.js groth16 prove <zkey> <wtns> <proof.json> <public.json>\n' +
-                  '       snarkjs_shim.js groth16 verify <vkey.json> <public.json> <proof.json>');
+                  '       snarkjs_shim.js groth16 verify <vkey.json> <public.json> <proof.json>\n' +
+                  '       snarkjs_shim.js wtns calculate <circuit.zkwp> <input.json> <out.wtns>');
     process.exit(99);
   }
 }

@@ -14,6 +14,8 @@
 //   keyInfo(key) -> {nVars, nPublic, domainSize}
 //   prove(ctx, key, wtnsBuffer[, rsBuffer]) -> Promise<{proof: Buffer(256), publicSignals: Buffer}>
 //   verify(ctx, vkBuffer, publicBuffer, proofBuffer) -> Promise<boolean>   (zkfl_groth16_verify)
+//   loadProgram(ctx, zkwpBuffer) -> prog                                   (zkfl_wprog_load)
+//   witness(ctx, prog, inputJsonString) -> Promise<Buffer(.wtns)>          (zkfl_witness_compute_json)
 #include <node_api.h>
 
 #include <cstring>
@@ -46,6 +48,7 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
 
 void ctx_finalize(napi_env, void* data, void*) { zkfl_ctx_destroy(static_cast<zkfl_ctx*>(data)); }
 void key_finalize(napi_env, void* data, void*) { zkfl_key_free(static_cast<zkfl_key*>(data)); }
+void prog_finalize(napi_env, void* data, void*) { zkfl_wprog_free(static_cast<zkfl_wprog*>(data)); }
 
 napi_value CreateContext(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -236,6 +239,88 @@ napi_value Verify(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+napi_value LoadProgram(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void* ctx = nullptr;
+  void* data = nullptr;
+  size_t len = 0;
+  if (argc < 2 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &data, &len) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "loadProgram(ctx, zkwpBuffer)");
+    return nullptr;
+  }
+  zkfl_wprog* prog = nullptr;
+  int rc = zkfl_wprog_load(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(data), len, &prog);
+  if (rc) return throw_err(env, rc);
+  napi_value ext;
+  napi_create_external(env, prog, prog_finalize, nullptr, &ext);
+  return ext;
+}
+
+struct WitnessWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  zkfl_ctx* ctx = nullptr;
+  zkfl_wprog* prog = nullptr;
+  std::string json;
+  std::vector<uint8_t> wtns;
+  int rc = 0;
+  std::string err;
+};
+
+void witness_execute(napi_env, void* data) {
+  WitnessWork* w = static_cast<WitnessWork*>(data);
+  w->wtns.resize(zkfl_wtns_size(w->prog));
+  w->rc = zkfl_witness_compute_json(w->ctx, w->prog, w->json.c_str(), w->wtns.data());
+  if (w->rc) w->err = zkfl_last_error();
+}
+
+void witness_complete(napi_env env, napi_status, void* data) {
+  WitnessWork* w = static_cast<WitnessWork*>(data);
+  if (w->rc) {
+    napi_value msg, err;
+    std::string m = "zkfl witness failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_reject_deferred(env, w->deferred, err);
+  } else {
+    napi_value buf;
+    void* p;
+    napi_create_buffer_copy(env, w->wtns.size(), w->wtns.data(), &p, &buf);
+    napi_resolve_deferred(env, w->deferred, buf);
+  }
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value Witness(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *prog = nullptr;
+  size_t jlen = 0;
+  if (argc < 3 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_value_external(env, argv[1], &prog) != napi_ok ||
+      napi_get_value_string_utf8(env, argv[2], nullptr, 0, &jlen) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "witness(ctx, prog, inputJsonString)");
+    return nullptr;
+  }
+  WitnessWork* w = new WitnessWork();
+  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->prog = static_cast<zkfl_wprog*>(prog);
+  w->json.resize(jlen + 1);
+  napi_get_value_string_utf8(env, argv[2], &w->json[0], jlen + 1, &jlen);
+  w->json.resize(jlen);
+  napi_value promise, name;
+  napi_create_promise(env, &w->deferred, &promise);
+  napi_create_string_utf8(env, "zkfl_witness", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, nullptr, name, witness_execute, witness_complete, w, &w->work);
+  napi_queue_async_work(env, w->work);
+  return promise;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -245,6 +330,8 @@ napi_value Init(napi_env env, napi_value exports) {
       {"keyInfo", nullptr, KeyInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"loadProgram", nullptr, LoadProgram, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"witness", nullptr, Witness, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -60,6 +60,9 @@ SIGNATURES = {
     "zkfl_wtns_size": (C.c_size_t, [_P]),
     "zkfl_witness_compute": (C.c_int, [_P, _P, C.c_size_t, C.c_char_p, _U8P]),
     "zkfl_witness_compute_resident": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_char_p, C.POINTER(_P)]),
+    "zkfl_wprog_parse_inputs": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, _U8P, C.c_size_t,
+                                          C.POINTER(C.c_size_t)]),
+    "zkfl_witness_compute_json": (C.c_int, [_P, _P, C.c_char_p, _U8P]),
 }
 
 
@@ -282,6 +285,14 @@ class ResidentWitness:
             pass
 
 
+def parse_inputs(image: bytes, input_json: str, cap: int = 1 << 20) -> bytes:
+    """circom input.json -> flattened input vector via the program's signal table (host only)."""
+    out = _buf(32 * cap)
+    n = C.c_size_t()
+    check(lib().zkfl_wprog_parse_inputs(image, len(image), input_json.encode(), out, cap, C.byref(n)))
+    return bytes(out)[:32 * n.value]
+
+
 class WitnessProgram:
     """A compiled circuit witness program (zkfl.wprog image) loaded on the device: the
     replacement of circom's <circuit>.wasm + generate_witness.cjs."""
@@ -319,6 +330,12 @@ class WitnessProgram:
         check(lib().zkfl_witness_compute(self.ctx.h, self.h, n, self._inputs(inputs), out))
         ob = bytes(out)
         return [ob[i * self.wtns_size:(i + 1) * self.wtns_size] for i in range(n)]
+
+    def compute_json(self, input_json: str) -> bytes:
+        """One witness from circom's input.json text -> .wtns image."""
+        out = _buf(self.wtns_size)
+        check(lib().zkfl_witness_compute_json(self.ctx.h, self.h, input_json.encode(), out))
+        return bytes(out)
 
     def compute_resident(self, key: ProvingKey, inputs) -> list:
         """-> ResidentWitness per input, computed in HBM for `key` (no host round trip)."""

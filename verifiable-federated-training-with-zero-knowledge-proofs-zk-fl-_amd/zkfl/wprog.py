@@ -13,7 +13,7 @@ independent, so the GPU runs one launch per level with one lane per (witness, op
 circuit (sgd_verified(128,4,7)) has 3,857 ops in 15 levels.
 
 Image layout (all little-endian u32 unless noted; Fr values 32 B Montgomery form, R = 2^256):
-  "zkwp" | version=1 | n_wires | n_pub_out | n_pub_in | n_prv_in | in_first
+  "zkwp" | version=2 | n_wires | n_pub_out | n_pub_in | n_prv_in | in_first
   | n_ops | n_levels | n_lcs | n_terms | n_asserts | n_templates | n_widths
   | level_ptr[n_levels+1]                       (op index ranges, ops stored level by level)
   | ops[n_ops] x 4 u32: kind | out | lc0 | aux   (kind: 0 LC, 1 MUL, 2 INV, 3 BITS, 4 POS;
@@ -24,6 +24,9 @@ Image layout (all little-endian u32 unless noted; Fr values 32 B Montgomery form
   | asserts[n_asserts]                          (lc0 of A; B = lc0+1, C = lc0+2)
   | templates[n_templates] x 8 u32: n_sbox | live bitmap words[7]   (204 S-boxes max)
   | widths[n_widths]: t | rp | C[(8+rp)*t] (Fr) | M[t*t] (Fr)
+  | n_signals | signals[n_signals]: name_len | name (padded to 4 B) | ndims | dims[ndims] | first_wire | public
+                                                 (the circuit's input signals in declaration order:
+                                                  what input.json is mapped through, zkfl_witness_compute_json)
 """
 
 from __future__ import annotations
@@ -33,7 +36,7 @@ import struct
 from .field import POSEIDON_RF, POSEIDON_RP, R, poseidon_params
 
 MAGIC = b"zkwp"
-VERSION = 1
+VERSION = 2
 K_LC, K_MUL, K_INV, K_BITS, K_POS = 0, 1, 2, 3, 4
 _MONT = 1 << 256
 _ONE_MONT = _MONT % R
@@ -156,6 +159,11 @@ def compile_program(b) -> bytes:
         parts.append(struct.pack("<2I", t, rp))
         parts.append(b"".join(_mont(c) for c in C))
         parts.append(b"".join(_mont(M[i][j]) for i in range(t) for j in range(t)))
+    parts.append(struct.pack("<I", len(b.inputs)))
+    for name, shape, first, public in b.inputs:
+        nb = name.encode()
+        parts.append(struct.pack("<I", len(nb)) + nb + b"\0" * (-len(nb) % 4))
+        parts.append(struct.pack(f"<I{len(shape)}I", len(shape), *shape) + struct.pack("<2I", first, int(public)))
     return b"".join(parts)
 
 
