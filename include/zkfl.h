@@ -78,7 +78,7 @@ int zkfl_ctx_synchronize(zkfl_ctx* ctx);
 int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out);
 int zkfl_key_free(zkfl_key* key);
 int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
-/* Number of proofs kept in flight by zkfl_groth16_prove_batch (1..16, default 3).  Each slot
+/* Number of proofs kept in flight by zkfl_groth16_prove_batch (1..32, default 3).  Each slot
  * owns three HIP streams and its own scratch; proofs in different slots overlap on the GPU.
  * HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): set it to >= 3 x slots
  * in the environment before the first HIP call, or the slots serialize. */

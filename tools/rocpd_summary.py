@@ -7,6 +7,9 @@
       the dispatches of bench.py's serialized roofline pass (the last `launches` dispatches of
       each instrumented kernel in a traced bench.py run): median / mean duration, to compare with
       the bench line's roofline.avg_launch_ms (median) / mean_launch_ms
+  rocpd_summary.py breakdown RUN.db OUT.csv [PROOFS]
+      per-proof kernel time of bench.py's serialized roofline pass (the last PROOFS=6 proofs,
+      one slot, every kernel alone on the GPU): where a proof's device time goes
   rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json
       per-kernel average FETCH_SIZE / WRITE_SIZE per launch (separate --pmc passes, as
       MI355X_MICROARCH.md §rocprofv3 PMC slots requires), plus the FETCH_SIZE calibration of the
@@ -88,8 +91,39 @@ def roofline(db, bench_log, out):
         json.dump(res, f, indent=1)
 
 
+def _short(name):
+    name = name.split("(")[0] if not name.startswith("void rocprim") else "rocprim::" + name.split("detail::")[2].split("<")[0]
+    return name.replace("void ", "").replace("zkfl::", "").replace("(anonymous namespace)::", "")
+
+
+def breakdown(db, out, proofs=6):
+    """k_set_extra opens every proof (zkfl.hip enqueue_proof); the roofline pass is the last
+    `proofs` proofs of the run, serialized on one stream."""
+    c = sqlite3.connect(db)
+    starts = [r[0] for r in c.execute("select start from kernels where name like '%k_set_extra%' order by start")]
+    t0 = starts[-proofs]
+    rows = c.execute("select name, count(*), sum(end-start) from kernels where start >= ? group by name", (t0,)).fetchall()
+    span = c.execute("select max(end) - ? from kernels where start >= ?", (t0, t0)).fetchone()[0]
+    agg = {}
+    for name, cnt, tot in rows:
+        k = _short(name)
+        a = agg.setdefault(k, [0, 0])
+        a[0] += cnt
+        a[1] += tot
+    busy = sum(v[1] for v in agg.values())
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "launches_per_proof", "ms_per_proof", "pct_of_busy"])
+        for k, (cnt, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            w.writerow([k, round(cnt / proofs, 2), round(tot / 1e6 / proofs, 4), round(100 * tot / busy, 2)])
+        w.writerow(["(busy total)", "", round(busy / 1e6 / proofs, 4), 100.0])
+        w.writerow(["(wall span)", "", round(span / 1e6 / proofs, 4), ""])
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "kernels":
+    if sys.argv[1] == "breakdown":
+        breakdown(sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 6)
+    elif sys.argv[1] == "kernels":
         kernels(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "roofline":
         roofline(sys.argv[2], sys.argv[3], sys.argv[4])

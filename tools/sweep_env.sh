@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B sweep of an environment switch on the default bench (GPU box):
+#   bash tools/sweep_env.sh VAR "v1 v2 ..." [extra bench args]
+set -o pipefail
+VAR=$1; VALS=$2; shift 2
+mkdir -p gpurun_out/sweep
+for v in $VALS; do
+  env $VAR=$v timeout -k 10 150 python -u bench.py --steps 96 --warmup 16 --no-cpu-baseline "$@" > gpurun_out/sweep/${VAR}_$v.log 2>&1 || exit 1
+  echo "$VAR=$v $(tail -1 gpurun_out/sweep/${VAR}_$v.log | python -c 'import json,sys;d=json.loads(sys.stdin.read());print(d["value"], d["stage_ms_isolated_per_proof"], d["roofline"]["valu"])')"
+done

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -437,8 +438,11 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
-  ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
-  ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
+  static const int streams = getenv("ZKFL_SLOT_STREAMS") ? atoi(getenv("ZKFL_SLOT_STREAMS")) : 3;
+  if (streams > 1) {
+    ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
+    ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
+  }
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
@@ -518,8 +522,8 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
-  hipStream_t st_g2 = prof->serialize ? st : s->st_g2;
-  hipStream_t st_asm = prof->serialize ? st : s->st_asm;
+  hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
+  hipStream_t st_asm = (prof->serialize || !s->st_asm) ? st : s->st_asm;
   const size_t nV = k->nVars, n = k->n;
   memcpy(s->pinned + 256, rs_host, 64);
   int pp = prof->begin("prove", st);
@@ -966,7 +970,7 @@ int zkfl_groth16_prove_resident(zkfl_ctx* ctx, zkfl_key* key, const zkfl_witness
 }
 
 int zkfl_key_set_slots(zkfl_key* key, int slots) {
-  if (!key || slots < 1 || slots > 16) return fail(ZKFL_E_ARG, "slots must be in 1..16");
+  if (!key || slots < 1 || slots > 32) return fail(ZKFL_E_ARG, "slots must be in 1..32");
   (void)hipSetDevice(key->ctx->device);
   for (ProofSlot* s : key->slots) {
     if (s->busy) return fail(ZKFL_E_ARG, "slots busy");
