@@ -10,6 +10,9 @@
   rocpd_summary.py breakdown RUN.db OUT.csv [PROOFS]
       per-proof kernel time of bench.py's serialized roofline pass (the last PROOFS=6 proofs,
       one slot, every kernel alone on the GPU): where a proof's device time goes
+  rocpd_summary.py timeline RUN.db OUT.txt
+      concurrency over the timed (throughput) region of a traced bench.py run: fraction of wall time
+      with k kernels of each category running, from 10-us samples
   rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json
       per-kernel average FETCH_SIZE / WRITE_SIZE per launch (separate --pmc passes, as
       MI355X_MICROARCH.md §rocprofv3 PMC slots requires), plus the FETCH_SIZE calibration of the
@@ -92,8 +95,10 @@ def roofline(db, bench_log, out):
 
 
 def _short(name):
-    name = name.split("(")[0] if not name.startswith("void rocprim") else "rocprim::" + name.split("detail::")[2].split("<")[0]
-    return name.replace("void ", "").replace("zkfl::", "").replace("(anonymous namespace)::", "")
+    name = name.replace("(anonymous namespace)::", "")
+    if name.startswith("void rocprim"):
+        return "rocprim::" + name.split("detail::")[2].split("<")[0]
+    return name.split("(")[0].replace("void ", "").replace("zkfl::", "")
 
 
 def breakdown(db, out, proofs=6):
@@ -120,8 +125,56 @@ def breakdown(db, out, proofs=6):
         w.writerow(["(wall span)", "", round(span / 1e6 / proofs, 4), ""])
 
 
+def _category(name):
+    for key, cat in (("k_msm_accumulate<zkfl::FqOps", "acc_g1"), ("k_msm_accumulate<zkfl::Fq2Ops", "acc_g2"),
+                     ("bucket_sum", "stitch"), ("reduce_level", "reduce"), ("sum8", "reduce"), ("rocprim", "sort"),
+                     ("k_ntt", "ntt"), ("k_abc", "abc"), ("assemble", "asm")):
+        if key in name:
+            return cat
+    return "other"
+
+
+def timeline(db, out, step_us=10.0):
+    """Samples the window between the first accumulate of the timed region and the start of the
+    serialized roofline pass (its first k_set_extra is the 7th from last)."""
+    c = sqlite3.connect(db)
+    ks = c.execute("select name, start, end from kernels order by start").fetchall()
+    sx = [k[1] for k in ks if "k_set_extra" in k[0]]
+    t_end = sx[-7]
+    t_begin = sx[len(sx) // 4]  # skip warmup-ish quarter
+    cats = {}
+    for name, s0, e0 in ks:
+        if e0 < t_begin or s0 > t_end:
+            continue
+        cats.setdefault(_category(name), []).append((max(s0, t_begin), min(e0, t_end)))
+    nsamp = int((t_end - t_begin) / (step_us * 1e3))
+    lines = [f"window {(t_end - t_begin) / 1e6:.2f} ms, {nsamp} samples of {step_us} us"]
+    import bisect
+    tot_any = [0] * nsamp
+    for cat, iv in sorted(cats.items()):
+        cnt = [0] * nsamp
+        for s0, e0 in iv:
+            a = int((s0 - t_begin) / (step_us * 1e3))
+            b = int((e0 - t_begin) / (step_us * 1e3))
+            for k in range(max(a, 0), min(b + 1, nsamp)):
+                cnt[k] += 1
+                tot_any[k] += 1
+        hist = {}
+        for v in cnt:
+            hist[v] = hist.get(v, 0) + 1
+        busy = sum(1 for v in cnt if v) / max(1, nsamp)
+        mean = sum(cnt) / max(1, nsamp)
+        lines.append(f"{cat:8s} busy {busy:6.1%}  mean running {mean:5.2f}  dist " +
+                     " ".join(f"{k}:{v / nsamp:.0%}" for k, v in sorted(hist.items()) if v / nsamp >= 0.01))
+    lines.append(f"all      mean running {sum(tot_any) / max(1, nsamp):5.2f}")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "breakdown":
+    if sys.argv[1] == "timeline":
+        timeline(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "breakdown":
         breakdown(sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 6)
     elif sys.argv[1] == "kernels":
         kernels(sys.argv[2], sys.argv[3])

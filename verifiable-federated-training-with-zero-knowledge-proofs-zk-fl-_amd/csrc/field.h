@@ -313,4 +313,32 @@ struct Fq2Ops {
   static ZK_DEV T from_mont(const T& a) { return f2_from_mont(a); }
 };
 
+// Out-of-line Fq multiplication.  The inlined FIPS multiply is ~2.5 KB of code; every curve
+// operation inlines several (a G2 XYZZ addition: 42), so kernels built from inlined products
+// run to 60-600 KB of code, beyond the instruction cache a CU pair shares.  Latency-tolerant
+// kernels use this one out-of-line copy instead (FqOpsCall / Fq2OpsCall).
+static __device__ __noinline__ Fq fq_mul_call(Fq a, Fq b) { return fp_mul<FqP>(a, b); }
+
+static __device__ __noinline__ Fq2 f2_mul_call(Fq2 a, Fq2 b) {
+  Fq t0 = fq_mul_call(a.c0, b.c0);
+  Fq t1 = fq_mul_call(a.c1, b.c1);
+  Fq t2 = fq_mul_call(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+static __device__ __noinline__ Fq2 f2_sqr_call(Fq2 a) {
+  Fq t0 = fq_mul_call(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fq t1 = fq_mul_call(a.c0, a.c1);
+  return {t0, fp_dbl(t1)};
+}
+
+// The same field interfaces with the multiplications out of line (same storage types).
+struct FqOpsCall : FqOps {
+  static ZK_DEV T mul(const T& a, const T& b) { return fq_mul_call(a, b); }
+  static ZK_DEV T sqr(const T& a) { return fq_mul_call(a, a); }
+};
+struct Fq2OpsCall : Fq2Ops {
+  static ZK_DEV T mul(const T& a, const T& b) { return f2_mul_call(a, b); }
+  static ZK_DEV T sqr(const T& a) { return f2_sqr_call(a); }
+};
+
 }  // namespace zkfl

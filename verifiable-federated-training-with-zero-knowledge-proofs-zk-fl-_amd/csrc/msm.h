@@ -14,15 +14,16 @@
 //    no window combination.  288 GB of HBM makes the 16x base expansion (~2 GB for the
 //    2^18-constraint training circuit) free.
 //  * Signed digits in [-2^15, 2^15]; the sign is applied by negating y on the fly.
-//  * (bucket, entry) pairs are radix-sorted (rocPRIM, 16 key bits), bucket ranges found by
-//    adjacent-key compare.  The sorted entries are cut into fixed chunks of L entries, one lane
-//    each, independent of bucket boundaries: every lane does exactly L additions (no idle lanes
-//    behind a short bucket tail, no task->bucket search), emits a partial sum at each bucket
-//    change (first segment -> head[chunk], last -> tail[chunk], a bucket wholly inside the chunk
-//    -> its final sum), and k_msm_bucket_sum stitches each bucket from its chunks' partials.
+//  * (bucket, entry) pairs are radix-sorted (rocPRIM, 16 key bits).  The sorted entries are cut
+//    into fixed chunks of L entries, one lane each, independent of bucket boundaries: every lane
+//    does exactly L additions.  A bucket run that starts and ends inside its chunk is final and
+//    written to its bucket; a run cut by a chunk edge becomes an "item" (<= 2 per chunk).
+//  * Stitching levels apply the same run logic to the items, SG per lane, until one lane holds
+//    what is left: a bucket spread over many chunks is summed by a shallow tree instead of one
+//    lane walking its chunks (that serial walk, not the arithmetic, used to set the MSM's latency).
 //  * Accumulation uses XYZZ + affine mixed additions (10 Fq mul for G1).
-//  * Bucket reduction sum_b (b+1) S_b uses grouped running sums (groups of RG buckets),
-//    recursively on the group sums, then a Horner combination.
+//  * Bucket reduction sum_b (b+1) S_b: 64-item blocks per wave (LDS suffix scan + tree, depth ~13
+//    additions), three levels for 2^15 buckets, the last writing the MSM result.
 #pragma once
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -37,14 +38,8 @@ namespace zkfl {
 #ifndef MSM_G1_WAVES
 #define MSM_G1_WAVES 4
 #endif
-#ifndef MSM_G1_PF
-#define MSM_G1_PF true
-#endif
 #ifndef MSM_G2_WAVES
 #define MSM_G2_WAVES 1
-#endif
-#ifndef MSM_G2_PF
-#define MSM_G2_PF true
 #endif
 
 // ---------------------------------------------------------------------------
@@ -87,183 +82,223 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
 // Per-MSM kernels
 // ---------------------------------------------------------------------------
 // Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31.
-static __global__ void k_msm_digits(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra,
-                                    const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t n,
-                                    uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
-  const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
-  const uint4* sp = reinterpret_cast<const uint4*>(src);
-  uint4 a = sp[0], b = sp[1];
-  uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t carry = 0;
+// Also counts the non-zero digits into *nnz (the sorted prefix the accumulation covers).
+static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
+                                                           const uint32_t* __restrict__ extra,
+                                                           const uint32_t* __restrict__ sidx, uint32_t extra_start,
+                                                           size_t n, uint16_t* __restrict__ keys,
+                                                           uint32_t* __restrict__ vals, uint32_t* __restrict__ nnz) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t cnt = 0;
+  if (i < n) {
+    const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
+    const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
+    const uint4* sp = reinterpret_cast<const uint4*>(src);
+    uint4 a = sp[0], b = sp[1];
+    uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t carry = 0;
 #pragma unroll
-  for (int j = 0; j < MSM_W; j++) {
-    uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-    int32_t d = (int32_t)(raw + carry);
-    if (d > MSM_NB) {
-      d -= (1 << MSM_C);
-      carry = 1;
-    } else {
-      carry = 0;
+    for (int j = 0; j < MSM_W; j++) {
+      uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+      int32_t d = (int32_t)(raw + carry);
+      if (d > MSM_NB) {
+        d -= (1 << MSM_C);
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      size_t e = i * MSM_W + j;
+      if (d == 0) {
+        keys[e] = MSM_KEY_NONE;
+        vals[e] = 0;
+      } else {
+        uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+        keys[e] = (uint16_t)(mag - 1);
+        vals[e] = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
+        cnt++;
+      }
     }
-    size_t e = i * MSM_W + j;
-    if (d == 0) {
-      keys[e] = MSM_KEY_NONE;
-      vals[e] = 0;
-    } else {
-      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      keys[e] = (uint16_t)(mag - 1);
-      vals[e] = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
-    }
+  }
+  // one atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(nnz, cnt);
+}
+
+// Where a bucket run found by one lane goes (shared by the accumulation and stitching levels).
+// A run [a, b] of bucket k inside a lane's range [q0, q1) is open on the left if it starts the
+// range and the previous range ends in the same bucket, open on the right likewise.  A closed
+// run is the whole bucket: written to buckets[k].  An open run becomes an item of the next
+// stitching level: the left-open run in slot 0, a (only) right-open run in slot 1.  Unused
+// slots are dummies carrying the range's first / last bucket, so item keys stay sorted.
+template <class F>
+ZK_DEV void msm_emit_run(uint32_t k, const XYZZ<F>& acc, bool real, bool open_left, bool open_right,
+                         XYZZ<F>* __restrict__ buckets, uint32_t* __restrict__ okey, XYZZ<F>* __restrict__ oval,
+                         bool& slot0, bool& slot1) {
+  if (!open_left && !open_right) {
+    if (real) buckets[k] = acc;
+  } else if (open_left) {
+    okey[0] = real ? k : (k | MSM_ITEM_DUMMY);
+    if (real) oval[0] = acc;
+    slot0 = true;
+  } else {
+    okey[1] = real ? k : (k | MSM_ITEM_DUMMY);
+    if (real) oval[1] = acc;
+    slot1 = true;
   }
 }
 
-static __global__ void k_msm_bounds(const uint16_t* __restrict__ keys, size_t m,
-                             uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend,
-                             uint32_t* __restrict__ nnz) {
-  size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= m) return;
-  uint16_t k = keys[p];
-  if (k == MSM_KEY_NONE) return;
-  if (p == 0 || keys[p - 1] != k) bstart[k] = (uint32_t)p;
-  const bool last = (p == m - 1 || keys[p + 1] != k);
-  if (last) bend[k] = (uint32_t)(p + 1);
-  if (p == m - 1 || keys[p + 1] == MSM_KEY_NONE) *nnz = (uint32_t)(p + 1);  // non-zero digits
-}
-
-// Lane c adds the sorted entries [c*L, min(c*L+L, nnz)).  Software-pipelined: the key/index of
-// entry p+1 and its base are in flight while entry p is added.
-// MINW: minimum waves per SIMD the register allocator must allow; PF: software-pipeline the
-// next entry's key/index/base loads behind the current addition (costs one affine point of
-// registers).  Chosen per curve in msm_run.
-template <class F, int MINW, bool PF>
+// Level 0: lane c adds the sorted entries [c*L, min(c*L+L, nnz)) (fixed-size chunks, independent
+// of bucket boundaries, so every lane does the same work).  Software-pipelined: the key/index of
+// entry p+1 and its base are in flight while entry p is added.  MINW: minimum waves per SIMD
+// the register allocator must allow (chosen per curve).
+template <class F, int MINW>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
-                                                        const uint16_t* __restrict__ keys,
-                                                        const uint32_t* __restrict__ vals,
-                                                        const Affine<F>* __restrict__ bases,
-                                                        const uint32_t* __restrict__ nnz_ptr,
-                                                        XYZZ<F>* __restrict__ head,
-                                                        XYZZ<F>* __restrict__ tail,
-                                                        XYZZ<F>* __restrict__ buckets) {
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<F>* __restrict__ bases,
+    const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<F>* __restrict__ item_val,
+    XYZZ<F>* __restrict__ buckets) {
   const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nnz = *nnz_ptr;
   const size_t p0 = c * MSM_L;
   if (p0 >= nnz) return;
   const uint32_t p1 = (uint32_t)(p0 + MSM_L < nnz ? p0 + MSM_L : nnz);
+  const uint32_t kprev = p0 > 0 ? keys[p0 - 1] : 0xFFFFFFFFu;
+  const uint32_t knext = p1 < nnz ? keys[p1] : 0xFFFFFFFFu;
+  uint32_t* okey = item_key + 2 * c;
+  XYZZ<F>* oval = item_val + 2 * c;
+  bool slot0 = false, slot1 = false;
   XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t cur = keys[p0];
-  bool first = true;
-  if (PF) {
-    uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
-    if (p0 + 1 < p1) {
-      k1 = keys[p0 + 1];
-      v1 = vals[p0 + 1];
-    }
-    Affine<F> a = bases[v0 & 0x7FFFFFFFu];
-    for (uint32_t p = (uint32_t)p0; p < p1; p++) {
-      Affine<F> an;
-      uint32_t k2 = 0, v2 = 0;
-      if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
-      if (p + 2 < p1) {
-        k2 = keys[p + 2];
-        v2 = vals[p + 2];
-      }
-      acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
-      if (p + 1 < p1 && k1 != cur) {  // bucket boundary inside the chunk
-        if (first) head[c] = acc;
-        else buckets[cur] = acc;     // starts and ends inside this chunk: complete
-        first = false;
-        acc = xyzz_inf<F>();
-        cur = k1;
-      }
-      v0 = v1;
-      v1 = v2;
-      k1 = k2;
-      a = an;
-    }
-  } else {
-    for (uint32_t p = (uint32_t)p0; p < p1; p++) {
-      const uint32_t k = keys[p], v = vals[p];
-      if (k != cur) {
-        if (first) head[c] = acc;
-        else buckets[cur] = acc;
-        first = false;
-        acc = xyzz_inf<F>();
-        cur = k;
-      }
-      Affine<F> a = bases[v & 0x7FFFFFFFu];
-      acc = xyzz_madd<F>(acc, (v & 0x80000000u) ? aff_neg<F>(a) : a);
-    }
+  uint32_t cur = keys[p0], run_start = (uint32_t)p0;
+  uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
+  if (p0 + 1 < p1) {
+    k1 = keys[p0 + 1];
+    v1 = vals[p0 + 1];
   }
-  if (first) head[c] = acc;
-  else tail[c] = acc;
+  Affine<F> a = bases[v0 & 0x7FFFFFFFu];
+  for (uint32_t p = (uint32_t)p0; p < p1; p++) {
+    Affine<F> an;
+    uint32_t k2 = 0, v2 = 0;
+    if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
+    if (p + 2 < p1) {
+      k2 = keys[p + 2];
+      v2 = vals[p + 2];
+    }
+    acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
+    const bool last = p + 1 == p1;
+    if (last || k1 != cur) {
+      msm_emit_run<F>(cur, acc, true, run_start == p0 && kprev == cur, last && knext == cur, buckets, okey, oval,
+                      slot0, slot1);
+      acc = xyzz_inf<F>();
+      cur = k1;
+      run_start = p + 1;
+    }
+    v0 = v1;
+    v1 = v2;
+    k1 = k2;
+    a = an;
+  }
+  if (!slot0) okey[0] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
+  if (!slot1) okey[1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
 }
 
-// Bucket b = its entries [s, e): stitched from the partials of chunks c0 = s/L .. c1 = (e-1)/L.
-template <class F>
-__global__ void __launch_bounds__(64) k_msm_bucket_sum(const uint32_t* __restrict__ bstart,
-                                                        const uint32_t* __restrict__ bend,
-                                                        const uint32_t* __restrict__ nnz_ptr,
-                                                        const XYZZ<F>* __restrict__ head,
-                                                        const XYZZ<F>* __restrict__ tail,
-                                                        XYZZ<F>* __restrict__ buckets) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= MSM_NB) return;
-  const uint32_t s = bstart[b], e = bend[b];
-  if (s == e) {
-    buckets[b] = xyzz_inf<F>();
-    return;
-  }
-  const uint32_t c0 = s / MSM_L, c1 = (e - 1) / MSM_L;
-  const bool starts_chunk = (s == c0 * MSM_L);
-  if (c0 == c1) {
-    const uint32_t nnz = *nnz_ptr;
-    const uint32_t cend = (c0 + 1) * MSM_L < nnz ? (c0 + 1) * MSM_L : nnz;
-    if (starts_chunk) buckets[b] = head[c0];
-    else if (e == cend) buckets[b] = tail[c0];
-    return;  // otherwise wholly inside the chunk: written by k_msm_accumulate
-  }
-  XYZZ<F> acc = starts_chunk ? head[c0] : tail[c0];
-  for (uint32_t c = c0 + 1; c <= c1; c++) acc = xyzz_add<F>(acc, head[c]);
-  buckets[b] = acc;
+// Item count of stitching level `level` (>= 1), derived on the device from nnz.
+ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
+  uint32_t n = 2 * ((nnz + MSM_L - 1) / MSM_L);
+  for (int l = 1; l < level; l++) n = 2 * ((n + MSM_SG - 1) / MSM_SG);
+  return n;
 }
 
-// One level of the grouped running-sum bucket reduction over in[0..K):
-//   acc[g] = sum_{k in group} (k - g*RG + 1) * in[k],   run[g] = sum_{k in group} in[k]
-// acc[g] is pre-scaled by RG^level (level doublings) so all levels sum together.
+// Stitching level: the same run logic over the previous level's items (SG per lane), so a
+// bucket spread over many chunks is summed by a tree of depth log_{SG/2}, not by one lane.
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_reduce_level(const XYZZ<F>* __restrict__ in, int K, int shift_dbls,
-                                   XYZZ<F>* __restrict__ acc_out, XYZZ<F>* __restrict__ run_out) {
-  int g = blockIdx.x * blockDim.x + threadIdx.x;
-  int G = (K + MSM_RG - 1) / MSM_RG;
-  if (g >= G) return;
-  int lo = g * MSM_RG;
-  int hi = lo + MSM_RG;
-  if (hi > K) hi = K;
-  XYZZ<F> run = xyzz_inf<F>();
+__global__ void __launch_bounds__(64) k_msm_stitch(const uint32_t* __restrict__ in_key,
+                                                   const XYZZ<F>* __restrict__ in_val,
+                                                   const uint32_t* __restrict__ nnz_ptr, int level,
+                                                   uint32_t* __restrict__ out_key, XYZZ<F>* __restrict__ out_val,
+                                                   XYZZ<F>* __restrict__ buckets) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t N = msm_items_at(*nnz_ptr, level);
+  const uint32_t q0 = g * MSM_SG;
+  if (q0 >= N) return;
+  const uint32_t q1 = q0 + MSM_SG < N ? q0 + MSM_SG : N;
+  constexpr uint32_t KM = ~MSM_ITEM_DUMMY;
+  const uint32_t kprev = q0 > 0 ? (in_key[q0 - 1] & KM) : 0xFFFFFFFFu;
+  const uint32_t knext = q1 < N ? (in_key[q1] & KM) : 0xFFFFFFFFu;
+  uint32_t* okey = out_key + 2 * g;
+  XYZZ<F>* oval = out_val + 2 * g;
+  bool slot0 = false, slot1 = false, real = false;
   XYZZ<F> acc = xyzz_inf<F>();
-  for (int k = hi - 1; k >= lo; k--) {
-    run = xyzz_add<F>(run, in[k]);
-    acc = xyzz_add<F>(acc, run);
+  uint32_t kq = in_key[q0];
+  uint32_t cur = kq & KM, run_start = q0;
+  for (uint32_t q = q0; q < q1; q++) {
+    const uint32_t kn = q + 1 < q1 ? in_key[q + 1] : 0xFFFFFFFFu;
+    if (!(kq & MSM_ITEM_DUMMY)) {
+      acc = xyzz_add<F>(acc, in_val[q]);
+      real = true;
+    }
+    const bool last = q + 1 == q1;
+    if (last || (kn & KM) != cur) {
+      msm_emit_run<F>(cur, acc, real, run_start == q0 && kprev == cur, last && knext == cur, buckets, okey, oval,
+                      slot0, slot1);
+      acc = xyzz_inf<F>();
+      real = false;
+      cur = kn & KM;
+      run_start = q + 1;
+    }
+    kq = kn;
   }
-  for (int d = 0; d < shift_dbls; d++) acc = xyzz_dbl<F>(acc);
-  acc_out[g] = acc;
-  run_out[g] = run;
+  if (!slot0) okey[0] = (in_key[q0] & KM) | MSM_ITEM_DUMMY;
+  if (!slot1) okey[1] = (in_key[q1 - 1] & KM) | MSM_ITEM_DUMMY;
 }
 
-// out[i] = sum of in[i*8 .. i*8+8)
+// Weighted bucket reduction sum_b (b+1) S_b, one 64-item block per wave.  An item i stands for
+// a group of g = 2^log2g consecutive buckets: s_i = its bucket sum, a_i = sum (b - first + 1) S_b.
+// A block of items combines as  a' = sum_t a_t + g * sum_t t s_t,  s' = sum_t s_t,
+// with sum_t t s_t = sum_{t>=1} R_t for the suffix sums R_t = sum_{u>=t} s_u: a 6-step LDS
+// suffix scan and a 6-step tree (depth ~13 additions per level instead of a lane-serial
+// running sum).  Level 0 reads the buckets as both a and s (g = 1).  The two trees run one after
+// the other: side by side they spill the G2 kernel.
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_sum8(const XYZZ<F>* __restrict__ in, int n, XYZZ<F>* __restrict__ out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int lo = i * 8;
-  if (lo >= n) return;
-  int hi = lo + 8;
-  if (hi > n) hi = n;
-  XYZZ<F> acc = in[lo];
-  for (int k = lo + 1; k < hi; k++) acc = xyzz_add<F>(acc, in[k]);
-  out[i] = acc;
+__global__ void __launch_bounds__(MSM_RB) k_msm_wsum(const XYZZ<F>* __restrict__ in_a, const XYZZ<F>* __restrict__ in_s,
+                                                    int N, int log2g, XYZZ<F>* __restrict__ out_a,
+                                                    XYZZ<F>* __restrict__ out_s) {
+  __shared__ XYZZ<F> shx[MSM_RB];
+  __shared__ XYZZ<F> shy[MSM_RB];
+  const int t = threadIdx.x;
+  const int i = blockIdx.x * MSM_RB + t;
+  XYZZ<F> R = i < N ? in_s[i] : xyzz_inf<F>();
+#pragma unroll 1
+  for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
+    shx[t] = R;
+    __syncthreads();
+    if (t + d < MSM_RB) R = xyzz_add<F>(R, shx[t + d]);
+    __syncthreads();
+  }
+  XYZZ<F> x = t >= 1 ? R : xyzz_inf<F>();
+#pragma unroll 1
+  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {  // tree sum of R_{t>=1}
+    shx[t] = x;
+    __syncthreads();
+    if (t < d) x = xyzz_add<F>(x, shx[t + d]);
+    __syncthreads();
+  }
+  // tree sum of a (level 0 reads the buckets as both a and s: that sum is R_0)
+  XYZZ<F> y = R;
+  if (in_a != in_s) {
+    y = i < N ? in_a[i] : xyzz_inf<F>();
+#pragma unroll 1
+    for (int d = MSM_RB / 2; d >= 1; d >>= 1) {
+      shy[t] = y;
+      __syncthreads();
+      if (t < d) y = xyzz_add<F>(y, shy[t + d]);
+      __syncthreads();
+    }
+  }
+  if (t == 0) {
+    for (int k = 0; k < log2g; k++) x = xyzz_dbl<F>(x);
+    out_a[blockIdx.x] = xyzz_add<F>(y, x);
+    out_s[blockIdx.x] = R;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -309,23 +344,24 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, s.sort_tmp_bytes, s.keys_in, s.keys_out, s.vals_in, s.vals_out, m, 0,
                                      16, st));
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
-  ZK_CHECK(hipMalloc(&s.bstart, MSM_NB * sizeof(uint32_t)));
-  ZK_CHECK(hipMalloc(&s.bend, MSM_NB * sizeof(uint32_t)));
   s.max_chunks = (m + MSM_L - 1) / MSM_L;
-  ZK_CHECK(hipMalloc(&s.head, s.max_chunks * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.tail, s.max_chunks * sizeof(XYZZ<F>)));
+  s.item_cap[0] = 2 * s.max_chunks;
+  s.item_cap[1] = 2 * ((s.item_cap[0] + MSM_SG - 1) / MSM_SG);
+  for (int k = 0; k < 2; k++) {
+    ZK_CHECK(hipMalloc(&s.item_key[k], s.item_cap[k] * sizeof(uint32_t)));
+    ZK_CHECK(hipMalloc(&s.item_val[k], s.item_cap[k] * sizeof(XYZZ<F>)));
+  }
   ZK_CHECK(hipMalloc(&s.buckets, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.red_acc, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.red_run, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.red_tmp, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.red_a, (MSM_NB / MSM_RB + 2 * MSM_RB) * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&s.red_s, (MSM_NB / MSM_RB + 2 * MSM_RB) * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&s.nnz, sizeof(uint32_t)));
   return hipSuccess;
 }
 
 template <class F>
 void msm_scratch_free(MsmScratch<F>& s) {
-  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.bstart, s.bend,
-                  s.head, s.tail, s.buckets, s.red_acc, s.red_run, s.red_tmp, s.nnz};
+  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.item_key[0], s.item_key[1],
+                  s.item_val[0], s.item_val[1], s.buckets, s.red_a, s.red_s, s.nnz};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s = MsmScratch<F>();
@@ -337,6 +373,9 @@ __global__ void k_msm_set_inf(XYZZ<F>* out) {
   *out = xyzz_inf<F>();
 }
 
+// Stream order: digits (+ nnz) -> radix sort by bucket -> accumulate (level 0: fixed chunks,
+// closed runs straight into buckets, open runs as items) -> stitching levels until one lane
+// holds every remaining item -> weighted reduction blocks (3 levels for 2^15 buckets) -> d_out.
 template <class F>
 hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_scalars, const uint32_t* d_extra,
                    XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
@@ -350,53 +389,46 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
   if (need > pl.sort_tmp_bytes || chunks > pl.max_chunks) return hipErrorInvalidValue;
+  ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
-                     b.extra_start, b.n, pl.keys_in, pl.vals_in);
+                     b.extra_start, b.n, pl.keys_in, pl.vals_in, pl.nnz);
   ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
                                      st));
-  ZK_CHECK(hipMemsetAsync(pl.bstart, 0, MSM_NB * sizeof(uint32_t), st));
-  ZK_CHECK(hipMemsetAsync(pl.bend, 0, MSM_NB * sizeof(uint32_t), st));
-  ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_msm_bounds, dim3(zk_grid(m, 256)), dim3(256), 0, st, pl.keys_out, m, pl.bstart, pl.bend,
-                     pl.nnz);
+  ZK_CHECK(hipMemsetAsync(pl.buckets, 0, MSM_NB * sizeof(XYZZ<F>), st));  // ZZ = 0: infinity
   const int pidx = prof ? prof->begin(tag, st) : -1;
   constexpr bool G1 = sizeof(typename F::T) == 32;
-  hipLaunchKernelGGL((k_msm_accumulate<F, G1 ? MSM_G1_WAVES : MSM_G2_WAVES, G1 ? MSM_G1_PF : MSM_G2_PF>),
-                     dim3(zk_grid(chunks, 64)), dim3(64), 0, st, pl.keys_out, pl.vals_out,
-                     b.bases_w, pl.nnz, pl.head, pl.tail, pl.buckets);
+  hipLaunchKernelGGL((k_msm_accumulate<F, G1 ? MSM_G1_WAVES : MSM_G2_WAVES>), dim3(zk_grid(chunks, 64)), dim3(64),
+                     0, st, pl.keys_out, pl.vals_out, b.bases_w, pl.nnz, pl.item_key[0], pl.item_val[0],
+                     pl.buckets);
   if (prof) prof->end(pidx, st, 0.0, pl.nnz);
-  hipLaunchKernelGGL(k_msm_bucket_sum<F>, dim3(zk_grid(MSM_NB, 64)), dim3(64), 0, st, pl.bstart, pl.bend, pl.nnz,
-                     pl.head, pl.tail, pl.buckets);
-  // grouped running-sum reduction
-  const XYZZ<F>* in = pl.buckets;
-  int K = MSM_NB;
-  int level = 0;
-  int nacc = 0;
-  XYZZ<F>* run_bufs[2] = {pl.red_run, pl.red_tmp};
-  while (K > 0) {
-    int G = (K + MSM_RG - 1) / MSM_RG;
-    int shift = 3 * level;  // RG = 8 = 2^3
-    XYZZ<F>* run_out = run_bufs[level & 1];
-    hipLaunchKernelGGL(k_msm_reduce_level<F>, dim3(zk_grid(G, 64)), dim3(64), 0, st, in, K, shift,
-                       pl.red_acc + nacc, run_out);
-    nacc += G;
-    in = run_out + 1;
-    K = G - 1;
-    level++;
+  // stitching levels (item counts here are the host-side upper bounds; kernels use nnz)
+  size_t N = 2 * chunks;
+  int cur = 0;
+  for (int level = 1;; level++) {
+    const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
+    hipLaunchKernelGGL(k_msm_stitch<F>, dim3(zk_grid(lanes, 64)), dim3(64), 0, st, pl.item_key[cur],
+                       pl.item_val[cur], pl.nnz, level, pl.item_key[cur ^ 1], pl.item_val[cur ^ 1], pl.buckets);
+    if (N <= (size_t)MSM_SG) break;
+    N = 2 * lanes;
+    cur ^= 1;
   }
-  // sum all acc entries
-  XYZZ<F>* src = pl.red_acc;
-  XYZZ<F>* dst = pl.red_tmp;
-  int cnt = nacc;
-  while (cnt > 1) {
-    int nout = (cnt + 7) / 8;
-    hipLaunchKernelGGL(k_msm_sum8<F>, dim3(zk_grid(nout, 64)), dim3(64), 0, st, src, cnt, dst);
-    XYZZ<F>* t = src;
-    src = dst;
-    dst = (t == pl.red_acc) ? pl.red_run : t;
-    cnt = nout;
+  // weighted reduction: 2^15 -> 512 -> 8 -> 1
+  const XYZZ<F>* ia = pl.buckets;
+  const XYZZ<F>* is = pl.buckets;
+  int n = MSM_NB, log2g = 0;
+  size_t off = 0;
+  while (true) {
+    const int blocks = (n + MSM_RB - 1) / MSM_RB;
+    XYZZ<F>* oa = blocks == 1 ? d_out : pl.red_a + off;
+    XYZZ<F>* os = pl.red_s + off;
+    hipLaunchKernelGGL(k_msm_wsum<F>, dim3(blocks), dim3(MSM_RB), 0, st, ia, is, n, log2g, oa, os);
+    if (blocks == 1) break;
+    ia = oa;
+    is = os;
+    off += blocks;
+    n = blocks;
+    log2g += 6;  // log2(MSM_RB)
   }
-  ZK_CHECK(hipMemcpyAsync(d_out, src, sizeof(XYZZ<F>), hipMemcpyDeviceToDevice, st));
   return hipGetLastError();
 }
 

@@ -12,7 +12,9 @@ constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 constexpr int MSM_L = 16;                  // sorted entries per accumulation lane (fixed-size chunks)
-constexpr int MSM_RG = 8;                  // running-sum group size in the bucket reduction
+constexpr int MSM_SG = 8;                  // partial sums per lane in each stitching level
+constexpr int MSM_RB = 64;                 // items per block (one wave) in the weighted bucket reduction
+constexpr uint32_t MSM_ITEM_DUMMY = 0x80000000u;  // stitch item flag: padding (its value is infinity)
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
 
 
@@ -38,15 +40,14 @@ struct MsmScratch {
   uint32_t* vals_out = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  uint32_t* bstart = nullptr;  // [NB]
-  uint32_t* bend = nullptr;    // [NB]
   size_t max_chunks = 0;        // ceil(cap * W / L)
-  XYZZ<F>* head = nullptr;      // [max_chunks] sum of the chunk's first bucket segment
-  XYZZ<F>* tail = nullptr;      // [max_chunks] sum of its last segment (when it differs)
+  // stitching items (ping-pong): 2 per chunk / per stitching lane, sorted by bucket
+  uint32_t* item_key[2] = {nullptr, nullptr};   // bucket | MSM_ITEM_DUMMY
+  XYZZ<F>* item_val[2] = {nullptr, nullptr};
+  size_t item_cap[2] = {0, 0};
   XYZZ<F>* buckets = nullptr;   // [NB]
-  XYZZ<F>* red_acc = nullptr;   // reduction scratch (all levels), [NB]
-  XYZZ<F>* red_run = nullptr;   // [NB]
-  XYZZ<F>* red_tmp = nullptr;   // [NB]
+  XYZZ<F>* red_a = nullptr;     // weighted-reduction block outputs [NB / RB] (+ next levels)
+  XYZZ<F>* red_s = nullptr;
   uint32_t* nnz = nullptr;      // number of non-zero digits of the last run (device)
 };
 
