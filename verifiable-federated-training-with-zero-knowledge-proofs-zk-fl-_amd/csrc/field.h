@@ -313,32 +313,65 @@ struct Fq2Ops {
   static ZK_DEV T from_mont(const T& a) { return f2_from_mont(a); }
 };
 
-// Out-of-line Fq multiplication.  The inlined FIPS multiply is ~2.5 KB of code; every curve
-// operation inlines several (a G2 XYZZ addition: 42), so kernels built from inlined products
-// run to 60-600 KB of code, beyond the instruction cache a CU pair shares.  Latency-tolerant
-// kernels use this one out-of-line copy instead (FqOpsCall / Fq2OpsCall).
-static __device__ __noinline__ Fq fq_mul_call(Fq a, Fq b) { return fp_mul<FqP>(a, b); }
+// ---------------------------------------------------------------------------
+// Fq2 split across a lane pair (G2 MSM kernels).  Lanes 2k and 2k+1 hold components c0 and c1
+// of the same Fq2 value; each lane keeps 8 registers per Fq2 instead of 16, so the G2 point
+// kernels fit the register budget of 3-4 waves/SIMD instead of one wave owning the whole SIMD.
+// A product costs each lane two Fq multiplications (the pair does 4 where one lane's Karatsuba
+// does 3), exchanging the partner's component through DPP (quad_perm [1,0,3,2]).
+// Callers keep control flow pair-uniform (both lanes of a pair always active together).
+// ---------------------------------------------------------------------------
+ZK_DEV uint32_t pair_half() { return __lane_id() & 1u; }
 
-static __device__ __noinline__ Fq2 f2_mul_call(Fq2 a, Fq2 b) {
-  Fq t0 = fq_mul_call(a.c0, b.c0);
-  Fq t1 = fq_mul_call(a.c1, b.c1);
-  Fq t2 = fq_mul_call(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-static __device__ __noinline__ Fq2 f2_sqr_call(Fq2 a) {
-  Fq t0 = fq_mul_call(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  Fq t1 = fq_mul_call(a.c0, a.c1);
-  return {t0, fp_dbl(t1)};
+ZK_DEV uint32_t pair_swap_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
-// The same field interfaces with the multiplications out of line (same storage types).
-struct FqOpsCall : FqOps {
-  static ZK_DEV T mul(const T& a, const T& b) { return fq_mul_call(a, b); }
-  static ZK_DEV T sqr(const T& a) { return fq_mul_call(a, a); }
-};
-struct Fq2OpsCall : Fq2Ops {
-  static ZK_DEV T mul(const T& a, const T& b) { return f2_mul_call(a, b); }
-  static ZK_DEV T sqr(const T& a) { return f2_sqr_call(a); }
+ZK_DEV Fq pair_swap(const Fq& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = pair_swap_u32(a.v[i]);
+  return r;
+}
+
+ZK_DEV Fq fq_sel(bool c, const Fq& a, const Fq& b) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+struct Fq2PairOps {
+  using T = Fq;  // this lane's component
+  static ZK_DEV T zero() { return fp_zero<FqP>(); }
+  static ZK_DEV T one() { return pair_half() ? fp_zero<FqP>() : fp_one<FqP>(); }
+  static ZK_DEV bool is_zero(const T& a) {
+    const uint32_t z = fp_is_zero(a) ? 1u : 0u;
+    return (z & pair_swap_u32(z)) != 0;
+  }
+  static ZK_DEV bool eq(const T& a, const T& b) {
+    const uint32_t e = fp_eq(a, b) ? 1u : 0u;
+    return (e & pair_swap_u32(e)) != 0;
+  }
+  static ZK_DEV T add(const T& a, const T& b) { return fp_add(a, b); }
+  static ZK_DEV T sub(const T& a, const T& b) { return fp_sub(a, b); }
+  static ZK_DEV T neg(const T& a) { return fp_neg(a); }
+  static ZK_DEV T dbl(const T& a) { return fp_dbl(a); }
+  // c0 = a0 b0 - a1 b1 (lane 0), c1 = a1 b0 + a0 b1 (lane 1)
+  static ZK_DEV T mul(const T& a, const T& b) {
+    const bool h = pair_half();
+    const Fq pa = pair_swap(a), pb = pair_swap(b);
+    const Fq p1 = fp_mul(a, fq_sel(h, pb, b));
+    const Fq p2 = fp_mul(pa, fq_sel(h, b, pb));
+    return h ? fp_add(p1, p2) : fp_sub(p1, p2);
+  }
+  // c0 = (a0 + a1)(a0 - a1) (lane 0), c1 = 2 a0 a1 (lane 1)
+  static ZK_DEV T sqr(const T& a) {
+    const bool h = pair_half();
+    const Fq pa = pair_swap(a);
+    const Fq t = fp_mul(fq_sel(h, a, fp_add(a, pa)), fq_sel(h, pa, fp_sub(a, pa)));
+    return h ? fp_dbl(t) : t;
+  }
 };
 
 }  // namespace zkfl

@@ -32,15 +32,65 @@
 
 namespace zkfl {
 
-// Accumulation kernel configuration per curve (measured on MI355X): G1 fits its
-// working set in 128 VGPRs -> 4 waves/SIMD with the pipelined gather; G2's Fq2 working set needs
-// > 256 registers, so it runs at 1 wave/SIMD (2 waves cost 130-280 spills in every schedule tried).
+// Kernel occupancy per curve (measured on MI355X).  G1: the accumulation fits 128
+// VGPRs (4 waves/SIMD); its stitching/reduction kernels run at 2-3.  G2 runs on lane pairs
+// (Fq2PairOps): 184-234 VGPRs, 2 waves/SIMD without spills; one lane per G2 point needed > 256
+// registers, so a single wave owned the whole SIMD for the kernel's duration (measured
+// 186 -> 208 proofs/s moving G2 to lane pairs, although the pair does 4 Fq products per Fq2
+// product where one lane does 3).
 #ifndef MSM_G1_WAVES
 #define MSM_G1_WAVES 4
 #endif
 #ifndef MSM_G2_WAVES
-#define MSM_G2_WAVES 1
+#define MSM_G2_WAVES 2
 #endif
+#ifndef MSM_G2_TAIL_WAVES
+#define MSM_G2_TAIL_WAVES 2
+#endif
+
+// Compute type -> storage: how the point kernels read and write the stored points.  G1 and plain
+// Fq2 hold a point per lane; Fq2PairOps holds it across a lane pair (component h of every
+// coordinate in lane 2k+h), reading and writing Affine/XYZZ<Fq2Ops> memory.
+template <class F>
+struct MsmIO {
+  using S = F;
+  static constexpr int LANES = 1;
+  static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return p[i]; }
+  static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return p[i]; }
+  static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<F>& v) { p[i] = v; }
+};
+template <>
+struct MsmIO<Fq2PairOps> {
+  using S = Fq2Ops;
+  static constexpr int LANES = 2;
+  static ZK_DEV Affine<Fq2PairOps> ld_aff(const Affine<S>* p, size_t i) {
+    const Fq* q = reinterpret_cast<const Fq*>(p + i);
+    const uint32_t h = pair_half();
+    return {q[h], q[2 + h]};
+  }
+  static ZK_DEV XYZZ<Fq2PairOps> ld(const XYZZ<S>* p, size_t i) {
+    const Fq* q = reinterpret_cast<const Fq*>(p + i);
+    const uint32_t h = pair_half();
+    return {q[h], q[2 + h], q[4 + h], q[6 + h]};
+  }
+  static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<Fq2PairOps>& v) {
+    Fq* q = reinterpret_cast<Fq*>(p + i);
+    const uint32_t h = pair_half();
+    q[h] = v.X;
+    q[2 + h] = v.Y;
+    q[4 + h] = v.ZZ;
+    q[6 + h] = v.ZZZ;
+  }
+};
+// Compute type the MSM kernels use for a stored curve.
+template <class F>
+struct MsmCompute {
+  using type = F;
+};
+template <>
+struct MsmCompute<Fq2Ops> {
+  using type = Fq2PairOps;
+};
 
 // ---------------------------------------------------------------------------
 // Key-load-time window expansion: out[i*W + j] = 2^(16 j) * in[i]  (affine)
@@ -131,19 +181,20 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
 // run is the whole bucket: written to buckets[k].  An open run becomes an item of the next
 // stitching level: the left-open run in slot 0, a (only) right-open run in slot 1.  Unused
 // slots are dummies carrying the range's first / last bucket, so item keys stay sorted.
-template <class F>
+template <class F, class S = typename MsmIO<F>::S>
 ZK_DEV void msm_emit_run(uint32_t k, const XYZZ<F>& acc, bool real, bool open_left, bool open_right,
-                         XYZZ<F>* __restrict__ buckets, uint32_t* __restrict__ okey, XYZZ<F>* __restrict__ oval,
+                         XYZZ<S>* __restrict__ buckets, uint32_t* __restrict__ okey, XYZZ<S>* __restrict__ oval,
                          bool& slot0, bool& slot1) {
+  using IO = MsmIO<F>;
   if (!open_left && !open_right) {
-    if (real) buckets[k] = acc;
+    if (real) IO::st(buckets, k, acc);
   } else if (open_left) {
     okey[0] = real ? k : (k | MSM_ITEM_DUMMY);
-    if (real) oval[0] = acc;
+    if (real) IO::st(oval, 0, acc);
     slot0 = true;
   } else {
     okey[1] = real ? k : (k | MSM_ITEM_DUMMY);
-    if (real) oval[1] = acc;
+    if (real) IO::st(oval, 1, acc);
     slot1 = true;
   }
 }
@@ -152,12 +203,13 @@ ZK_DEV void msm_emit_run(uint32_t k, const XYZZ<F>& acc, bool real, bool open_le
 // of bucket boundaries, so every lane does the same work).  Software-pipelined: the key/index of
 // entry p+1 and its base are in flight while entry p is added.  MINW: minimum waves per SIMD
 // the register allocator must allow (chosen per curve).
-template <class F, int MINW>
+template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
-    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<F>* __restrict__ bases,
-    const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<F>* __restrict__ item_val,
-    XYZZ<F>* __restrict__ buckets) {
-  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<S>* __restrict__ bases,
+    const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
+    XYZZ<S>* __restrict__ buckets) {
+  using IO = MsmIO<F>;
+  const size_t c = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
   const uint32_t nnz = *nnz_ptr;
   const size_t p0 = c * MSM_L;
   if (p0 >= nnz) return;
@@ -165,7 +217,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   const uint32_t kprev = p0 > 0 ? keys[p0 - 1] : 0xFFFFFFFFu;
   const uint32_t knext = p1 < nnz ? keys[p1] : 0xFFFFFFFFu;
   uint32_t* okey = item_key + 2 * c;
-  XYZZ<F>* oval = item_val + 2 * c;
+  XYZZ<S>* oval = item_val + 2 * c;
   bool slot0 = false, slot1 = false;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t cur = keys[p0], run_start = (uint32_t)p0;
@@ -174,11 +226,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     k1 = keys[p0 + 1];
     v1 = vals[p0 + 1];
   }
-  Affine<F> a = bases[v0 & 0x7FFFFFFFu];
+  Affine<F> a = IO::ld_aff(bases, v0 & 0x7FFFFFFFu);
   for (uint32_t p = (uint32_t)p0; p < p1; p++) {
     Affine<F> an;
     uint32_t k2 = 0, v2 = 0;
-    if (p + 1 < p1) an = bases[v1 & 0x7FFFFFFFu];
+    if (p + 1 < p1) an = IO::ld_aff(bases, v1 & 0x7FFFFFFFu);
     if (p + 2 < p1) {
       k2 = keys[p + 2];
       v2 = vals[p + 2];
@@ -210,13 +262,12 @@ ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
 
 // Stitching level: the same run logic over the previous level's items (SG per lane), so a
 // bucket spread over many chunks is summed by a tree of depth log_{SG/2}, not by one lane.
-template <class F>
-__global__ void __launch_bounds__(64) k_msm_stitch(const uint32_t* __restrict__ in_key,
-                                                   const XYZZ<F>* __restrict__ in_val,
-                                                   const uint32_t* __restrict__ nnz_ptr, int level,
-                                                   uint32_t* __restrict__ out_key, XYZZ<F>* __restrict__ out_val,
-                                                   XYZZ<F>* __restrict__ buckets) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
+    const uint32_t* __restrict__ in_key, const XYZZ<S>* __restrict__ in_val, const uint32_t* __restrict__ nnz_ptr,
+    int level, uint32_t* __restrict__ out_key, XYZZ<S>* __restrict__ out_val, XYZZ<S>* __restrict__ buckets) {
+  using IO = MsmIO<F>;
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
   const uint32_t N = msm_items_at(*nnz_ptr, level);
   const uint32_t q0 = g * MSM_SG;
   if (q0 >= N) return;
@@ -225,7 +276,7 @@ __global__ void __launch_bounds__(64) k_msm_stitch(const uint32_t* __restrict__ 
   const uint32_t kprev = q0 > 0 ? (in_key[q0 - 1] & KM) : 0xFFFFFFFFu;
   const uint32_t knext = q1 < N ? (in_key[q1] & KM) : 0xFFFFFFFFu;
   uint32_t* okey = out_key + 2 * g;
-  XYZZ<F>* oval = out_val + 2 * g;
+  XYZZ<S>* oval = out_val + 2 * g;
   bool slot0 = false, slot1 = false, real = false;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t kq = in_key[q0];
@@ -233,7 +284,7 @@ __global__ void __launch_bounds__(64) k_msm_stitch(const uint32_t* __restrict__ 
   for (uint32_t q = q0; q < q1; q++) {
     const uint32_t kn = q + 1 < q1 ? in_key[q + 1] : 0xFFFFFFFFu;
     if (!(kq & MSM_ITEM_DUMMY)) {
-      acc = xyzz_add<F>(acc, in_val[q]);
+      acc = xyzz_add<F>(acc, IO::ld(in_val, q));
       real = true;
     }
     const bool last = q + 1 == q1;
@@ -256,48 +307,47 @@ __global__ void __launch_bounds__(64) k_msm_stitch(const uint32_t* __restrict__ 
 // A block of items combines as  a' = sum_t a_t + g * sum_t t s_t,  s' = sum_t s_t,
 // with sum_t t s_t = sum_{t>=1} R_t for the suffix sums R_t = sum_{u>=t} s_u: a 6-step LDS
 // suffix scan and a 6-step tree (depth ~13 additions per level instead of a lane-serial
-// running sum).  Level 0 reads the buckets as both a and s (g = 1).  The two trees run one after
-// the other: side by side they spill the G2 kernel.
-template <class F>
-__global__ void __launch_bounds__(MSM_RB) k_msm_wsum(const XYZZ<F>* __restrict__ in_a, const XYZZ<F>* __restrict__ in_s,
-                                                    int N, int log2g, XYZZ<F>* __restrict__ out_a,
-                                                    XYZZ<F>* __restrict__ out_s) {
-  __shared__ XYZZ<F> shx[MSM_RB];
-  __shared__ XYZZ<F> shy[MSM_RB];
-  const int t = threadIdx.x;
+// running sum).  Level 0 reads the buckets as both a and s (g = 1).
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
+k_msm_wsum(const XYZZ<S>* __restrict__ in_a, const XYZZ<S>* __restrict__ in_s, int N, int log2g,
+           XYZZ<S>* __restrict__ out_a, XYZZ<S>* __restrict__ out_s) {
+  using IO = MsmIO<F>;
+  __shared__ XYZZ<S> sh[MSM_RB];
+  const int t = threadIdx.x / IO::LANES;
   const int i = blockIdx.x * MSM_RB + t;
-  XYZZ<F> R = i < N ? in_s[i] : xyzz_inf<F>();
+  XYZZ<F> R = i < N ? IO::ld(in_s, i) : xyzz_inf<F>();
 #pragma unroll 1
   for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
-    shx[t] = R;
+    IO::st(sh, t, R);
     __syncthreads();
-    if (t + d < MSM_RB) R = xyzz_add<F>(R, shx[t + d]);
+    if (t + d < MSM_RB) R = xyzz_add<F>(R, IO::ld(sh, t + d));
     __syncthreads();
   }
   XYZZ<F> x = t >= 1 ? R : xyzz_inf<F>();
 #pragma unroll 1
   for (int d = MSM_RB / 2; d >= 1; d >>= 1) {  // tree sum of R_{t>=1}
-    shx[t] = x;
+    IO::st(sh, t, x);
     __syncthreads();
-    if (t < d) x = xyzz_add<F>(x, shx[t + d]);
+    if (t < d) x = xyzz_add<F>(x, IO::ld(sh, t + d));
     __syncthreads();
   }
   // tree sum of a (level 0 reads the buckets as both a and s: that sum is R_0)
   XYZZ<F> y = R;
   if (in_a != in_s) {
-    y = i < N ? in_a[i] : xyzz_inf<F>();
+    y = i < N ? IO::ld(in_a, i) : xyzz_inf<F>();
 #pragma unroll 1
     for (int d = MSM_RB / 2; d >= 1; d >>= 1) {
-      shy[t] = y;
+      IO::st(sh, t, y);
       __syncthreads();
-      if (t < d) y = xyzz_add<F>(y, shy[t + d]);
+      if (t < d) y = xyzz_add<F>(y, IO::ld(sh, t + d));
       __syncthreads();
     }
   }
   if (t == 0) {
     for (int k = 0; k < log2g; k++) x = xyzz_dbl<F>(x);
-    out_a[blockIdx.x] = xyzz_add<F>(y, x);
-    out_s[blockIdx.x] = R;
+    IO::st(out_a, blockIdx.x, xyzz_add<F>(y, x));
+    IO::st(out_s, blockIdx.x, R);
   }
 }
 
@@ -396,17 +446,19 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
                                      st));
   ZK_CHECK(hipMemsetAsync(pl.buckets, 0, MSM_NB * sizeof(XYZZ<F>), st));  // ZZ = 0: infinity
   const int pidx = prof ? prof->begin(tag, st) : -1;
+  using FC = typename MsmCompute<F>::type;
+  constexpr int LN = MsmIO<FC>::LANES;
   constexpr bool G1 = sizeof(typename F::T) == 32;
-  hipLaunchKernelGGL((k_msm_accumulate<F, G1 ? MSM_G1_WAVES : MSM_G2_WAVES>), dim3(zk_grid(chunks, 64)), dim3(64),
-                     0, st, pl.keys_out, pl.vals_out, b.bases_w, pl.nnz, pl.item_key[0], pl.item_val[0],
-                     pl.buckets);
+  constexpr int AW = G1 ? MSM_G1_WAVES : MSM_G2_WAVES, TW = G1 ? 2 : MSM_G2_TAIL_WAVES;
+  hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, pl.keys_out,
+                     pl.vals_out, b.bases_w, pl.nnz, pl.item_key[0], pl.item_val[0], pl.buckets);
   if (prof) prof->end(pidx, st, 0.0, pl.nnz);
   // stitching levels (item counts here are the host-side upper bounds; kernels use nnz)
   size_t N = 2 * chunks;
   int cur = 0;
   for (int level = 1;; level++) {
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
-    hipLaunchKernelGGL(k_msm_stitch<F>, dim3(zk_grid(lanes, 64)), dim3(64), 0, st, pl.item_key[cur],
+    hipLaunchKernelGGL((k_msm_stitch<FC, TW>), dim3(zk_grid(lanes * LN, 64)), dim3(64), 0, st, pl.item_key[cur],
                        pl.item_val[cur], pl.nnz, level, pl.item_key[cur ^ 1], pl.item_val[cur ^ 1], pl.buckets);
     if (N <= (size_t)MSM_SG) break;
     N = 2 * lanes;
@@ -421,7 +473,7 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
     const int blocks = (n + MSM_RB - 1) / MSM_RB;
     XYZZ<F>* oa = blocks == 1 ? d_out : pl.red_a + off;
     XYZZ<F>* os = pl.red_s + off;
-    hipLaunchKernelGGL(k_msm_wsum<F>, dim3(blocks), dim3(MSM_RB), 0, st, ia, is, n, log2g, oa, os);
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(blocks), dim3(MSM_RB * LN), 0, st, ia, is, n, log2g, oa, os);
     if (blocks == 1) break;
     ia = oa;
     is = os;
