@@ -296,7 +296,7 @@ def test_node_snarkjs_cli_prove(gpu_ctx, tmp_path):
     import subprocess
     from zkfl import native, zkey
     node = shutil.which("node")
-    shim = os.path.join(os.path.dirname(native.LIB_PATH), "node", "snarkjs_shim.js")
+    shim = os.path.join(native._PKG_DIR, "node", "snarkjs_shim.js")
     if not node or not os.path.exists(os.path.join(os.path.dirname(shim), "zkfl.node")):
         pytest.skip("node / addon not available")
     b, zk = _setup(gpu_ctx, "poseidon_hash2")

@@ -1,4 +1,2 @@
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/parity.log 2>&1 || { tail -30 gpurun_out/parity.log; exit 1; }
-tail -2 gpurun_out/parity.log
-bash tools/sweep_env.sh ZKFL_G2AW "3 2"
+bash tools/sweep_env.sh ZKFL_LIB "$PWD/build_ab/libzkfl_L16.so $PWD/build_ab/libzkfl_L32.so"

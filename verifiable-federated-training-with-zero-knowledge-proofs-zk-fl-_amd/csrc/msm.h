@@ -22,8 +22,8 @@
 //    what is left: a bucket spread over many chunks is summed by a shallow tree instead of one
 //    lane walking its chunks (that serial walk, not the arithmetic, used to set the MSM's latency).
 //  * Accumulation uses XYZZ + affine mixed additions (10 Fq mul for G1).
-//  * Bucket reduction sum_b (b+1) S_b: 64-item blocks per wave (LDS suffix scan + tree, depth ~13
-//    additions), three levels for 2^15 buckets, the last writing the MSM result.
+//  * Bucket reduction sum_b (b+1) S_b: 8 buckets folded serially per lane, then 64-lane blocks
+//    (LDS suffix scan + trees); two levels for 2^15 buckets, the second writing the MSM result.
 #pragma once
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -302,21 +302,37 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   if (!slot1) okey[1] = (in_key[q1 - 1] & KM) | MSM_ITEM_DUMMY;
 }
 
-// Weighted bucket reduction sum_b (b+1) S_b, one 64-item block per wave.  An item i stands for
-// a group of g = 2^log2g consecutive buckets: s_i = its bucket sum, a_i = sum (b - first + 1) S_b.
-// A block of items combines as  a' = sum_t a_t + g * sum_t t s_t,  s' = sum_t s_t,
-// with sum_t t s_t = sum_{t>=1} R_t for the suffix sums R_t = sum_{u>=t} s_u: a 6-step LDS
-// suffix scan and a 6-step tree (depth ~13 additions per level instead of a lane-serial
-// running sum).  Level 0 reads the buckets as both a and s (g = 1).
+// Weighted bucket reduction sum_b (b+1) S_b.  An item i stands for a group of g = 2^log2g
+// consecutive buckets: s_i = its bucket sum, a_i = sum (b - first + 1) S_b; items combine as
+//   a' = sum_k a_k + g * sum_k k s_k,   s' = sum_k s_k,   sum_k k s_k = sum_{k>=1} R_k
+// with the suffix sums R_k = sum_{j>=k} s_j.  Each logical lane first folds Q consecutive items
+// serially (running sum, 2 additions per bucket), then a 64-lane block combines the lanes with an
+// LDS suffix scan and two trees (depth ~18).  Level 0 reads the buckets as both a and s (g = 1,
+// Q = 8: 64 blocks); level 1 (Q = 1) combines the 64 block results into the MSM result.  Serial
+// folding first keeps the waves few: the reduction's cost is its waves' register-time.
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
-k_msm_wsum(const XYZZ<S>* __restrict__ in_a, const XYZZ<S>* __restrict__ in_s, int N, int log2g,
+k_msm_wsum(const XYZZ<S>* __restrict__ in_a, const XYZZ<S>* __restrict__ in_s, int N, int log2g, int Q,
            XYZZ<S>* __restrict__ out_a, XYZZ<S>* __restrict__ out_s) {
   using IO = MsmIO<F>;
   __shared__ XYZZ<S> sh[MSM_RB];
   const int t = threadIdx.x / IO::LANES;
-  const int i = blockIdx.x * MSM_RB + t;
-  XYZZ<F> R = i < N ? IO::ld(in_s, i) : xyzz_inf<F>();
+  const bool same = in_a == in_s;
+  // serial fold of items [(blk*RB + t)*Q, +Q)
+  const int i0 = (blockIdx.x * MSM_RB + t) * Q;
+  XYZZ<F> R = xyzz_inf<F>(), W = xyzz_inf<F>(), y = xyzz_inf<F>();
+#pragma unroll 1
+  for (int k = Q - 1; k >= 0; k--) {
+    if (i0 + k < N) {
+      R = xyzz_add<F>(R, IO::ld(in_s, i0 + k));
+      if (!same) y = xyzz_add<F>(y, IO::ld(in_a, i0 + k));
+    }
+    if (k >= 1) W = xyzz_add<F>(W, R);
+  }
+  if (same) y = R;
+#pragma unroll 1
+  for (int k = 0; k < log2g; k++) W = xyzz_dbl<F>(W);
+  y = xyzz_add<F>(y, W);  // this lane's item: group of Q*g buckets
 #pragma unroll 1
   for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
     IO::st(sh, t, R);
@@ -326,26 +342,22 @@ k_msm_wsum(const XYZZ<S>* __restrict__ in_a, const XYZZ<S>* __restrict__ in_s, i
   }
   XYZZ<F> x = t >= 1 ? R : xyzz_inf<F>();
 #pragma unroll 1
-  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {  // tree sum of R_{t>=1}
+  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {  // tree sums of R_{t>=1} and of a
     IO::st(sh, t, x);
     __syncthreads();
     if (t < d) x = xyzz_add<F>(x, IO::ld(sh, t + d));
     __syncthreads();
   }
-  // tree sum of a (level 0 reads the buckets as both a and s: that sum is R_0)
-  XYZZ<F> y = R;
-  if (in_a != in_s) {
-    y = i < N ? IO::ld(in_a, i) : xyzz_inf<F>();
 #pragma unroll 1
-    for (int d = MSM_RB / 2; d >= 1; d >>= 1) {
-      IO::st(sh, t, y);
-      __syncthreads();
-      if (t < d) y = xyzz_add<F>(y, IO::ld(sh, t + d));
-      __syncthreads();
-    }
+  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {
+    IO::st(sh, t, y);
+    __syncthreads();
+    if (t < d) y = xyzz_add<F>(y, IO::ld(sh, t + d));
+    __syncthreads();
   }
   if (t == 0) {
-    for (int k = 0; k < log2g; k++) x = xyzz_dbl<F>(x);
+    const int lq = 31 - __builtin_clz((unsigned)Q);
+    for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
     IO::st(out_a, blockIdx.x, xyzz_add<F>(y, x));
     IO::st(out_s, blockIdx.x, R);
   }
@@ -464,23 +476,12 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
     N = 2 * lanes;
     cur ^= 1;
   }
-  // weighted reduction: 2^15 -> 512 -> 8 -> 1
-  const XYZZ<F>* ia = pl.buckets;
-  const XYZZ<F>* is = pl.buckets;
-  int n = MSM_NB, log2g = 0;
-  size_t off = 0;
-  while (true) {
-    const int blocks = (n + MSM_RB - 1) / MSM_RB;
-    XYZZ<F>* oa = blocks == 1 ? d_out : pl.red_a + off;
-    XYZZ<F>* os = pl.red_s + off;
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(blocks), dim3(MSM_RB * LN), 0, st, ia, is, n, log2g, oa, os);
-    if (blocks == 1) break;
-    ia = oa;
-    is = os;
-    off += blocks;
-    n = blocks;
-    log2g += 6;  // log2(MSM_RB)
-  }
+  // weighted reduction: 2^15 buckets -> 64 blocks (8 buckets per lane) -> 1
+  static_assert(MSM_NB == MSM_RB * MSM_RB * 8, "two reduction levels cover the buckets");
+  hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(MSM_RB), dim3(MSM_RB * LN), 0, st, pl.buckets, pl.buckets, MSM_NB, 0,
+                     8, pl.red_a, pl.red_s);
+  hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(1), dim3(MSM_RB * LN), 0, st, pl.red_a, pl.red_s, MSM_RB, 9, 1,
+                     d_out, pl.red_s + MSM_RB);
   return hipGetLastError();
 }
 
