@@ -21,10 +21,12 @@ import os
 import sys
 import time
 
-# Each in-flight proof slot drives 3 HIP streams; HIP maps a process's streams onto
+# Each in-flight proof slot drives one HIP stream; HIP maps a process's streams onto
 # GPU_MAX_HW_QUEUES hardware queues (HIP default 4, which the GPU boxes also export), and streams
-# sharing a queue serialize.  Set it before anything initializes HIP (measured: 4 queues 87-95
-# proofs/s -> 24 queues, 8 slots 164 proofs/s).  ZKFL_HW_QUEUES overrides the value used here.
+# sharing a queue serialize.  Set it before anything initializes HIP.  Measured on MI355X
+# (tools/concurrency_probe.hip): kernels on distinct streams run concurrently up to ~20 at 24
+# queues, while 32 queues oversubscribe the hardware queue slots; 16 slots x 1 stream at 24 queues
+# is the best measured configuration.  ZKFL_HW_QUEUES overrides the value used here.
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "24")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -159,7 +161,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--slots", type=int, default=8, help="proofs in flight per GPU (HIP stream sets)")
+    ap.add_argument("--slots", type=int, default=16, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     args = ap.parse_args()
 

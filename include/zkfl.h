@@ -79,9 +79,10 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
 int zkfl_key_free(zkfl_key* key);
 int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
 /* Number of proofs kept in flight by zkfl_groth16_prove_batch (1..32, default 3).  Each slot
- * owns three HIP streams and its own scratch; proofs in different slots overlap on the GPU.
- * HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): set it to >= 3 x slots
- * in the environment before the first HIP call, or the slots serialize. */
+ * owns one HIP stream (ZKFL_SLOT_STREAMS=2|3: two or three) and its own scratch; proofs in
+ * different slots overlap on the GPU.  HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
+ * (default 4): set it to >= streams x slots (at most 24 helps on MI355X) in the environment
+ * before the first HIP call, or the slots serialize. */
 int zkfl_key_set_slots(zkfl_key* key, int slots);
 
 /* Full prove from a .wtns byte image (host).  pub_out may be NULL; otherwise receives

@@ -1,7 +1,11 @@
+#!/bin/bash
+# Proof slots x streams per slot x HW queues sweep of the default bench (GPU box).
+#   bash tools/sweep_slots.sh STREAMS,QUEUES,SLOTS ...
 set -o pipefail
 mkdir -p gpurun_out/sweep
-for cfg in "3 24 8" "1 24 24" "1 32 32" "1 16 16" "3 32 10"; do
-  set -- $cfg
-  ZKFL_SLOT_STREAMS=$1 ZKFL_HW_QUEUES=$2 timeout -k 10 120 python -u bench.py --steps 96 --warmup 16 --slots $3 --no-cpu-baseline > gpurun_out/sweep/s$1_q$2_n$3.log 2>&1 || exit 1
-  echo "streams=$1 queues=$2 slots=$3 $(tail -1 gpurun_out/sweep/s$1_q$2_n$3.log | python -c 'import json,sys;d=json.loads(sys.stdin.read());print(d["value"], d["stage_ms_isolated_per_proof"])')"
+for cfg in "$@"; do
+  IFS=, read -r S Q N <<< "$cfg"
+  LOG=gpurun_out/sweep/s${S}_q${Q}_n${N}.log
+  ZKFL_SLOT_STREAMS=$S ZKFL_HW_QUEUES=$Q timeout -k 10 150 python -u bench.py --steps 96 --warmup 16 --slots $N --no-cpu-baseline > $LOG 2>&1 || exit 1
+  echo "streams=$S queues=$Q slots=$N $(tail -1 $LOG | python -c 'import json,sys;d=json.loads(sys.stdin.read());print(d["value"])')"
 done

@@ -438,11 +438,12 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
-  static const int streams = getenv("ZKFL_SLOT_STREAMS") ? atoi(getenv("ZKFL_SLOT_STREAMS")) : 3;
-  if (streams > 1) {
-    ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
-    ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
-  }
+  // One stream per slot by default: a slot's proof is a serial chain and throughput comes from
+  // many slots (measured on MI355X, 24 HW queues: 16 slots x 1 stream 238-241 proofs/s vs
+  // 8 slots x 3 streams 216-217).  ZKFL_SLOT_STREAMS=2|3 splits off the G2 MSM / assembly.
+  static const int streams = getenv("ZKFL_SLOT_STREAMS") ? atoi(getenv("ZKFL_SLOT_STREAMS")) : 1;
+  if (streams > 1) ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
+  if (streams > 2) ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
@@ -513,7 +514,8 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
   return ZKFL_OK;
 }
 
-// Enqueue one proof on a slot (asynchronous).  Stream graph:
+// Enqueue one proof on a slot (asynchronous).  Stream graph (with 1 stream per slot, the
+// default, all three are the slot's one stream):
 //   main : rs, scalar vectors, [ev_ready] MSM A, MSM B1 [ev_ab] ABC, coset NTT x3, join,
 //          MSM H, MSM C, wait(ev_t, ev_b2), finalize, proof D2H [ev_done]
 //   g2   : wait(ev_ready) MSM B2, pi_b affine [ev_b2]
