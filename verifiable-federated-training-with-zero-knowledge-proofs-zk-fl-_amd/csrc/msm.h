@@ -25,6 +25,7 @@
 //  * Bucket reduction sum_b (b+1) S_b: 8 buckets folded serially per lane, then 64-lane blocks
 //    (LDS suffix scan + trees); two levels for 2^15 buckets, the second writing the MSM result.
 #pragma once
+#include <algorithm>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -262,13 +263,30 @@ ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
 
 // Stitching level: the same run logic over the previous level's items (SG per lane), so a
 // bucket spread over many chunks is summed by a tree of depth log_{SG/2}, not by one lane.
+// Kernel argument of the batched tail launches: up to MSM_TAIL_MAX MSMs, one per blockIdx.y.
+template <class S>
+struct MsmTailArgs {
+  uint32_t* key[MSM_TAIL_MAX][2];
+  XYZZ<S>* val[MSM_TAIL_MAX][2];
+  XYZZ<S>* buckets[MSM_TAIL_MAX];
+  XYZZ<S>* red_a[MSM_TAIL_MAX];
+  XYZZ<S>* red_s[MSM_TAIL_MAX];
+  const uint32_t* nnz[MSM_TAIL_MAX];
+  XYZZ<S>* out[MSM_TAIL_MAX];
+};
+
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
-    const uint32_t* __restrict__ in_key, const XYZZ<S>* __restrict__ in_val, const uint32_t* __restrict__ nnz_ptr,
-    int level, uint32_t* __restrict__ out_key, XYZZ<S>* __restrict__ out_val, XYZZ<S>* __restrict__ buckets) {
+    const MsmTailArgs<S> ta, int level, int src) {
   using IO = MsmIO<F>;
+  const int y = blockIdx.y;
+  const uint32_t* __restrict__ in_key = ta.key[y][src];
+  const XYZZ<S>* __restrict__ in_val = ta.val[y][src];
+  uint32_t* __restrict__ out_key = ta.key[y][src ^ 1];
+  XYZZ<S>* __restrict__ out_val = ta.val[y][src ^ 1];
+  XYZZ<S>* __restrict__ buckets = ta.buckets[y];
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
-  const uint32_t N = msm_items_at(*nnz_ptr, level);
+  const uint32_t N = msm_items_at(*ta.nnz[y], level);
   const uint32_t q0 = g * MSM_SG;
   if (q0 >= N) return;
   const uint32_t q1 = q0 + MSM_SG < N ? q0 + MSM_SG : N;
@@ -310,10 +328,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
 // LDS suffix scan and two trees (depth ~18).  Level 0 reads the buckets as both a and s (g = 1,
 // Q = 8: 64 blocks); level 1 (Q = 1) combines the 64 block results into the MSM result.  Serial
 // folding first keeps the waves few: the reduction's cost is its waves' register-time.
+static_assert(MSM_NB == MSM_RB * MSM_RB * 8, "two reduction levels cover the buckets");
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
-k_msm_wsum(const XYZZ<S>* __restrict__ in_a, const XYZZ<S>* __restrict__ in_s, int N, int log2g, int Q,
-           XYZZ<S>* __restrict__ out_a, XYZZ<S>* __restrict__ out_s) {
+k_msm_wsum(const MsmTailArgs<S> ta, int level) {
+  const int yb = blockIdx.y;
+  const bool l0 = level == 0;
+  const XYZZ<S>* __restrict__ in_a = l0 ? ta.buckets[yb] : ta.red_a[yb];
+  const XYZZ<S>* __restrict__ in_s = l0 ? ta.buckets[yb] : ta.red_s[yb];
+  const int N = l0 ? MSM_NB : MSM_RB, log2g = l0 ? 0 : 9, Q = l0 ? 8 : 1;
+  XYZZ<S>* __restrict__ out_a = l0 ? ta.red_a[yb] : ta.out[yb];
+  XYZZ<S>* __restrict__ out_s = l0 ? ta.red_s[yb] : ta.red_s[yb] + MSM_RB;
   using IO = MsmIO<F>;
   __shared__ XYZZ<S> sh[MSM_RB];
   const int t = threadIdx.x / IO::LANES;
@@ -406,83 +431,116 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, s.sort_tmp_bytes, s.keys_in, s.keys_out, s.vals_in, s.vals_out, m, 0,
                                      16, st));
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
-  s.max_chunks = (m + MSM_L - 1) / MSM_L;
-  s.item_cap[0] = 2 * s.max_chunks;
-  s.item_cap[1] = 2 * ((s.item_cap[0] + MSM_SG - 1) / MSM_SG);
-  for (int k = 0; k < 2; k++) {
-    ZK_CHECK(hipMalloc(&s.item_key[k], s.item_cap[k] * sizeof(uint32_t)));
-    ZK_CHECK(hipMalloc(&s.item_val[k], s.item_cap[k] * sizeof(XYZZ<F>)));
-  }
-  ZK_CHECK(hipMalloc(&s.buckets, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.red_a, (MSM_NB / MSM_RB + 2 * MSM_RB) * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.red_s, (MSM_NB / MSM_RB + 2 * MSM_RB) * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&s.nnz, sizeof(uint32_t)));
   return hipSuccess;
 }
 
 template <class F>
 void msm_scratch_free(MsmScratch<F>& s) {
-  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp, s.item_key[0], s.item_key[1],
-                  s.item_val[0], s.item_val[1], s.buckets, s.red_a, s.red_s, s.nnz};
+  void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s = MsmScratch<F>();
 }
 
-// One MSM: n = b.n standard-form scalars (8 x u32, device) -> *d_out (device XYZZ).
 template <class F>
-__global__ void k_msm_set_inf(XYZZ<F>* out) {
-  *out = xyzz_inf<F>();
+hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
+  const size_t m = cap * MSM_W;
+  t.max_chunks = (m + MSM_L - 1) / MSM_L;
+  t.item_cap[0] = 2 * t.max_chunks;
+  t.item_cap[1] = 2 * ((t.item_cap[0] + MSM_SG - 1) / MSM_SG);
+  for (int k = 0; k < 2; k++) {
+    ZK_CHECK(hipMalloc(&t.item_key[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(uint32_t)));
+    ZK_CHECK(hipMalloc(&t.item_val[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(XYZZ<F>)));
+  }
+  ZK_CHECK(hipMalloc(&t.buckets, MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.red_a, 2 * MSM_RB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.red_s, 2 * MSM_RB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.nnz, sizeof(uint32_t)));
+  return hipSuccess;
 }
 
-// Stream order: digits (+ nnz) -> radix sort by bucket -> accumulate (level 0: fixed chunks,
-// closed runs straight into buckets, open runs as items) -> stitching levels until one lane
-// holds every remaining item -> weighted reduction blocks (3 levels for 2^15 buckets) -> d_out.
 template <class F>
-hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_scalars, const uint32_t* d_extra,
-                   XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
+void msm_tail_free(MsmTail<F>& t) {
+  void* ptrs[] = {t.item_key[0], t.item_key[1], t.item_val[0], t.item_val[1], t.buckets, t.red_a, t.red_s, t.nnz};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  t = MsmTail<F>();
+}
+
+// digits (+ nnz) -> radix sort by bucket -> accumulate (level 0: fixed chunks, closed runs
+// straight into the buckets, open runs as items).  An MSM with no bases leaves nnz = 0 and
+// empty buckets: its tail yields infinity.
+template <class F>
+hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
+                          const uint32_t* d_extra, hipStream_t st, Profiler* prof = nullptr,
+                          const char* tag = nullptr) {
   if (b.n > pl.cap) return hipErrorInvalidValue;
-  if (b.n == 0) {
-    hipLaunchKernelGGL(k_msm_set_inf<F>, dim3(1), dim3(1), 0, st, d_out);
-    return hipGetLastError();
-  }
+  ZK_CHECK(hipMemsetAsync(t.nnz, 0, sizeof(uint32_t), st));
+  ZK_CHECK(hipMemsetAsync(t.buckets, 0, MSM_NB * sizeof(XYZZ<F>), st));  // ZZ = 0: infinity
+  if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
   const size_t chunks = (m + MSM_L - 1) / MSM_L;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
-  if (need > pl.sort_tmp_bytes || chunks > pl.max_chunks) return hipErrorInvalidValue;
-  ZK_CHECK(hipMemsetAsync(pl.nnz, 0, sizeof(uint32_t), st));
+  if (need > pl.sort_tmp_bytes || chunks > t.max_chunks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
-                     b.extra_start, b.n, pl.keys_in, pl.vals_in, pl.nnz);
+                     b.extra_start, b.n, pl.keys_in, pl.vals_in, t.nnz);
   ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
                                      st));
-  ZK_CHECK(hipMemsetAsync(pl.buckets, 0, MSM_NB * sizeof(XYZZ<F>), st));  // ZZ = 0: infinity
   const int pidx = prof ? prof->begin(tag, st) : -1;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
-  constexpr bool G1 = sizeof(typename F::T) == 32;
-  constexpr int AW = G1 ? MSM_G1_WAVES : MSM_G2_WAVES, TW = G1 ? 2 : MSM_G2_TAIL_WAVES;
+  constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
   hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, pl.keys_out,
-                     pl.vals_out, b.bases_w, pl.nnz, pl.item_key[0], pl.item_val[0], pl.buckets);
-  if (prof) prof->end(pidx, st, 0.0, pl.nnz);
-  // stitching levels (item counts here are the host-side upper bounds; kernels use nnz)
-  size_t N = 2 * chunks;
+                     pl.vals_out, b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
+  if (prof) prof->end(pidx, st, 0.0, t.nnz);
+  return hipGetLastError();
+}
+
+// Tails of n accumulated MSMs in one batch: stitching levels until one lane holds every
+// remaining item (item counts here are host-side upper bounds; the kernels use each nnz), then
+// the two weighted-reduction levels, the last writing outs[i].
+template <class F>
+hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {
+  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  using FC = typename MsmCompute<F>::type;
+  constexpr int LN = MsmIO<FC>::LANES;
+  constexpr int TW = sizeof(typename F::T) == 32 ? 2 : MSM_G2_TAIL_WAVES;
+  MsmTailArgs<F> ta = {};
+  size_t N = 0;
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 2; k++) {
+      ta.key[i][k] = t[i]->item_key[k];
+      ta.val[i][k] = t[i]->item_val[k];
+    }
+    ta.buckets[i] = t[i]->buckets;
+    ta.red_a[i] = t[i]->red_a;
+    ta.red_s[i] = t[i]->red_s;
+    ta.nnz[i] = t[i]->nnz;
+    ta.out[i] = outs[i];
+    N = std::max(N, t[i]->item_cap[0]);
+  }
+  N = std::max<size_t>(N, 2);
   int cur = 0;
   for (int level = 1;; level++) {
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
-    hipLaunchKernelGGL((k_msm_stitch<FC, TW>), dim3(zk_grid(lanes * LN, 64)), dim3(64), 0, st, pl.item_key[cur],
-                       pl.item_val[cur], pl.nnz, level, pl.item_key[cur ^ 1], pl.item_val[cur ^ 1], pl.buckets);
+    hipLaunchKernelGGL((k_msm_stitch<FC, TW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
     if (N <= (size_t)MSM_SG) break;
     N = 2 * lanes;
     cur ^= 1;
   }
-  // weighted reduction: 2^15 buckets -> 64 blocks (8 buckets per lane) -> 1
-  static_assert(MSM_NB == MSM_RB * MSM_RB * 8, "two reduction levels cover the buckets");
-  hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(MSM_RB), dim3(MSM_RB * LN), 0, st, pl.buckets, pl.buckets, MSM_NB, 0,
-                     8, pl.red_a, pl.red_s);
-  hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(1), dim3(MSM_RB * LN), 0, st, pl.red_a, pl.red_s, MSM_RB, 9, 1,
-                     d_out, pl.red_s + MSM_RB);
+  for (int level = 0; level < 2; level++)
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(level == 0 ? MSM_RB : 1, n), dim3(MSM_RB * LN), 0, st, ta, level);
   return hipGetLastError();
+}
+
+template <class F>
+hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
+                   const uint32_t* d_extra, XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr,
+                   const char* tag = nullptr) {
+  ZK_CHECK(msm_accumulate(b, pl, t, d_scalars, d_extra, st, prof, tag));
+  MsmTail<F>* tp = &t;
+  return msm_tails(&tp, &d_out, 1, st);
 }
 
 // Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
@@ -497,9 +555,18 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, const uint32_t* d_sc
     return msm_scratch_alloc(s, cap, st);                                                                \
   }                                                                                                      \
   void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
-  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* sc, const uint32_t* ex, \
-                           XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag) {              \
-    return msm_run(b, s, sc, ex, out, st, prof, tag);                                                    \
+  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap) { return msm_tail_alloc(t, cap); }          \
+  void msm_tail_free_##SUF(MsmTail<F>& t) { msm_tail_free(t); }                                          \
+  hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc, \
+                                  const uint32_t* ex, hipStream_t st, Profiler* prof, const char* tag) { \
+    return msm_accumulate(b, s, t, sc, ex, st, prof, tag);                                               \
+  }                                                                                                      \
+  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {         \
+    return msm_tails(t, outs, n, st);                                                                    \
+  }                                                                                                      \
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc,     \
+                           const uint32_t* ex, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag) { \
+    return msm_run(b, s, t, sc, ex, out, st, prof, tag);                                                 \
   }
 
 }  // namespace zkfl

@@ -30,7 +30,8 @@ struct MsmBases {
   uint32_t extra_start = 0xFFFFFFFFu;
 };
 
-// Mutable, per in-flight proof (one stream at a time): sort/bucket/reduction scratch.
+// Mutable, per in-flight proof (one stream at a time): digit/sort scratch shared by the MSMs a
+// slot runs one after another.
 template <class F>
 struct MsmScratch {
   size_t cap = 0;                // max number of bases served
@@ -40,25 +41,41 @@ struct MsmScratch {
   uint32_t* vals_out = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+};
+
+// Per MSM of a proof: what the accumulation leaves for the tail (stitching + reduction), so the
+// tails of several MSMs can run as one batch (one launch per level for all of them).
+template <class F>
+struct MsmTail {
   size_t max_chunks = 0;        // ceil(cap * W / L)
   // stitching items (ping-pong): 2 per chunk / per stitching lane, sorted by bucket
   uint32_t* item_key[2] = {nullptr, nullptr};   // bucket | MSM_ITEM_DUMMY
   XYZZ<F>* item_val[2] = {nullptr, nullptr};
   size_t item_cap[2] = {0, 0};
   XYZZ<F>* buckets = nullptr;   // [NB]
-  XYZZ<F>* red_a = nullptr;     // weighted-reduction block outputs [NB / RB] (+ next levels)
+  XYZZ<F>* red_a = nullptr;     // weighted-reduction block outputs
   XYZZ<F>* red_s = nullptr;
   uint32_t* nnz = nullptr;      // number of non-zero digits of the last run (device)
 };
 
-#define ZKFL_MSM_DECLARE(SUF, F)                                                                  \
-  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                     \
-  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,    \
-                                 uint32_t extra_start, hipStream_t st);                            \
-  void msm_bases_free_##SUF(MsmBases<F>& b);                                                      \
-  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st);               \
-  void msm_scratch_free_##SUF(MsmScratch<F>& s);                                                  \
-  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, const uint32_t* scalars,            \
+constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs of a proof)
+
+#define ZKFL_MSM_DECLARE(SUF, F)                                                                    \
+  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                       \
+  hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,      \
+                                 uint32_t extra_start, hipStream_t st);                              \
+  void msm_bases_free_##SUF(MsmBases<F>& b);                                                        \
+  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st);                 \
+  void msm_scratch_free_##SUF(MsmScratch<F>& s);                                                    \
+  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap);                                       \
+  void msm_tail_free_##SUF(MsmTail<F>& t);                                                          \
+  /* digits -> sort -> accumulation into t (the MSM is finished by msm_tails) */                    \
+  hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t,            \
+                                  const uint32_t* scalars, const uint32_t* extra, hipStream_t st,    \
+                                  Profiler* prof, const char* tag);                                  \
+  /* stitching + bucket reduction of n <= MSM_TAIL_MAX accumulated MSMs -> outs[i] (device) */      \
+  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st);    \
+  hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \
                            const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
 
 ZKFL_MSM_DECLARE(g1, FqOps)

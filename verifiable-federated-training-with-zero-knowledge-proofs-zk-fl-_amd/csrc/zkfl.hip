@@ -369,8 +369,10 @@ struct zkfl_ctx {
 struct ProofSlot {
   hipStream_t st_main = nullptr, st_g2 = nullptr, st_asm = nullptr;
   hipEvent_t ev_ready = nullptr, ev_ab = nullptr, ev_b2 = nullptr, ev_t = nullptr, ev_done = nullptr;
-  MsmScratch<FqOps> g1s;
+  MsmScratch<FqOps> g1s;   // digit/sort scratch shared by the four G1 MSMs
+  MsmTail<FqOps> g1t[4];   // A, B1, C, H: accumulated, finished by one batched tail
   MsmScratch<Fq2Ops> g2s;
+  MsmTail<Fq2Ops> g2t;
   Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs
   Fr* abc = nullptr;  // [3n]
   Fr* abc_head = nullptr;  // [ceil(K / ABC_L)] ABC segmented-sum partials
@@ -419,7 +421,9 @@ void slot_release(ProofSlot* s) {
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_asm})
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s);
+  for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
+  msm_tail_free_g2(s->g2t);
   void* ptrs[] = {s->extra, s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -447,7 +451,10 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
+  const size_t caps[4] = {k->bA.n, k->bB1.n, k->bC.n, k->bH.n};
+  for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
+  ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
   (void)nV;
   ZK_CHECK(hipMalloc(&s->extra, 4 * 32));
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
@@ -516,8 +523,9 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 
 // Enqueue one proof on a slot (asynchronous).  Stream graph (with 1 stream per slot, the
 // default, all three are the slot's one stream):
-//   main : rs, scalar vectors, [ev_ready] MSM A, MSM B1 [ev_ab] ABC, coset NTT x3, join,
-//          MSM H, MSM C, wait(ev_t, ev_b2), finalize, proof D2H [ev_done]
+//   main : rs, scalar vectors, [ev_ready] accumulate A, B1, C, ABC, coset NTT x3, join,
+//          accumulate H, the four G1 tails as one batch [ev_ab], wait(ev_t, ev_b2), finalize,
+//          proof D2H [ev_done]
 //   g2   : wait(ev_ready) MSM B2, pi_b affine [ev_b2]
 //   asm  : wait(ev_ab) T = s*A + r*B1, pi_a affine [ev_t]
 // plain = 1 (parity hook): alpha/beta/delta/r/s terms zeroed, nothing assembled.
@@ -526,29 +534,23 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   hipStream_t st = s->st_main;
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
   hipStream_t st_asm = (prof->serialize || !s->st_asm) ? st : s->st_asm;
-  const size_t nV = k->nVars, n = k->n;
+  const size_t n = k->n;
   memcpy(s->pinned + 256, rs_host, 64);
   int pp = prof->begin("prove", st);
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
   hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain);
-  (void)nV;
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   // G2 stream
   HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
-  HIP_TRY(msm_run_g2(k->bB2, s->g2s, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
+  HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
   if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, st_g2, s->resB2, s->d_proof);
   HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
-  // main: A, B1 first so the assembly chain can start early
-  HIP_TRY(msm_run_g1(k->bA, s->g1s, W, E, s->res + 0, st, prof, "msm_accumulate_g1"), "msm A");
-  HIP_TRY(msm_run_g1(k->bB1, s->g1s, W, E, s->res + 1, st, prof, "msm_accumulate_g1"), "msm B1");
-  HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
-  if (!plain) {
-    HIP_TRY(hipStreamWaitEvent(st_asm, s->ev_ab, 0), "wait");
-    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
-    HIP_TRY(hipEventRecord(s->ev_t, st_asm), "event");
-  }
+  // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
+  HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+  HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
   int pi = prof->begin("abc", st);
   if (k->K) {
     const uint32_t K = (uint32_t)k->K;
@@ -562,8 +564,19 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
   prof->end(pi, st, 3.0 * (double)n);
   hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
-  HIP_TRY(msm_run_g1(k->bH, s->g1s, (const uint32_t*)s->h, nullptr, s->res + 3, st, prof, "msm_accumulate_g1"), "msm H");
-  HIP_TRY(msm_run_g1(k->bC, s->g1s, W, E, s->res + 2, st, prof, "msm_accumulate_g1"), "msm C");
+  HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
+          "msm H");
+  {
+    MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
+    G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
+    HIP_TRY(msm_tails_g1(tails, outs, 4, st), "msm tails");
+  }
+  HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
+  if (!plain) {
+    HIP_TRY(hipStreamWaitEvent(st_asm, s->ev_ab, 0), "wait");
+    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
+    HIP_TRY(hipEventRecord(s->ev_t, st_asm), "event");
+  }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (!plain) {
     HIP_TRY(hipStreamWaitEvent(st, s->ev_t, 0), "wait");
@@ -583,13 +596,13 @@ int wait_slot(ProofSlot* s, uint8_t* proof_out) {
   return ZKFL_OK;
 }
 
-hipError_t msm_run_any(const MsmBases<FqOps>& b, MsmScratch<FqOps>& s, const uint32_t* sc, G1P* o, hipStream_t st,
-                       Profiler* p) {
-  return msm_run_g1(b, s, sc, nullptr, o, st, p, "msm_accumulate_g1");
+hipError_t msm_run_any(const MsmBases<FqOps>& b, MsmScratch<FqOps>& s, MsmTail<FqOps>& t, const uint32_t* sc,
+                       G1P* o, hipStream_t st, Profiler* p) {
+  return msm_run_g1(b, s, t, sc, nullptr, o, st, p, "msm_accumulate_g1");
 }
-hipError_t msm_run_any(const MsmBases<Fq2Ops>& b, MsmScratch<Fq2Ops>& s, const uint32_t* sc, G2P* o, hipStream_t st,
-                       Profiler* p) {
-  return msm_run_g2(b, s, sc, nullptr, o, st, p, "msm_accumulate_g2");
+hipError_t msm_run_any(const MsmBases<Fq2Ops>& b, MsmScratch<Fq2Ops>& s, MsmTail<Fq2Ops>& t, const uint32_t* sc,
+                       G2P* o, hipStream_t st, Profiler* p) {
+  return msm_run_g2(b, s, t, sc, nullptr, o, st, p, "msm_accumulate_g2");
 }
 hipError_t bases_alloc_any(MsmBases<FqOps>& b, size_t n) { return msm_bases_alloc_g1(b, n); }
 hipError_t bases_alloc_any(MsmBases<Fq2Ops>& b, size_t n) { return msm_bases_alloc_g2(b, n); }
@@ -611,6 +624,10 @@ hipError_t scratch_alloc_any(MsmScratch<FqOps>& s, size_t n, hipStream_t st) { r
 hipError_t scratch_alloc_any(MsmScratch<Fq2Ops>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g2(s, n, st); }
 void scratch_free_any(MsmScratch<FqOps>& s) { msm_scratch_free_g1(s); }
 void scratch_free_any(MsmScratch<Fq2Ops>& s) { msm_scratch_free_g2(s); }
+hipError_t tail_alloc_any(MsmTail<FqOps>& t, size_t n) { return msm_tail_alloc_g1(t, n); }
+hipError_t tail_alloc_any(MsmTail<Fq2Ops>& t, size_t n) { return msm_tail_alloc_g2(t, n); }
+void tail_free_any(MsmTail<FqOps>& t) { msm_tail_free_g1(t); }
+void tail_free_any(MsmTail<Fq2Ops>& t) { msm_tail_free_g2(t); }
 
 template <class F>
 int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out) {
@@ -618,6 +635,7 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   hipStream_t st = ctx->st;
   MsmBases<F> mb;
   MsmScratch<F> ms;
+  MsmTail<F> mt;
   Affine<F>* d_b = nullptr;
   uint32_t* d_s = nullptr;
   XYZZ<F>* d_r = nullptr;
@@ -625,6 +643,7 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   int rc = ZKFL_OK;
   hipError_t e = bases_alloc_any(mb, n);
   if (e == hipSuccess) e = scratch_alloc_any(ms, n, st);
+  if (e == hipSuccess) e = tail_alloc_any(mt, n);
   if (e == hipSuccess) e = hipMalloc(&d_b, n * sizeof(Affine<F>));
   if (e == hipSuccess) e = hipMalloc(&d_s, n * 32);
   if (e == hipSuccess) e = hipMalloc(&d_r, sizeof(XYZZ<F>));
@@ -632,7 +651,7 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   if (e == hipSuccess) e = hipMemcpyAsync(d_b, bases, n * sizeof(Affine<F>), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = bases_set_any(mb, d_b, st);
-  if (e == hipSuccess) e = msm_run_any(mb, ms, d_s, d_r, st, &ctx->prof);
+  if (e == hipSuccess) e = msm_run_any(mb, ms, mt, d_s, d_r, st, &ctx->prof);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_point_out<F>, dim3(1), dim3(1), 0, st, d_r, 1, d_o);
     e = hipGetLastError();
@@ -642,6 +661,7 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   if (e != hipSuccess) rc = hip_fail(e, "msm primitive");
   bases_free_any(mb);
   scratch_free_any(ms);
+  tail_free_any(mt);
   for (void* p : {(void*)d_b, (void*)d_s, (void*)d_r, (void*)d_o})
     if (p) (void)hipFree(p);
   return rc;
