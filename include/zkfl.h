@@ -107,6 +107,11 @@ int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_
 int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, uint8_t* h_out,
                            uint8_t* msm_out);
 
+/* GLV split used by the proof assembly (host code, no device): k (32 B std, < r) ->
+ * out = k1 || k2, each 20 B: |k_i| (16 B little-endian) then a u32 sign (1 = negative), with
+ * k = k1 + k2 * lambda (mod r), |k_i| < 2^128 (csrc/glv.h; tests/test_abi.py checks it). */
+int zkfl_debug_glv_split(const uint8_t k[32], uint8_t out[40]);
+
 /* Stand-alone primitives (parity tests).  bases: mont affine; scalars: std, n x 32 B. */
 int zkfl_msm_g1(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[64]);
 int zkfl_msm_g2(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t out[128]);

@@ -35,6 +35,27 @@ def test_version_and_error_paths_without_device():
     assert L.zkfl_ctx_set_profiling(None, 1) == -1
 
 
+def test_glv_split_host():
+    """The assembly's GLV split (csrc/glv.h, host code): k = k1 + k2*lambda (mod r), |k_i| < 2^128,
+    on edge scalars and seeded random ones; r >= r is rejected."""
+    import random
+    from oracle import bn254 as bn
+    lam = 0xb3c4d79d41a917585bfc41088d8daaa78b17ea66b99c90dd
+    assert (lam * lam + lam + 1) % bn.R == 0
+    L = native.lib()
+    rnd = random.Random(5)
+    ks = [0, 1, 2, lam, bn.R - 1, bn.R // 2, (1 << 253)] + [rnd.randrange(bn.R) for _ in range(500)]
+    out = (ctypes.c_uint8 * 40)()
+    for k in ks:
+        assert L.zkfl_debug_glv_split(k.to_bytes(32, "little"), out) == 0
+        b = bytes(out)
+        k1 = int.from_bytes(b[0:16], "little") * (-1 if b[16] else 1)
+        k2 = int.from_bytes(b[20:36], "little") * (-1 if b[36] else 1)
+        assert (k1 + k2 * lam - k) % bn.R == 0, k
+        assert abs(k1) < 1 << 128 and abs(k2) < 1 << 128
+    assert L.zkfl_debug_glv_split(bn.R.to_bytes(32, "little"), out) == -1
+
+
 def test_node_addon_loads():
     """N-API addon (node/zkfl.node) loads in Node and exposes the binding (no GPU calls)."""
     import shutil

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "curve.h"
+#include "glv.h"
 #include "field.h"
 #include "msm_api.h"
 #include "ntt.h"
@@ -259,40 +260,73 @@ __device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out)
   }
 }
 
-// s*A + r*B1 (Shamir's trick, one lane) -> T; also pi_a (= A) in std affine -> proof[0..15].
-// Runs on its own stream as soon as the A and B1 MSMs are done (overlaps the H/C/B2 MSMs).
-__global__ void __launch_bounds__(64) k_assemble_T(const G1P* __restrict__ res, const Fr* __restrict__ rs,
-                                                   G1P* __restrict__ T_out, uint32_t* __restrict__ proof) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const G1P A = res[0], B1 = res[1];
-  const G1P AB = xyzz_add<FqOps>(A, B1);
-  const Fr r = rs[0], s = rs[1];
-  G1P T = xyzz_inf<FqOps>();
-  for (int i = 7; i >= 0; i--) {
-    for (int b = 31; b >= 0; b--) {
-      T = xyzz_dbl<FqOps>(T);
-      const uint32_t bs = (s.v[i] >> b) & 1u, br = (r.v[i] >> b) & 1u;
-      if (bs && br) T = xyzz_add<FqOps>(T, AB);
-      else if (bs) T = xyzz_add<FqOps>(T, A);
-      else if (br) T = xyzz_add<FqOps>(T, B1);
+// Proof assembly, one block of three waves (replaces snarkjs's final
+// pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
+//   wave 0, lanes 0..3: k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)), the GLV
+//     halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over a per-lane table
+//     of 1P..8P in LDS; then lane 0: pi_c = C' + H + sum -> proof[48..63]
+//   wave 1, lane 0: pi_a affine -> proof[0..15];  wave 2, lane 0: pi_b affine -> proof[16..47]
+// The three field inversions and the four scalar multiplications run side by side; the
+// critical path is 132 doublings + 33 additions + one inversion.
+__global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                  const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
+  __shared__ G1P tab[4][8];
+  __shared__ G1P part[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 0 && lane < 4) {
+    G1P P = res[lane >> 1];
+    if (lane & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
+      Fq beta;
+#pragma unroll
+      for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
+      P.X = fp_mul(P.X, fp_to_mont(beta));
     }
+    const GlvScalar k = ks[lane];
+    if (k.neg) P = xyzz_neg<FqOps>(P);
+    tab[lane][0] = P;
+    G1P Q = xyzz_dbl<FqOps>(P);
+    tab[lane][1] = Q;
+#pragma unroll 1
+    for (int j = 2; j < 8; j++) {
+      Q = xyzz_add<FqOps>(Q, P);
+      tab[lane][j] = Q;
+    }
+    // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
+    // d_8i .. d_8i+7, word 4 holds d_32 (the final carry)
+    uint32_t dg[5] = {0, 0, 0, 0, 0};
+    uint32_t carry = 0;
+    for (int w = 0; w < 32; w++) {
+      const uint32_t v = ((k.mag[w >> 3] >> (4 * (w & 7))) & 15u) + carry;
+      carry = v > 8 ? 1u : 0u;
+      dg[w >> 3] |= (carry ? (v - 16) & 15u : v) << (4 * (w & 7));
+    }
+    dg[4] = carry;
+    G1P acc = xyzz_inf<FqOps>();
+#pragma unroll 1
+    for (int w = 32; w >= 0; w--) {
+      if (w < 32)
+        for (int j = 0; j < 4; j++) acc = xyzz_dbl<FqOps>(acc);
+      const int wi = w >> 3;
+      const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
+      const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
+      if (nib) {
+        const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
+        const G1P t = tab[lane][(d < 0 ? -d : d) - 1];
+        acc = xyzz_add<FqOps>(acc, d < 0 ? xyzz_neg<FqOps>(t) : t);
+      }
+    }
+    part[lane] = acc;
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(res[0]), proof);
+  } else if (wave == 2 && lane == 0) {
+    store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
   }
-  *T_out = T;
-  store_affine_std<FqOps>(xyzz_to_affine<FqOps>(A), proof);
-}
-
-// pi_b affine -> proof[16..47] (G2 stream)
-__global__ void __launch_bounds__(64) k_b2_affine(const G2P* __restrict__ resB2, uint32_t* __restrict__ proof) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
-}
-
-// pi_c = C' + H + T -> proof[48..63]
-__global__ void __launch_bounds__(64) k_finalize(const G1P* __restrict__ res, uint32_t* __restrict__ proof) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  G1P C = xyzz_add<FqOps>(res[2], res[3]);
-  C = xyzz_add<FqOps>(C, res[4]);
-  store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    G1P T = xyzz_add<FqOps>(xyzz_add<FqOps>(part[0], part[1]), xyzz_add<FqOps>(part[2], part[3]));
+    G1P C = xyzz_add<FqOps>(xyzz_add<FqOps>(res[2], res[3]), T);
+    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
+  }
 }
 
 // MSM result(s) -> std affine bytes (parity hooks)
@@ -367,8 +401,8 @@ struct zkfl_ctx {
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
 struct ProofSlot {
-  hipStream_t st_main = nullptr, st_g2 = nullptr, st_asm = nullptr;
-  hipEvent_t ev_ready = nullptr, ev_ab = nullptr, ev_b2 = nullptr, ev_t = nullptr, ev_done = nullptr;
+  hipStream_t st_main = nullptr, st_g2 = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_b2 = nullptr, ev_done = nullptr;
   MsmScratch<FqOps> g1s;   // digit/sort scratch shared by the four G1 MSMs
   MsmTail<FqOps> g1t[4];   // A, B1, C, H: accumulated, finished by one batched tail
   MsmScratch<Fq2Ops> g2s;
@@ -380,9 +414,9 @@ struct ProofSlot {
   Fr* h = nullptr;    // [n]
   G1P* res = nullptr;     // [5]: A', B1', C', H, T
   G2P* resB2 = nullptr;   // [1]
-  Fr* d_rs = nullptr;     // [2]
+  Fr* d_rs = nullptr;     // r, s (64 B) | GLV halves s1, s2, r1, r2 (4 x 32 B)
   uint32_t* d_proof = nullptr;  // [64]
-  uint8_t* pinned = nullptr;    // proof (256) | rs (64)
+  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128)
   bool busy = false;
   size_t out_index = 0;
 };
@@ -418,7 +452,7 @@ namespace {
 
 void slot_release(ProofSlot* s) {
   if (!s) return;
-  for (hipStream_t st : {s->st_main, s->st_g2, s->st_asm})
+  for (hipStream_t st : {s->st_main, s->st_g2})
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s);
   for (auto& t : s->g1t) msm_tail_free_g1(t);
@@ -428,9 +462,9 @@ void slot_release(ProofSlot* s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
-  for (hipEvent_t e : {s->ev_ready, s->ev_ab, s->ev_b2, s->ev_t, s->ev_done})
+  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t st : {s->st_main, s->st_g2, s->st_asm})
+  for (hipStream_t st : {s->st_main, s->st_g2})
     if (st) (void)hipStreamDestroy(st);
   delete s;
 }
@@ -444,11 +478,10 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
   // One stream per slot by default: a slot's proof is a serial chain and throughput comes from
   // many slots (measured on MI355X, 24 HW queues: 16 slots x 1 stream 238-241 proofs/s vs
-  // 8 slots x 3 streams 216-217).  ZKFL_SLOT_STREAMS=2|3 splits off the G2 MSM / assembly.
+  // 8 slots x 3 streams 216-217).  ZKFL_SLOT_STREAMS=2 runs the G2 MSM on a second stream.
   static const int streams = getenv("ZKFL_SLOT_STREAMS") ? atoi(getenv("ZKFL_SLOT_STREAMS")) : 1;
   if (streams > 1) ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
-  if (streams > 2) ZK_CHECK(hipStreamCreateWithFlags(&s->st_asm, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&s->ev_ready, &s->ev_ab, &s->ev_b2, &s->ev_t, &s->ev_done})
+  for (hipEvent_t* e : {&s->ev_ready, &s->ev_b2, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
   const size_t caps[4] = {k->bA.n, k->bB1.n, k->bC.n, k->bH.n};
@@ -464,7 +497,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ZK_CHECK(hipMalloc(&s->h, n * 32));
   ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
-  ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32));
+  ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32 + 4 * sizeof(GlvScalar)));
   ZK_CHECK(hipMalloc(&s->d_proof, 256));
   ZK_CHECK(hipHostMalloc(&s->pinned, 512));
   return hipStreamSynchronize(st);
@@ -522,22 +555,24 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 }
 
 // Enqueue one proof on a slot (asynchronous).  Stream graph (with 1 stream per slot, the
-// default, all three are the slot's one stream):
-//   main : rs, scalar vectors, [ev_ready] accumulate A, B1, C, ABC, coset NTT x3, join,
-//          accumulate H, the four G1 tails as one batch [ev_ab], wait(ev_t, ev_b2), finalize,
-//          proof D2H [ev_done]
-//   g2   : wait(ev_ready) MSM B2, pi_b affine [ev_b2]
-//   asm  : wait(ev_ab) T = s*A + r*B1, pi_a affine [ev_t]
+// default, both are the slot's one stream):
+//   main : r, s + GLV halves, scalar vectors, [ev_ready] accumulate A, B1, C, ABC, coset NTT x3,
+//          join, accumulate H, the four G1 tails as one batch, wait(ev_b2), assembly (T, pi_a,
+//          pi_b, pi_c), proof D2H [ev_done]
+//   g2   : wait(ev_ready) MSM B2 [ev_b2]
 // plain = 1 (parity hook): alpha/beta/delta/r/s terms zeroed, nothing assembled.
 int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
-  hipStream_t st_asm = (prof->serialize || !s->st_asm) ? st : s->st_asm;
   const size_t n = k->n;
   memcpy(s->pinned + 256, rs_host, 64);
+  GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
+  glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
+  glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
   int pp = prof->begin("prove", st);
-  HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64, hipMemcpyHostToDevice, st), "upload r,s");
+  HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
+          "upload r,s");
   hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain);
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
@@ -545,7 +580,6 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   // G2 stream
   HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
   HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
-  if (!plain) hipLaunchKernelGGL(k_b2_affine, dim3(1), dim3(1), 0, st_g2, s->resB2, s->d_proof);
   HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
@@ -571,16 +605,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
     HIP_TRY(msm_tails_g1(tails, outs, 4, st), "msm tails");
   }
-  HIP_TRY(hipEventRecord(s->ev_ab, st), "event");
-  if (!plain) {
-    HIP_TRY(hipStreamWaitEvent(st_asm, s->ev_ab, 0), "wait");
-    hipLaunchKernelGGL(k_assemble_T, dim3(1), dim3(1), 0, st_asm, s->res, s->d_rs, s->res + 4, s->d_proof);
-    HIP_TRY(hipEventRecord(s->ev_t, st_asm), "event");
-  }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (!plain) {
-    HIP_TRY(hipStreamWaitEvent(st, s->ev_t, 0), "wait");
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, st, s->res, s->d_proof);
+    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
+                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
     HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   }
   prof->end(pp, st, 1.0);
@@ -710,6 +738,20 @@ int run_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out, b
 extern "C" {
 
 int zkfl_version(void) { return 1; }
+
+int zkfl_debug_glv_split(const uint8_t k[32], uint8_t out[40]) {
+  if (!k || !out) return fail(ZKFL_E_ARG, "null argument");
+  uint32_t kk[8];
+  memcpy(kk, k, 32);
+  if (!lt_r(kk)) return fail(ZKFL_E_ARG, "k must be < r");
+  GlvScalar a, b;
+  glv_split(kk, a, b);
+  memcpy(out, a.mag, 16);
+  memcpy(out + 16, &a.neg, 4);
+  memcpy(out + 20, b.mag, 16);
+  memcpy(out + 36, &b.neg, 4);
+  return ZKFL_OK;
+}
 
 const char* zkfl_last_error(void) { return g_err.c_str(); }
 

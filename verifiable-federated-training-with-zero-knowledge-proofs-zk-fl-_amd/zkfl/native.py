@@ -45,6 +45,7 @@ SIGNATURES = {
     "zkfl_groth16_prove_resident": (C.c_int, [_P, _P, _P, C.c_char_p, _U8P]),
     "zkfl_groth16_prove_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_debug_prove_parts": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, _U8P, _U8P]),
+    "zkfl_debug_glv_split": (C.c_int, [C.c_char_p, _U8P]),
     "zkfl_msm_g1": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_msm_g2": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_ntt_coset": (C.c_int, [_P, _U8P, C.c_uint32]),
