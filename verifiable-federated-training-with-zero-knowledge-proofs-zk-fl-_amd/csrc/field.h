@@ -194,6 +194,48 @@ ZK_DEV Fp<PR> fp_mul(const Fp<PR>& a, const Fp<PR>& b) {
   return r;
 }
 
+// (a*b + c*d) * 2^-256 mod p with ONE Montgomery reduction (a, b, c, d < p): both products
+// accumulate into the same FIPS columns (<= 24 terms per column, < 2^69: the 96-bit column
+// accumulator holds it); a*b + c*d < 2p^2 < 2^256 p, so the result is < 2p before the final
+// subtraction.  200 multiply-adds instead of 2 x 136 (the lane-pair Fq2 product).
+template <class PR>
+ZK_DEV Fp<PR> fp_mul_sum2(const Fp<PR>& a, const Fp<PR>& b, const Fp<PR>& c, const Fp<PR>& d) {
+  uint32_t m[8], u[9];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      ZK_MAC_VV(lo, hi, a.v[j], b.v[i - j]);
+      ZK_MAC_VV(lo, hi, c.v[j], d.v[i - j]);
+      ZK_MAC_VS(lo, hi, m[j], PR::P[i - j]);
+    }
+    ZK_MAC_VV(lo, hi, a.v[i], b.v[0]);
+    ZK_MAC_VV(lo, hi, c.v[i], d.v[0]);
+    m[i] = (uint32_t)lo * PR::INV;
+    ZK_MAC_VS(lo, hi, m[i], PR::P[0]);
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) {
+      ZK_MAC_VV(lo, hi, a.v[j], b.v[i - j]);
+      ZK_MAC_VV(lo, hi, c.v[j], d.v[i - j]);
+      ZK_MAC_VS(lo, hi, m[j], PR::P[i - j]);
+    }
+    u[i - 8] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  u[8] = (uint32_t)lo;
+  Fp<PR> r;
+  fp_reduce_once<PR>(r.v, u);
+  return r;
+}
+
 template <class PR>
 ZK_DEV Fp<PR> fp_sqr(const Fp<PR>& a) {
   return fp_mul<PR>(a, a);
@@ -314,11 +356,33 @@ struct Fq2Ops {
 };
 
 // ---------------------------------------------------------------------------
+// Compact-code Fq multiplication for the G1 accumulation loop: the whole product as one asm
+// statement (tools/gen_fp_mul_asm.py: VOP2 carries through VCC, no hazard nops or register-pair
+// shuffles between statements) is ~1.7 KB instead of ~2.9 KB.  The mixed addition inlines ten
+// products, and the loop outgrew the instruction cache: rocprofv3 SQ_WAIT_INST_ANY was 43% of
+// the G1 accumulation's wave cycles.  Same values as fp_mul (tests/test_gpu_parity.py).
+// ---------------------------------------------------------------------------
+#include "fp_mul_asm.h"
+
+ZK_DEV Fq fq_mul_compact(const Fq& a, const Fq& b) {
+  uint32_t u[8];
+  ZK_FP_MUL_ASM(u, a.v, b.v, FqP::P, FqP::INV);
+  Fq r;
+  fp_reduce_once<FqP>(r.v, u);
+  return r;
+}
+
+struct FqOpsCompact : FqOps {
+  static ZK_DEV T mul(const T& a, const T& b) { return fq_mul_compact(a, b); }
+  static ZK_DEV T sqr(const T& a) { return fq_mul_compact(a, a); }
+};
+
+// ---------------------------------------------------------------------------
 // Fq2 split across a lane pair (G2 MSM kernels).  Lanes 2k and 2k+1 hold components c0 and c1
 // of the same Fq2 value; each lane keeps 8 registers per Fq2 instead of 16, so the G2 point
 // kernels fit the register budget of 3-4 waves/SIMD instead of one wave owning the whole SIMD.
-// A product costs each lane two Fq multiplications (the pair does 4 where one lane's Karatsuba
-// does 3), exchanging the partner's component through DPP (quad_perm [1,0,3,2]).
+// A product costs each lane one sum of two Fq products with a single reduction (fp_mul_sum2),
+// exchanging the partner's component through DPP (quad_perm [1,0,3,2]).
 // Callers keep control flow pair-uniform (both lanes of a pair always active together).
 // ---------------------------------------------------------------------------
 ZK_DEV uint32_t pair_half() { return __lane_id() & 1u; }
@@ -357,13 +421,12 @@ struct Fq2PairOps {
   static ZK_DEV T sub(const T& a, const T& b) { return fp_sub(a, b); }
   static ZK_DEV T neg(const T& a) { return fp_neg(a); }
   static ZK_DEV T dbl(const T& a) { return fp_dbl(a); }
-  // c0 = a0 b0 - a1 b1 (lane 0), c1 = a1 b0 + a0 b1 (lane 1)
+  // c0 = a0 b0 + (-a1) b1 (lane 0), c1 = a1 b0 + a0 b1 (lane 1): one sum of two products with
+  // a single Montgomery reduction per lane
   static ZK_DEV T mul(const T& a, const T& b) {
     const bool h = pair_half();
     const Fq pa = pair_swap(a), pb = pair_swap(b);
-    const Fq p1 = fp_mul(a, fq_sel(h, pb, b));
-    const Fq p2 = fp_mul(pa, fq_sel(h, b, pb));
-    return h ? fp_add(p1, p2) : fp_sub(p1, p2);
+    return fp_mul_sum2(a, fq_sel(h, pb, b), fq_sel(h, pa, fp_neg(pa)), fq_sel(h, b, pb));
   }
   // c0 = (a0 + a1)(a0 - a1) (lane 0), c1 = 2 a0 a1 (lane 1)
   static ZK_DEV T sqr(const T& a) {

@@ -83,11 +83,26 @@ struct MsmIO<Fq2PairOps> {
     q[6 + h] = v.ZZZ;
   }
 };
+template <>
+struct MsmIO<FqOpsCompact> {
+  using S = FqOps;
+  static constexpr int LANES = 1;
+  using F = FqOpsCompact;
+  static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return reinterpret_cast<const Affine<F>*>(p)[i]; }
+  static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return reinterpret_cast<const XYZZ<F>*>(p)[i]; }
+  static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<F>& v) { reinterpret_cast<XYZZ<F>*>(p)[i] = v; }
+};
 // Compute type the MSM kernels use for a stored curve.
 template <class F>
 struct MsmCompute {
   using type = F;
 };
+#ifndef MSM_G1_NO_COMPACT
+template <>
+struct MsmCompute<FqOps> {
+  using type = FqOpsCompact;
+};
+#endif
 template <>
 struct MsmCompute<Fq2Ops> {
   using type = Fq2PairOps;
