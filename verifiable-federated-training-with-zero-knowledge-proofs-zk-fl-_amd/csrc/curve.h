@@ -83,7 +83,7 @@ ZK_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
   T M = F::add(F::dbl(X2), X2);
   XYZZ<F> r;
   r.X = F::sub(F::sqr(M), F::dbl(S));
-  r.Y = F::sub(F::mul(M, F::sub(S, r.X)), F::mul(W, p.Y));
+  r.Y = F::mul_sub(M, F::sub(S, r.X), W, p.Y);
   r.ZZ = F::mul(V, p.ZZ);
   r.ZZZ = F::mul(W, p.ZZZ);
   return r;
@@ -101,7 +101,7 @@ ZK_DEV XYZZ<F> xyzz_dbl_affine(const Affine<F>& a) {
   T M = F::add(F::dbl(X2), X2);
   XYZZ<F> r;
   r.X = F::sub(F::sqr(M), F::dbl(S));
-  r.Y = F::sub(F::mul(M, F::sub(S, r.X)), F::mul(W, a.y));
+  r.Y = F::mul_sub(M, F::sub(S, r.X), W, a.y);
   r.ZZ = V;
   r.ZZZ = W;
   return r;
@@ -126,7 +126,7 @@ ZK_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
   T Q = F::mul(p.X, PP);
   XYZZ<F> r;
   r.X = F::sub(F::sub(F::sqr(R), PPP), F::dbl(Q));
-  r.Y = F::sub(F::mul(R, F::sub(Q, r.X)), F::mul(p.Y, PPP));
+  r.Y = F::mul_sub(R, F::sub(Q, r.X), p.Y, PPP);
   r.ZZ = F::mul(p.ZZ, PP);
   r.ZZZ = F::mul(p.ZZZ, PPP);
   return r;
@@ -153,7 +153,7 @@ ZK_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   T Q = F::mul(U1, PP);
   XYZZ<F> r;
   r.X = F::sub(F::sub(F::sqr(R), PPP), F::dbl(Q));
-  r.Y = F::sub(F::mul(R, F::sub(Q, r.X)), F::mul(S1, PPP));
+  r.Y = F::mul_sub(R, F::sub(Q, r.X), S1, PPP);
   r.ZZ = F::mul(F::mul(p.ZZ, q.ZZ), PP);
   r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
   return r;

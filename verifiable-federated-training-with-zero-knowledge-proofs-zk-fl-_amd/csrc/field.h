@@ -335,6 +335,10 @@ struct FqOps {
   static ZK_DEV T dbl(const T& a) { return fp_dbl(a); }
   static ZK_DEV T mul(const T& a, const T& b) { return fp_mul(a, b); }
   static ZK_DEV T sqr(const T& a) { return fp_sqr(a); }
+  // a*b - c*d with one reduction
+  static ZK_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
+    return fp_mul_sum2(a, b, fp_neg(c), d);
+  }
   static ZK_DEV T inv(const T& a) { return fp_inv(a); }
   static ZK_DEV T from_mont(const T& a) { return fp_from_mont(a); }
 };
@@ -351,6 +355,7 @@ struct Fq2Ops {
   static ZK_DEV T dbl(const T& a) { return f2_dbl(a); }
   static ZK_DEV T mul(const T& a, const T& b) { return f2_mul(a, b); }
   static ZK_DEV T sqr(const T& a) { return f2_sqr(a); }
+  static ZK_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) { return f2_sub(f2_mul(a, b), f2_mul(c, d)); }
   static ZK_DEV T inv(const T& a) { return f2_inv(a); }
   static ZK_DEV T from_mont(const T& a) { return f2_from_mont(a); }
 };
@@ -428,6 +433,7 @@ struct Fq2PairOps {
     const Fq pa = pair_swap(a), pb = pair_swap(b);
     return fp_mul_sum2(a, fq_sel(h, pb, b), fq_sel(h, pa, fp_neg(pa)), fq_sel(h, b, pb));
   }
+  static ZK_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) { return fp_sub(mul(a, b), mul(c, d)); }
   // c0 = (a0 + a1)(a0 - a1) (lane 0), c1 = 2 a0 a1 (lane 1)
   static ZK_DEV T sqr(const T& a) {
     const bool h = pair_half();
