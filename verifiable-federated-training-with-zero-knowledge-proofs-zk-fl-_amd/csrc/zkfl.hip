@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "curve.h"
@@ -136,14 +137,27 @@ int parse_wtns(const uint8_t* buf, size_t len, WtnsView& out) {
 // straight to abc[row]; k_abc_rows stitches rows j and n+j and forms c = a*b.
 constexpr uint32_t ABC_L = 16;
 
-__global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ rp, uint32_t nrows,
-                                                   const uint32_t* __restrict__ cols, const Fr* __restrict__ coefs,
+// Terms are either packed (col | coefficient-dictionary index << cshift in one u32: circuits
+// with few distinct coefficients, e.g. 1,971 among the 7.0 M A/B terms of the training circuit;
+// 4 B per term instead of 36 B, the dictionary stays in cache) or wide (cols[] + coefs[]).
+struct AbcTerms {
+  const uint32_t* cols;  // packed terms, or column indices (wide)
+  const Fr* coefs;       // dictionary (packed) or one coefficient per term (wide)
+  uint32_t cshift;       // 0: wide
+};
+
+template <bool PACKED>
+__global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ rp, uint32_t nrows, AbcTerms T,
                                                    const Fr* __restrict__ w, uint32_t K, Fr* __restrict__ head,
                                                    Fr* __restrict__ tail, Fr* __restrict__ abc) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t p0 = c * ABC_L;
   if (p0 >= K) return;
   const uint32_t p1 = p0 + ABC_L < K ? p0 + ABC_L : K;
+  const uint32_t* __restrict__ cols = T.cols;
+  const Fr* __restrict__ coefs = T.coefs;
+  const uint32_t cmask = PACKED ? (1u << T.cshift) - 1u : 0xFFFFFFFFu;
+  auto coef_of = [&](uint32_t t, uint32_t p) { return PACKED ? coefs[t >> T.cshift] : coefs[p]; };
   // row containing p0: largest r with rp[r] <= p0 (empty rows share their start with the next)
   uint32_t lo = 0, hi = nrows - 1;
   while (lo < hi) {
@@ -154,18 +168,19 @@ __global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ 
   uint32_t r = lo, rend = rp[r + 1];
   Fr acc = fp_zero<FrP>();
   bool first = true;
-  // software-pipelined: term p+1's witness gather (and p+2's column index) are in flight while
+  // software-pipelined: term p+1's witness gather (and p+2's term word) are in flight while
   // term p is multiplied
-  uint32_t col1 = (p0 + 1 < p1) ? cols[p0 + 1] : 0u;
-  Fr wv = w[cols[p0]], cf = coefs[p0];
+  uint32_t t1 = (p0 + 1 < p1) ? cols[p0 + 1] : 0u;
+  const uint32_t t0 = cols[p0];
+  Fr wv = w[t0 & cmask], cf = coef_of(t0, p0);
   for (uint32_t p = p0; p < p1; p++) {
     Fr wn, cn;
-    uint32_t col2 = 0;
+    uint32_t t2 = 0;
     if (p + 1 < p1) {
-      wn = w[col1];
-      cn = coefs[p + 1];
+      wn = w[t1 & cmask];
+      cn = coef_of(t1, p + 1);
     }
-    if (p + 2 < p1) col2 = cols[p + 2];
+    if (p + 2 < p1) t2 = cols[p + 2];
     if (p == rend) {  // row boundary inside the chunk
       if (first) head[c] = acc;
       else abc[r] = acc;
@@ -179,7 +194,7 @@ __global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ 
     acc = fp_add(acc, fp_mul(cf, wv));
     wv = wn;
     cf = cn;
-    col1 = col2;
+    t1 = t2;
   }
   if (first) head[c] = acc;
   else tail[c] = acc;
@@ -429,7 +444,8 @@ struct zkfl_key {
   size_t K = 0;
   uint32_t* rows = nullptr;  // [2n+1]: A rows then B rows over one term array
   uint32_t* cols = nullptr;  // [K]
-  Fr* coefs = nullptr;       // [K]
+  Fr* coefs = nullptr;       // [K] (wide) or the coefficient dictionary (packed)
+  uint32_t cshift = 0;       // packed terms: col | dict index << cshift in cols[]; 0 = wide
   MsmBases<FqOps> bA, bB1, bC, bH;
   MsmBases<Fq2Ops> bB2;
   NttPlan ntt;
@@ -588,8 +604,13 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   int pi = prof->begin("abc", st);
   if (k->K) {
     const uint32_t K = (uint32_t)k->K;
-    hipLaunchKernelGGL(k_abc_chunks, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
-                       (uint32_t)(2 * n), k->cols, k->coefs, d_w, K, s->abc_head, s->abc_tail, s->abc);
+    const AbcTerms T = {k->cols, k->coefs, k->cshift};
+    if (k->cshift)
+      hipLaunchKernelGGL(k_abc_chunks<true>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+    else
+      hipLaunchKernelGGL(k_abc_chunks<false>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
   }
   hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
                      s->abc_tail, s->abc);
@@ -884,6 +905,50 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     cols[pos] = mcs[2];
     memcpy(&coefs[(size_t)pos * 8], e + 12, 32);
   }
+  // coefficient dictionary: pack col | index << cshift when both fit one u32
+  uint32_t cshift = 0;
+  {
+    uint32_t colbits = 1;
+    while (colbits < 32 && (1ull << colbits) < nVars) colbits++;
+    struct K32 {
+      uint32_t v[8];
+      bool operator==(const K32& o) const { return memcmp(v, o.v, 32) == 0; }
+    };
+    struct H32 {
+      size_t operator()(const K32& k) const {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (uint32_t x : k.v) h = (h ^ x) * 0x100000001B3ull;
+        return (size_t)(h ^ (h >> 29));
+      }
+    };
+    std::unordered_map<K32, uint32_t, H32> idx;
+    std::vector<uint32_t> dict;
+    std::vector<uint32_t> packed(ncoef);
+    bool ok = colbits < 32;
+    for (uint32_t p = 0; p < ncoef && ok; p++) {
+      K32 key;
+      memcpy(key.v, &coefs[(size_t)p * 8], 32);
+      auto it = idx.find(key);
+      uint32_t id;
+      if (it == idx.end()) {
+        id = (uint32_t)idx.size();
+        if ((uint64_t)id >= (1ull << (32 - colbits))) {
+          ok = false;
+          break;
+        }
+        idx.emplace(key, id);
+        dict.insert(dict.end(), &coefs[(size_t)p * 8], &coefs[(size_t)p * 8] + 8);
+      } else {
+        id = it->second;
+      }
+      packed[p] = cols[p] | (id << colbits);
+    }
+    if (ok && ncoef) {
+      cshift = colbits;
+      cols.swap(packed);
+      coefs.swap(dict);
+    }
+  }
 
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   hipStream_t st = ctx->st;
@@ -906,14 +971,16 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
   } while (0)
   KTRY(hipMalloc(&k->rows, (2 * (size_t)dom + 1) * 4), "alloc rows");
   KTRY(hipMalloc(&k->cols, (size_t)(ncoef ? ncoef : 1) * 4), "alloc cols");
-  KTRY(hipMalloc(&k->coefs, (size_t)(ncoef ? ncoef : 1) * 32), "alloc coefs");
+  k->cshift = cshift;
+  const size_t ncoefs_dev = coefs.size() / 8;
+  KTRY(hipMalloc(&k->coefs, (ncoefs_dev ? ncoefs_dev : 1) * 32), "alloc coefs");
   // combined row pointers: A rows [0, dom), B rows [dom, 2 dom) over one term array (rowA[dom] == rowB[0])
   KTRY(hipMemcpyAsync(k->rows, rowptr.data(), (size_t)dom * 4, hipMemcpyHostToDevice, st), "upload");
   KTRY(hipMemcpyAsync(k->rows + dom, rowptr.data() + dom + 1, ((size_t)dom + 1) * 4, hipMemcpyHostToDevice, st),
        "upload");
   if (ncoef) {
     KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
-    KTRY(hipMemcpyAsync(k->coefs, coefs.data(), (size_t)ncoef * 32, hipMemcpyHostToDevice, st), "upload");
+    KTRY(hipMemcpyAsync(k->coefs, coefs.data(), ncoefs_dev * 32, hipMemcpyHostToDevice, st), "upload");
   }
   // MSM bases: infinity points dropped (e.g. ~1/3 of B1/B2 for Poseidon-heavy circuits: x^4
   // wires never appear in B), plus augmentation slots alpha1/delta1 (A), beta1/delta1 (B1),
