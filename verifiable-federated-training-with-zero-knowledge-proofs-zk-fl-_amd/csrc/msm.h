@@ -163,6 +163,7 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
     uint4 a = sp[0], b = sp[1];
     uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     uint32_t carry = 0;
+    uint32_t kw[MSM_W / 2], vw[MSM_W];  // this scalar's 16 keys / vals, stored as 16-B vectors
 #pragma unroll
     for (int j = 0; j < MSM_W; j++) {
       uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
@@ -173,17 +174,24 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
       } else {
         carry = 0;
       }
-      size_t e = i * MSM_W + j;
-      if (d == 0) {
-        keys[e] = MSM_KEY_NONE;
-        vals[e] = 0;
-      } else {
-        uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-        keys[e] = (uint16_t)(mag - 1);
-        vals[e] = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
+      const size_t e = i * MSM_W + j;
+      uint32_t key = MSM_KEY_NONE, val = 0;
+      if (d != 0) {
+        const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+        key = mag - 1;
+        val = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
         cnt++;
       }
+      if (j & 1) kw[j >> 1] |= key << 16;
+      else kw[j >> 1] = key;
+      vw[j] = val;
     }
+    uint4* kp = reinterpret_cast<uint4*>(keys + i * MSM_W);
+    uint4* vp = reinterpret_cast<uint4*>(vals + i * MSM_W);
+    kp[0] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+    kp[1] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) vp[q] = make_uint4(vw[4 * q], vw[4 * q + 1], vw[4 * q + 2], vw[4 * q + 3]);
   }
   // one atomic per wave
 #pragma unroll
@@ -289,6 +297,18 @@ struct MsmTailArgs {
   const uint32_t* nnz[MSM_TAIL_MAX];
   XYZZ<S>* out[MSM_TAIL_MAX];
 };
+
+// Zero the buckets (ZZ = 0: infinity) and the nnz counter of every tail in the batch: one launch
+// for all MSMs of a proof instead of two memsets each.
+template <class S>
+__global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta) {
+  const int y = blockIdx.y;
+  uint4* b = reinterpret_cast<uint4*>(ta.buckets[y]);
+  constexpr size_t nv = MSM_NB * sizeof(XYZZ<S>) / sizeof(uint4);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
+    b[i] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *const_cast<uint32_t*>(ta.nnz[y]) = 0;
+}
 
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
@@ -482,16 +502,40 @@ void msm_tail_free(MsmTail<F>& t) {
   t = MsmTail<F>();
 }
 
+template <class F>
+MsmTailArgs<F> msm_tail_args(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n) {
+  MsmTailArgs<F> ta = {};
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 2; k++) {
+      ta.key[i][k] = t[i]->item_key[k];
+      ta.val[i][k] = t[i]->item_val[k];
+    }
+    ta.buckets[i] = t[i]->buckets;
+    ta.red_a[i] = t[i]->red_a;
+    ta.red_s[i] = t[i]->red_s;
+    ta.nnz[i] = t[i]->nnz;
+    ta.out[i] = outs ? outs[i] : nullptr;
+  }
+  return ta;
+}
+
+// Empty buckets and zero nnz for n tails (before their accumulations).
+template <class F>
+hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
+  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_msm_tail_reset<F>, dim3(128, n), dim3(256), 0, st, msm_tail_args<F>(t, nullptr, n));
+  return hipGetLastError();
+}
+
 // digits (+ nnz) -> radix sort by bucket -> accumulate (level 0: fixed chunks, closed runs
-// straight into the buckets, open runs as items).  An MSM with no bases leaves nnz = 0 and
-// empty buckets: its tail yields infinity.
+// straight into the buckets, open runs as items).  The tail must have been reset
+// (msm_tails_reset).  An MSM with no bases leaves nnz = 0 and empty buckets: its tail yields
+// infinity.
 template <class F>
 hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
                           const uint32_t* d_extra, hipStream_t st, Profiler* prof = nullptr,
                           const char* tag = nullptr) {
   if (b.n > pl.cap) return hipErrorInvalidValue;
-  ZK_CHECK(hipMemsetAsync(t.nnz, 0, sizeof(uint32_t), st));
-  ZK_CHECK(hipMemsetAsync(t.buckets, 0, MSM_NB * sizeof(XYZZ<F>), st));  // ZZ = 0: infinity
   if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
   const size_t chunks = (m + MSM_L - 1) / MSM_L;
@@ -521,20 +565,9 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int TW = sizeof(typename F::T) == 32 ? 2 : MSM_G2_TAIL_WAVES;
-  MsmTailArgs<F> ta = {};
+  const MsmTailArgs<F> ta = msm_tail_args<F>(t, outs, n);
   size_t N = 0;
-  for (int i = 0; i < n; i++) {
-    for (int k = 0; k < 2; k++) {
-      ta.key[i][k] = t[i]->item_key[k];
-      ta.val[i][k] = t[i]->item_val[k];
-    }
-    ta.buckets[i] = t[i]->buckets;
-    ta.red_a[i] = t[i]->red_a;
-    ta.red_s[i] = t[i]->red_s;
-    ta.nnz[i] = t[i]->nnz;
-    ta.out[i] = outs[i];
-    N = std::max(N, t[i]->item_cap[0]);
-  }
+  for (int i = 0; i < n; i++) N = std::max(N, t[i]->item_cap[0]);
   N = std::max<size_t>(N, 2);
   int cur = 0;
   for (int level = 1;; level++) {
@@ -553,8 +586,9 @@ template <class F>
 hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
                    const uint32_t* d_extra, XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr,
                    const char* tag = nullptr) {
-  ZK_CHECK(msm_accumulate(b, pl, t, d_scalars, d_extra, st, prof, tag));
   MsmTail<F>* tp = &t;
+  ZK_CHECK(msm_tails_reset(&tp, 1, st));
+  ZK_CHECK(msm_accumulate(b, pl, t, d_scalars, d_extra, st, prof, tag));
   return msm_tails(&tp, &d_out, 1, st);
 }
 
@@ -578,6 +612,9 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
   }                                                                                                      \
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {         \
     return msm_tails(t, outs, n, st);                                                                    \
+  }                                                                                                      \
+  hipError_t msm_tails_reset_##SUF(MsmTail<F>* const* t, int n, hipStream_t st) {                        \
+    return msm_tails_reset(t, n, st);                                                                    \
   }                                                                                                      \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc,     \
                            const uint32_t* ex, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag) { \

@@ -73,6 +73,8 @@ constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs 
   hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t,            \
                                   const uint32_t* scalars, const uint32_t* extra, hipStream_t st,    \
                                   Profiler* prof, const char* tag);                                  \
+  /* empty buckets + zero nnz of n <= MSM_TAIL_MAX tails (before their accumulations) */              \
+  hipError_t msm_tails_reset_##SUF(MsmTail<F>* const* t, int n, hipStream_t st);                     \
   /* stitching + bucket reduction of n <= MSM_TAIL_MAX accumulated MSMs -> outs[i] (device) */      \
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st);    \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \

@@ -598,6 +598,8 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
   HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
+  MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
+  HIP_TRY(msm_tails_reset_g1(tails, 4, st), "msm reset");
   HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
@@ -622,7 +624,6 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
           "msm H");
   {
-    MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
     HIP_TRY(msm_tails_g1(tails, outs, 4, st), "msm tails");
   }
