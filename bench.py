@@ -35,8 +35,9 @@ sys.path.insert(0, PKG_DIR)
 
 METRIC = "Groth16 proofs/sec (training-step circuit, ~2^18 constraints) at 1/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# algorithmic bytes per accumulated (base, window) entry: 4 B sorted index + affine base
-BYTES_PER_ENTRY = {"msm_accumulate_g1": 4 + 64, "msm_accumulate_g2": 4 + 128}
+# algorithmic bytes per accumulated (base, window) entry: sorted bucket key (2 B) + entry index
+# (4 B) + the affine base it names (64 B G1, 128 B G2)
+BYTES_PER_ENTRY = {"msm_accumulate_g1": 2 + 4 + 64, "msm_accumulate_g2": 2 + 4 + 128}
 # Fq multiplications per entry: XYZZ mixed addition madd-2008-s = 8M + 2S over Fq (G1), over Fq2
 # (G2: 3 Fq products per Fq2 product, Karatsuba)
 FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
@@ -44,8 +45,8 @@ FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
 # occupancy, measured on MI355X by tools/fp_microbench.hip (tools/README.md)
 FQMUL_PEAK_GPS = 125.1
 # rocprofv3 kernel names of the instrumented kernels (profiles/pmc_traffic.json keys)
-KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps,",
-                 "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2Ops,"}
+KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOpsCompact,",
+                 "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2PairOps,"}
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")
 
@@ -157,8 +158,8 @@ def report(args, world, elapsed, prof, config, cpu, prof_proofs=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=256)   # ~1 s at 16 proofs in flight
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slots", type=int, default=16, help="proofs in flight per GPU (one HIP stream each)")

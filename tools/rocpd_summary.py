@@ -70,7 +70,8 @@ def pmc(fetch_db, write_db, calib_db, out):
         json.dump(res, f, indent=1, sort_keys=True)
 
 
-ROOFLINE_KERNELS = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps", "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2Ops"}
+ROOFLINE_KERNELS = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOpsCompact",
+                    "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2PairOps"}
 
 
 def roofline(db, bench_log, out):
@@ -126,8 +127,8 @@ def breakdown(db, out, proofs=6):
 
 
 def _category(name):
-    for key, cat in (("k_msm_accumulate<zkfl::FqOps", "acc_g1"), ("k_msm_accumulate<zkfl::Fq2Ops", "acc_g2"),
-                     ("bucket_sum", "stitch"), ("reduce_level", "reduce"), ("sum8", "reduce"), ("rocprim", "sort"),
+    for key, cat in (("k_msm_accumulate<zkfl::FqOps", "acc_g1"), ("k_msm_accumulate<zkfl::Fq2", "acc_g2"),
+                     ("stitch", "stitch"), ("wsum", "reduce"), ("rocprim", "sort"),
                      ("k_ntt", "ntt"), ("k_abc", "abc"), ("assemble", "asm")):
         if key in name:
             return cat
