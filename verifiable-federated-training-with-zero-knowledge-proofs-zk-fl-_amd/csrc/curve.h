@@ -159,6 +159,12 @@ ZK_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   return r;
 }
 
+// Coordinates back to the canonical range (identity unless F keeps a redundant representation).
+template <class F>
+ZK_DEV XYZZ<F> xyzz_canon(const XYZZ<F>& p) {
+  return {F::canon(p.X), F::canon(p.Y), F::canon(p.ZZ), F::canon(p.ZZZ)};
+}
+
 // XYZZ -> affine (Montgomery), one field inversion.  Infinity -> (0, 0).
 template <class F>
 ZK_DEV Affine<F> xyzz_to_affine(const XYZZ<F>& p) {

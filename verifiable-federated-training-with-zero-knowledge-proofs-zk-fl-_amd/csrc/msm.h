@@ -83,26 +83,33 @@ struct MsmIO<Fq2PairOps> {
     q[6 + h] = v.ZZZ;
   }
 };
-template <>
-struct MsmIO<FqOpsCompact> {
+// G1 compute types with another arithmetic over the same storage (one lane per point).
+template <class F>
+struct MsmIOSameLayout {
   using S = FqOps;
   static constexpr int LANES = 1;
-  using F = FqOpsCompact;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return reinterpret_cast<const Affine<F>*>(p)[i]; }
   static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return reinterpret_cast<const XYZZ<F>*>(p)[i]; }
   static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<F>& v) { reinterpret_cast<XYZZ<F>*>(p)[i] = v; }
 };
-// Compute type the MSM kernels use for a stored curve.
+template <>
+struct MsmIO<FqOpsCompact> : MsmIOSameLayout<FqOpsCompact> {};
+template <>
+struct MsmIO<FqOpsLazy> : MsmIOSameLayout<FqOpsLazy> {};
+// Compute type the MSM kernels use for a stored curve (G1: redundant [0, 2p) arithmetic with
+// the compact multiply; MSM_G1_NO_LAZY: canonical values, compact multiply).
 template <class F>
 struct MsmCompute {
   using type = F;
 };
-#ifndef MSM_G1_NO_COMPACT
 template <>
 struct MsmCompute<FqOps> {
+#ifndef MSM_G1_NO_LAZY
+  using type = FqOpsLazy;
+#else
   using type = FqOpsCompact;
-};
 #endif
+};
 template <>
 struct MsmCompute<Fq2Ops> {
   using type = Fq2PairOps;
@@ -418,7 +425,7 @@ k_msm_wsum(const MsmTailArgs<S> ta, int level) {
   if (t == 0) {
     const int lq = 31 - __builtin_clz((unsigned)Q);
     for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
-    IO::st(out_a, blockIdx.x, xyzz_add<F>(y, x));
+    IO::st(out_a, blockIdx.x, xyzz_canon<F>(xyzz_add<F>(y, x)));  // [0, p) when it leaves the MSM
     IO::st(out_s, blockIdx.x, R);
   }
 }
