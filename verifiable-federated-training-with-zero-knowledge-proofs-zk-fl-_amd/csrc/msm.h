@@ -35,24 +35,24 @@ namespace zkfl {
 
 // Kernel occupancy per curve (measured on MI355X).  G1: the accumulation fits 128
 // VGPRs (4 waves/SIMD); its stitching/reduction kernels run at 2-3.  G2 runs on lane pairs
-// (Fq2PairOps): 184-234 VGPRs, 2 waves/SIMD without spills; one lane per G2 point needed > 256
-// registers, so a single wave owned the whole SIMD for the kernel's duration (measured
-// 186 -> 208 proofs/s moving G2 to lane pairs, although the pair does 4 Fq products per Fq2
-// product where one lane does 3).
+// (Fq2PairOps): the accumulation 168 VGPRs (3 waves/SIMD), the tails 179-241 (2 waves/SIMD), no
+// spills; one lane per G2 point needed > 256 registers, so a single wave owned the whole SIMD
+// for the kernel's duration (measured 186 -> 208 proofs/s moving G2 to lane pairs).
 #ifndef MSM_G1_WAVES
 #define MSM_G1_WAVES 4
 #endif
+#ifndef MSM_G2_WAVES
+#define MSM_G2_WAVES 3
+#endif
 // 1: the next entry's base is loaded while the current one is added (one affine point of
-// registers); 0: loaded after it, latency hidden by the other waves only.  G1 at 4 waves/SIMD:
-// without it 19 -> 3 spilled VGPRs and 1.71 -> 1.65 ms per proof (measured).
+// registers); 0: loaded after it, latency hidden by the other waves only.  Without it G1 at 4
+// waves/SIMD spills 3 VGPRs instead of 19 (1.71 -> 1.65 ms per proof) and G2 fits 3 waves/SIMD
+// without spills (1.00 -> 0.955 ms per proof); measured.
 #ifndef MSM_G1_PREFETCH
 #define MSM_G1_PREFETCH 0
 #endif
 #ifndef MSM_G2_PREFETCH
-#define MSM_G2_PREFETCH 1
-#endif
-#ifndef MSM_G2_WAVES
-#define MSM_G2_WAVES 2
+#define MSM_G2_PREFETCH 0
 #endif
 #ifndef MSM_G2_TAIL_WAVES
 #define MSM_G2_TAIL_WAVES 2
