@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, i
 // 2^(logn-k).  One workgroup takes NTT_COL_TILE / 2^k consecutive columns (rows of consecutive
 // elements are contiguous in memory), runs the k stages in LDS and writes back: one global pass
 // instead of k radix-2 passes.
-constexpr int NTT_COL_TILE_LOG = 11;
+constexpr int NTT_COL_TILE_LOG = 10;
 constexpr int NTT_COL_TILE = 1 << NTT_COL_TILE_LOG;
 template <bool DIF>
 __global__ void __launch_bounds__(256) k_ntt_cols(Fr* __restrict__ a, int logn, int k, const Fr* __restrict__ tw,
