@@ -45,8 +45,8 @@ FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
 # occupancy, measured on MI355X by tools/fp_microbench.hip (tools/README.md)
 FQMUL_PEAK_GPS = 125.1
 # rocprofv3 kernel names of the instrumented kernels (profiles/pmc_traffic.json keys)
-KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOpsCompact,",
-                 "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2PairOps,"}
+KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOpsLazy (G1 compute type)
+                 "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}     # Fq2PairOps
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")
 

@@ -70,8 +70,8 @@ def pmc(fetch_db, write_db, calib_db, out):
         json.dump(res, f, indent=1, sort_keys=True)
 
 
-ROOFLINE_KERNELS = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOpsCompact",
-                    "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2PairOps"}
+ROOFLINE_KERNELS = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",
+                    "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}
 
 
 def roofline(db, bench_log, out):
