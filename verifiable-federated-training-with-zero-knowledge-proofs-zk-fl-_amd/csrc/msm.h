@@ -255,13 +255,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   const size_t p0 = c * MSM_L;
   if (p0 >= nnz) return;
   const uint32_t p1 = (uint32_t)(p0 + MSM_L < nnz ? p0 + MSM_L : nnz);
-  const uint32_t kprev = p0 > 0 ? keys[p0 - 1] : 0xFFFFFFFFu;
-  const uint32_t knext = p1 < nnz ? keys[p1] : 0xFFFFFFFFu;
-  uint32_t* okey = item_key + 2 * c;
-  XYZZ<S>* oval = item_val + 2 * c;
-  bool slot0 = false, slot1 = false;
+  // the neighbouring chunks' keys and the item slots are only read at a run's end (registers are
+  // the G1 kernel's limit at 4 waves/SIMD)
+  bool slot0 = false, slot1 = false, first_run = true;
   XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t cur = keys[p0], run_start = (uint32_t)p0;
+  uint32_t cur = keys[p0];
   uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
   if (p0 + 1 < p1) {
     k1 = keys[p0 + 1];
@@ -279,11 +277,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
     const bool last = p + 1 == p1;
     if (last || k1 != cur) {
-      msm_emit_run<F>(cur, acc, true, run_start == p0 && kprev == cur, last && knext == cur, buckets, okey, oval,
-                      slot0, slot1);
+      const bool open_left = first_run && p0 > 0 && keys[p0 - 1] == cur;
+      const bool open_right = last && p1 < nnz && keys[p1] == cur;
+      msm_emit_run<F>(cur, acc, true, open_left, open_right, buckets, item_key + 2 * c, item_val + 2 * c, slot0,
+                      slot1);
       acc = xyzz_inf<F>();
       cur = k1;
-      run_start = p + 1;
+      first_run = false;
     }
     v0 = v1;
     v1 = v2;
@@ -291,8 +291,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     if (PF) a = an;
     else if (p + 1 < p1) a = IO::ld_aff(bases, v0 & 0x7FFFFFFFu);
   }
-  if (!slot0) okey[0] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
-  if (!slot1) okey[1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
+  if (!slot0) item_key[2 * c] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
+  if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
 }
 
 // Item count of stitching level `level` (>= 1), derived on the device from nnz.
