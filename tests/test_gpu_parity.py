@@ -162,6 +162,47 @@ def test_msm_g2_identity(gpu_ctx, n):
     assert _g2_std(out) == bn.mul(bn.G2_GEN, _expect(ks, ss))
 
 
+@pytest.mark.parametrize("case", ["zeros", "ones", "dup", "cancel", "neg", "inf_base"])
+def test_msm_g2_edge_cases(gpu_ctx, case):
+    """G2 runs on lane pairs (csrc/field.h Fq2PairOps): the exceptional additions (P + P inside a
+    bucket, P + (-P), infinity bases) and a single-bucket skew must stay pair-uniform."""
+    rnd = random.Random(hash(case) & 0xFFFF)
+    n = 1500
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [rnd.randrange(R) for _ in range(n)]
+    if case == "zeros":
+        ss = [0] * n
+    elif case == "ones":
+        ss = [1] * n
+    elif case == "dup":
+        ks = [ks[0]] * n
+        ss = [ss[0]] * n
+    elif case == "cancel":
+        ks = [ks[i // 2] if i % 2 == 0 else R - ks[i // 2] for i in range(n)]
+        ss = [ss[i // 2] for i in range(n)]
+    elif case == "neg":
+        ss = [(R - rnd.randrange(1, 1 << 20)) for _ in range(n)]
+    bases = bytearray(_bases_g2(gpu_ctx, ks))
+    if case == "inf_base":
+        for i in range(0, n, 3):
+            bases[128 * i:128 * i + 128] = bytes(128)
+            ks[i] = 0
+    out = gpu_ctx.msm_g2(bytes(bases), _scal(ss))
+    want = _expect(ks, ss)
+    assert _g2_std(out) == (bn.mul(bn.G2_GEN, want) if want else None)
+
+
+def test_msm_g1_single_bucket_deep_stitch(gpu_ctx):
+    """60,000 entries in one bucket: 3,750 chunks, several stitching levels before one lane holds
+    the bucket (csrc/msm.h k_msm_stitch)."""
+    rnd = random.Random(77)
+    n = 60000
+    ks = [rnd.randrange(1, R) for _ in range(n)]
+    ss = [1] * n
+    out = gpu_ctx.msm_g1(_bases_g1(gpu_ctx, ks), _scal(ss))
+    assert _g1_std(out) == bn.mul(bn.G1_GEN, _expect(ks, ss))
+
+
 def test_msm_g2_small_scalars(gpu_ctx):
     rnd = random.Random(3)
     n = 2000
