@@ -163,8 +163,10 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
 // ---------------------------------------------------------------------------
 // Per-MSM kernels
 // ---------------------------------------------------------------------------
-// Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31.
-// Also counts the non-zero digits into *nnz (the sorted prefix the accumulation covers).
+// Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31, written
+// window-major (position j*n + i: consecutive lanes store consecutive words; the sort that
+// follows does not care about the input order).  Also counts the non-zero digits into *nnz
+// (the sorted prefix the accumulation covers).
 static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
                                                            const uint32_t* __restrict__ extra,
                                                            const uint32_t* __restrict__ sidx, uint32_t extra_start,
@@ -179,7 +181,6 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
     uint4 a = sp[0], b = sp[1];
     uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     uint32_t carry = 0;
-    uint32_t kw[MSM_W / 2], vw[MSM_W];  // this scalar's 16 keys / vals, stored as 16-B vectors
 #pragma unroll
     for (int j = 0; j < MSM_W; j++) {
       uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
@@ -190,24 +191,16 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
       } else {
         carry = 0;
       }
-      const size_t e = i * MSM_W + j;
       uint32_t key = MSM_KEY_NONE, val = 0;
       if (d != 0) {
         const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
         key = mag - 1;
-        val = (uint32_t)e | (d < 0 ? 0x80000000u : 0u);
+        val = (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u);
         cnt++;
       }
-      if (j & 1) kw[j >> 1] |= key << 16;
-      else kw[j >> 1] = key;
-      vw[j] = val;
+      keys[(size_t)j * n + i] = (uint16_t)key;
+      vals[(size_t)j * n + i] = val;
     }
-    uint4* kp = reinterpret_cast<uint4*>(keys + i * MSM_W);
-    uint4* vp = reinterpret_cast<uint4*>(vals + i * MSM_W);
-    kp[0] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
-    kp[1] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
-#pragma unroll
-    for (int q = 0; q < 4; q++) vp[q] = make_uint4(vw[4 * q], vw[4 * q + 1], vw[4 * q + 2], vw[4 * q + 3]);
   }
   // one atomic per wave
 #pragma unroll
