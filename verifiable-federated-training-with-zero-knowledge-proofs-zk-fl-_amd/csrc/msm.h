@@ -245,9 +245,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   constexpr bool PF = sizeof(typename S::T) == 32 ? MSM_G1_PREFETCH : MSM_G2_PREFETCH;
   const size_t c = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
   const uint32_t nnz = *nnz_ptr;
-  const size_t p0 = c * MSM_L;
+  constexpr uint32_t L = MsmChunk<S>::L;
+  const size_t p0 = c * L;
   if (p0 >= nnz) return;
-  const uint32_t p1 = (uint32_t)(p0 + MSM_L < nnz ? p0 + MSM_L : nnz);
+  const uint32_t p1 = (uint32_t)(p0 + L < nnz ? p0 + L : nnz);
   // the neighbouring chunks' keys and the item slots are only read at a run's end (registers are
   // the G1 kernel's limit at 4 waves/SIMD)
   bool slot0 = false, slot1 = false, first_run = true;
@@ -289,8 +290,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
 }
 
 // Item count of stitching level `level` (>= 1), derived on the device from nnz.
+template <class S>
 ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
-  uint32_t n = 2 * ((nnz + MSM_L - 1) / MSM_L);
+  constexpr uint32_t L = MsmChunk<S>::L;
+  uint32_t n = 2 * ((nnz + L - 1) / L);
   for (int l = 1; l < level; l++) n = 2 * ((n + MSM_SG - 1) / MSM_SG);
   return n;
 }
@@ -332,7 +335,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   XYZZ<S>* __restrict__ out_val = ta.val[y][src ^ 1];
   XYZZ<S>* __restrict__ buckets = ta.buckets[y];
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
-  const uint32_t N = msm_items_at(*ta.nnz[y], level);
+  const uint32_t N = msm_items_at<S>(*ta.nnz[y], level);
   const uint32_t q0 = g * MSM_SG;
   if (q0 >= N) return;
   const uint32_t q1 = q0 + MSM_SG < N ? q0 + MSM_SG : N;
@@ -491,7 +494,7 @@ void msm_scratch_free(MsmScratch<F>& s) {
 template <class F>
 hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
   const size_t m = cap * MSM_W;
-  t.max_chunks = (m + MSM_L - 1) / MSM_L;
+  t.max_chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
   t.item_cap[0] = 2 * t.max_chunks;
   t.item_cap[1] = 2 * ((t.item_cap[0] + MSM_SG - 1) / MSM_SG);
   for (int k = 0; k < 2; k++) {
@@ -549,7 +552,7 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
   if (b.n > pl.cap) return hipErrorInvalidValue;
   if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
-  const size_t chunks = (m + MSM_L - 1) / MSM_L;
+  const size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
   if (need > pl.sort_tmp_bytes || chunks > t.max_chunks) return hipErrorInvalidValue;

@@ -16,6 +16,18 @@ constexpr int MSM_SG = 8;                  // partial sums per lane in each stit
 constexpr int MSM_RB = 64;                 // items per block (one wave) in the weighted bucket reduction
 constexpr uint32_t MSM_ITEM_DUMMY = 0x80000000u;  // stitch item flag: padding (its value is infinity)
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
+#ifndef MSM_G2_L
+#define MSM_G2_L 16
+#endif
+// Chunk length per curve (storage field type S)
+template <class S>
+struct MsmChunk {
+  static constexpr int L = MSM_L;
+};
+template <>
+struct MsmChunk<Fq2Ops> {
+  static constexpr int L = MSM_G2_L;
+};
 
 
 // Read-only, per proving key: every base expanded into its W window copies.
