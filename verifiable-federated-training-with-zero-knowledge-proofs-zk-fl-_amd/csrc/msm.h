@@ -57,6 +57,12 @@ namespace zkfl {
 #ifndef MSM_G2_TAIL_WAVES
 #define MSM_G2_TAIL_WAVES 2
 #endif
+#ifndef MSM_G1_TAIL_WAVES
+#define MSM_G1_TAIL_WAVES 2
+#endif
+#ifndef MSM_G1_STITCH_WAVES
+#define MSM_G1_STITCH_WAVES MSM_G1_TAIL_WAVES
+#endif
 
 // Compute type -> storage: how the point kernels read and write the stored points.  G1 and plain
 // Fq2 hold a point per lane; Fq2PairOps holds it across a lane pair (component h of every
@@ -578,7 +584,8 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
-  constexpr int TW = sizeof(typename F::T) == 32 ? 2 : MSM_G2_TAIL_WAVES;
+  constexpr int TW = sizeof(typename F::T) == 32 ? MSM_G1_TAIL_WAVES : MSM_G2_TAIL_WAVES;
+  constexpr int SW = sizeof(typename F::T) == 32 ? MSM_G1_STITCH_WAVES : MSM_G2_TAIL_WAVES;
   const MsmTailArgs<F> ta = msm_tail_args<F>(t, outs, n);
   size_t N = 0;
   for (int i = 0; i < n; i++) N = std::max(N, t[i]->item_cap[0]);
@@ -586,7 +593,7 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   int cur = 0;
   for (int level = 1;; level++) {
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
-    hipLaunchKernelGGL((k_msm_stitch<FC, TW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
+    hipLaunchKernelGGL((k_msm_stitch<FC, SW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
     if (N <= (size_t)MSM_SG) break;
     N = 2 * lanes;
     cur ^= 1;
