@@ -25,9 +25,10 @@ import time
 # GPU_MAX_HW_QUEUES hardware queues (HIP default 4, which the GPU boxes also export), and streams
 # sharing a queue serialize.  Set it before anything initializes HIP.  Measured on MI355X
 # (tools/concurrency_probe.hip): kernels on distinct streams run concurrently up to ~20 at 24
-# queues, while 32 queues oversubscribe the hardware queue slots; 16 slots x 1 stream at 24 queues
-# is the best measured configuration.  ZKFL_HW_QUEUES overrides the value used here.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "24")
+# queues, while 32 queues oversubscribe the hardware queue slots; 20 slots x 1 stream at 28 queues
+# is the best measured configuration (322.2 / 320.0 against 317.4 for 16 x 24,
+# profiles/r01_experiments.md).  ZKFL_HW_QUEUES overrides the value used here.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "28")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd")
@@ -162,7 +163,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--slots", type=int, default=16, help="proofs in flight per GPU (one HIP stream each)")
+    ap.add_argument("--slots", type=int, default=20, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     args = ap.parse_args()
 
