@@ -5,12 +5,17 @@ Workload (BASELINE.json metric): TrainingStepVerified(B
 DIM=4, DEPTH=7, PRECISION=1000) — the reference's sgd_verified.circom at the Report's N=128
 scale — with synthetic client inputs from the reference harness's seeded generator
 (tests/full_system_simulation.mjs:273-303, weights = 0, tau^2 = 1e8, round 1).
-A step = one full Groth16 proof (ABC, 3x coset NTT, 4 G1 + 1 G2 MSM, assembly) from a
-device-resident witness with the proving key resident in HBM; r, s from the OS CSPRNG.
-Multi-GPU: one process per GPU, independent proofs per rank (weak scaling, no collective on
-the data path); the barrier / max-over-ranks timing uses torch.distributed.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the roofline definitions).
+A step = one batch of `--slots` Groth16 proofs (ABC, 3x coset NTT, 4 G1 + 1 G2 MSM, assembly),
+one per in-flight proof slot, from device-resident witnesses with the proving key resident in HBM;
+K steps = K x slots proofs pushed through the batch prover in one call (the slots stay full across
+step boundaries).  r, s come from the OS CSPRNG on the host and are passed in, so every timed
+proof is checked after the timed region: all of them by the GPU batch verifier, and the first one
+bit-for-bit against the C oracle inside the cpu_baseline leg.  Multi-GPU: one process per GPU,
+independent proofs per rank (weak scaling, no collective on the data path); the barrier /
+max-over-ranks timing uses torch.distributed.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §6 for the roofline definitions).
 """
 
 from __future__ import annotations
@@ -36,15 +41,21 @@ sys.path.insert(0, PKG_DIR)
 
 METRIC = "Groth16 proofs/sec (training-step circuit, ~2^18 constraints) at 1/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# algorithmic bytes per accumulated (base, window) entry: sorted bucket key (2 B) + entry index
-# (4 B) + the affine base it names (64 B G1, 128 B G2)
-BYTES_PER_ENTRY = {"msm_accumulate_g1": 2 + 4 + 64, "msm_accumulate_g2": 2 + 4 + 128}
+# Roofline of record: algorithmic bytes of one G1 MSM = every base of its query
+# read once (64 B affine) + its scalar (32 B); a launch of k_msm_accumulate<G1> is one MSM (A, B1,
+# C or H, query lengths nVars, nVars, nVars - nPublic - 1, domainSize).
+ALGO_BYTES_PER_BASE = {"msm_accumulate_g1": 64 + 32, "msm_accumulate_g2": 128 + 32}
+# What this implementation moves instead: bases are window-expanded 16x at key load
+# so every accumulated (base, window) entry reads its own 64 B / 128 B point + 2 B key + 4 B index.
+IMPL_BYTES_PER_ENTRY = {"msm_accumulate_g1": 2 + 4 + 64, "msm_accumulate_g2": 2 + 4 + 128}
 # Fq multiplications per entry: XYZZ mixed addition madd-2008-s = 8M + 2S over Fq (G1), over Fq2
-# (G2: 3 Fq products per Fq2 product, Karatsuba)
+# (G2: 3 Fq products per Fq2 product)
 FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
-# the integer-VALU ceiling: Fq Montgomery multiplications/s of the library's fp_mul at full
-# occupancy, measured on MI355X by tools/fp_microbench.hip (tools/README.md)
-FQMUL_PEAK_GPS = 125.1
+# Integer-VALU ceiling from ISA issue rates, not from this library's own multiply: a 256-bit
+# product-scanning Montgomery multiply is 128 v_mad_u64_u32 (8x8 limb products for a*b and for
+# m*p) + 128 carry adds; issue costs relative to a 2-cycle wave64 v_add_u32 are 2.2x / 1.8x
+# (tools/isa_rate.hip, MI355X).  1024 SIMDs x 32 lanes/cycle x 2.4 GHz / (128 x 2.2 + 128 x 1.8).
+FQMUL_PEAK_GPS = 1024 * 32 * 2.4 / (128 * 2.2 + 128 * 1.8)     # = 153.6 G Fq-mul/s
 # rocprofv3 kernel names of the instrumented kernels (profiles/pmc_traffic.json keys)
 KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOpsLazy (G1 compute type)
                  "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}     # Fq2PairOps
@@ -61,17 +72,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline_leg(zk: bytes, wt: bytes, seconds_budget=20.0):
+def cpu_baseline_leg(zk: bytes, wt: bytes, rs: bytes, seconds_budget=20.0):
     """Oracle ("port") on the host cores: the C restatement (oracle/c/groth16_ref.c) proving
-    the same zkey/wtns, bounded to ~seconds_budget, reported as proofs/s."""
+    the same zkey/wtns with the same (r, s) as the first timed GPU proof, bounded to
+    ~seconds_budget, reported as proofs/s.  -> (report dict, the oracle's proof bytes)."""
     sys.path.insert(0, ROOT)
     from oracle import cbaseline
-    return cbaseline.time_prove(zk, wt, seconds_budget)
+    return cbaseline.time_prove(zk, wt, seconds_budget, rs)
 
 
-def timed_run(key, warm_w, steps_w, ctx, dist):
-    """W untimed proofs, then exactly K timed proofs bracketed by barrier + synchronize on both
-    sides; returns (max-over-ranks elapsed seconds, proofs)."""
+def draw_rs(n):
+    """n x (r || s), 32 B little-endian each, uniform below the BN254 scalar order (OS CSPRNG)."""
+    import secrets
+    from zkfl.field import R
+    return b"".join(secrets.randbelow(R).to_bytes(32, "little") + secrets.randbelow(R).to_bytes(32, "little")
+                    for _ in range(n))
+
+
+def timed_run(key, warm_w, steps_w, rs, ctx, dist):
+    """W untimed steps, then exactly K timed steps (K x slots proofs in one batch call) bracketed
+    by barrier + synchronize on both sides; returns (max-over-ranks elapsed seconds, proofs)."""
 
     def barrier_sync():
         ctx.synchronize()
@@ -85,7 +105,7 @@ def timed_run(key, warm_w, steps_w, ctx, dist):
         key.prove_batch(warm_w)
     barrier_sync()
     t_start = time.perf_counter()
-    proofs = key.prove_batch(steps_w)          # K proofs, `slots` in flight
+    proofs = key.prove_batch(steps_w, rs)      # K steps x `slots` proofs, `slots` in flight
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
@@ -97,8 +117,37 @@ def timed_run(key, warm_w, steps_w, ctx, dist):
     return elapsed, proofs
 
 
+def verify_all(ctx, zk, proofs, pubs_of):
+    """Every timed proof through the GPU batch verifier (zkfl_groth16_verify_batch)."""
+    from zkfl import groth16
+    vk = groth16.vk_bytes(groth16.export_verification_key(zk, alphabeta=False))
+    pubs = b"".join(pubs_of(i) for i in range(len(proofs)))
+    npub = len(pubs_of(0)) // 32
+    ok = ctx.verify_batch(vk, pubs, b"".join(proofs), npub)
+    return sum(ok)
+
+
+def end_to_end_leg(key, wp, json_inputs, slots, batches):
+    """input.json text -> proofs: the C parser (zkfl_wprog_parse_inputs), the GPU witness engine
+    straight into HBM, then the batch prover; `batches` x `slots` proofs, host-timed."""
+    from zkfl import native
+    image = wp.image
+    t0 = time.perf_counter()
+    n = 0
+    for b in range(batches):
+        texts = [json_inputs[(b * slots + i) % len(json_inputs)] for i in range(slots)]
+        res = wp.compute_resident(key, [native.parse_inputs(image, t) for t in texts])
+        proofs = key.prove_batch(res)
+        n += len(proofs)
+        for r_ in res:
+            r_.close()
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "proofs/s", "proofs": n,
+            "path": "input.json -> C parse -> GPU witness (resident) -> GPU proof, serial per batch"}
+
+
 def roofline_pass(key, ctx, ws, slots, n=6):
-    """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's three
+    """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's
     streams serialized onto one), after the timed region: the roofline's average launch time."""
     key.set_slots(1)
     key.prove_batch(ws[:1])
@@ -125,46 +174,46 @@ def _pmc_traffic(kernel):
     return None
 
 
-def report(args, world, elapsed, prof, config, cpu, prof_proofs=1):
-    """The one JSON line (rank 0)."""
-    ms_per_step = elapsed / args.steps * 1e3
-    value = world * args.steps / elapsed
-    cand = {k: v for k, v in prof.items() if k in BYTES_PER_ENTRY and v[1] > 0}
-    roofline = None
-    if cand:
-        dom = max(cand, key=lambda k: cand[k][0])
-        ms_tot, launches, units, med_ms = prof[dom]
-        avg_s = med_ms / 1e3        # median launch: robust to a one-off stalled dispatch
-        entries = units / launches
-        achieved = entries * BYTES_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
-        fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": _pmc_traffic(dom),
-                    "algorithmic_bytes": round(entries * BYTES_PER_ENTRY[dom]),
-                    "avg_launch_ms": round(avg_s * 1e3, 4), "mean_launch_ms": round(ms_tot / launches, 4),
-                    "launches": launches,
-                    "entries_per_launch": round(entries),
-                    "valu": {"achieved": round(fq, 2), "peak": FQMUL_PEAK_GPS, "unit": "G Fq-mul/s",
-                             "frac": round(fq / FQMUL_PEAK_GPS, 4)}}
-    stage_ms = {k: round(v[3] * v[1] / max(1, prof_proofs), 3) for k, v in prof.items()}  # median x launches
-    return {
-        "metric": METRIC, "value": round(value, 4), "unit": "proofs/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic (reference harness seeded client generator)",
-        "config": config, "roofline": roofline, "stage_ms_isolated_per_proof": stage_ms, "cpu_baseline": cpu,
-    }
+def roofline(prof, key):
+    """The dominant kernel's roofline."""
+    cand = {k: v for k, v in prof.items() if k in IMPL_BYTES_PER_ENTRY and v[1] > 0}
+    if not cand:
+        return None
+    dom = max(cand, key=lambda k: cand[k][0])
+    ms_tot, launches, units, med_ms = prof[dom]
+    avg_s = med_ms / 1e3        # median launch: robust to a one-off stalled dispatch
+    if dom == "msm_accumulate_g1":      # launches cycle A, B1, C, H
+        q = (2 * key.n_vars + (key.n_vars - key.n_public - 1) + key.domain_size) / 4
+    else:
+        q = key.n_vars
+    algo = q * ALGO_BYTES_PER_BASE[dom]
+    entries = units / launches
+    impl = entries * IMPL_BYTES_PER_ENTRY[dom]
+    traffic = _pmc_traffic(dom)
+    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "algorithmic_bytes": round(algo), "query_length": round(q),
+            "impl_bytes": round(impl), "impl_GBps": round(impl / avg_s / 1e9, 1) if avg_s > 0 else 0.0,
+            "traffic_over_algorithmic": round(traffic / algo, 2) if traffic else None,
+            "avg_launch_ms": round(avg_s * 1e3, 4), "mean_launch_ms": round(ms_tot / launches, 4),
+            "launches": launches, "entries_per_launch": round(entries),
+            "valu": {"achieved": round(fq, 2), "peak": round(FQMUL_PEAK_GPS, 1), "unit": "G Fq-mul/s",
+                     "frac": round(fq / FQMUL_PEAK_GPS, 4),
+                     "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (128 mad x 2.2 + 128 addc x 1.8)"}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=256)   # ~1 s at 16 proofs in flight
-    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=16, help="timed steps (one step = --slots proofs)")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed steps")
     ap.add_argument("--circuit", default="M", choices=sorted(CIRCUITS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slots", type=int, default=20, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
+    ap.add_argument("--e2e-steps", type=int, default=4, help="steps of the input.json -> proof leg (0: skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -186,10 +235,11 @@ def main():
     t0 = time.perf_counter()
     b = circuits.build(name, *params)
     batch, dim, depth, precision = params
-    inputs = []
+    input_objs = []
     for c in range(args.clients):
         client = clients.Client(rank * args.clients + c + 1, batch, dim, depth, clients.JsLcg(12345 + c))
-        inputs.append(wprog.input_bytes(b, client.training_input(batch, precision, 100000000)[0]))
+        input_objs.append(client.training_input(batch, precision, 100000000)[0])
+    inputs = [wprog.input_bytes(b, x) for x in input_objs]
     log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires "
         f"({time.perf_counter() - t0:.1f} s)")
 
@@ -206,24 +256,53 @@ def main():
     t0 = time.perf_counter()
     res = wp.compute_resident(key, inputs)      # GPU witness generation straight into HBM
     log(f"[bench r{rank}] {len(res)} client witnesses on the GPU ({(time.perf_counter() - t0) * 1e3:.1f} ms)")
-    steps_w = [res[i % len(res)] for i in range(args.steps)]
-    warm_w = [res[i % len(res)] for i in range(max(args.warmup, args.slots) if args.warmup else 0)]
+    wts = wp.compute(inputs)                    # host .wtns images: public signals + the oracle check
+    n_timed = args.steps * args.slots
+    steps_w = [res[i % len(res)] for i in range(n_timed)]
+    warm_w = [res[i % len(res)] for i in range(args.warmup * args.slots)]
+    rs = draw_rs(n_timed)
 
-    elapsed, proofs = timed_run(key, warm_w, steps_w, ctx, dist)
+    elapsed, proofs = timed_run(key, warm_w, steps_w, rs, ctx, dist)
+    assert len(proofs) == n_timed and all(len(p) == 256 for p in proofs)
+    pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]   # wtns v2: header 76 B, wire 0 = 1
+    verified = verify_all(ctx, zk, proofs, lambda i: pubs[i % len(pubs)])
+    log(f"[bench r{rank}] {n_timed} proofs in {elapsed:.3f} s; GPU batch verifier: {verified}/{n_timed} valid")
+    if verified != n_timed:
+        raise SystemExit(f"[bench r{rank}] {n_timed - verified} timed proofs do not verify")
     prof, nprof = roofline_pass(key, ctx, res, args.slots)
+    e2e = None
+    if args.e2e_steps:
+        wp.image = wprog.compile_program(b)
+        e2e = end_to_end_leg(key, wp, [json.dumps(x) for x in input_objs], args.slots, args.e2e_steps)
+        log(f"[bench r{rank}] end to end: {e2e}")
     if rank == 0:
-        cpu = None
+        cpu, oracle_match = None, None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline_leg(zk, wp.compute(inputs[:1])[0])
+                cpu, ref = cpu_baseline_leg(zk, wts[0], rs[:64])
+                oracle_match = ref == proofs[0]
+                cpu["oracle_check"] = "timed proof 0 == C oracle proof (same zkey, wtns, r, s)" if oracle_match \
+                    else "MISMATCH: timed proof 0 differs from the C oracle"
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
         config = {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
                   "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
-                  "global_batch": world, "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
+                  "global_batch": args.slots * world, "step": f"{args.slots} proofs per GPU (one per slot)",
+                  "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}
-        print(json.dumps(report(args, world, elapsed, prof, config, cpu, nprof)), flush=True)
-    assert len(proofs) == args.steps and all(len(p) == 256 for p in proofs)
+        stage_ms = {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()}  # median x launches
+        line = {
+            "metric": METRIC, "value": round(world * n_timed / elapsed, 4), "unit": "proofs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (reference harness seeded client generator)",
+            "config": config, "proofs_timed": n_timed * world, "verified": verified * world,
+            "oracle_match": oracle_match, "roofline": roofline(prof, key),
+            "stage_ms_isolated_per_proof": stage_ms, "end_to_end": e2e, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+        if oracle_match is False:
+            raise SystemExit("[bench] timed proof 0 differs from the C oracle")
     for r_ in res:
         r_.close()
     wp.close()

@@ -428,8 +428,11 @@ static void g2_to_std_aff(uint8_t* out, const g2_jac* p) {
   memcpy(out + 64, y.c0.v, 32); memcpy(out + 96, y.c1.v, 32);
 }
 
-int ref_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, const uint8_t* rs, uint8_t* proof,
-              int threads) {
+/* Full proof plus the deterministic core for parity checks: h_out (n x 32 B std, the H-MSM
+ * scalars) and msm_out (A 64 | B1 64 | B2 128 | C 64 | H 64, std affine, without the
+ * alpha/beta/delta/r/s terms), both nullable: the layout of zkfl_debug_prove_parts. */
+int ref_prove_ex(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, const uint8_t* rs, uint8_t* proof,
+                 int threads, uint8_t* h_out, uint8_t* msm_out) {
   init_consts();
   if (threads > 0) omp_set_num_threads(threads);
   sec_t s[16], w[4];
@@ -497,6 +500,7 @@ int ref_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, co
     from_mont_r(&hs[i]);
   }
   free(abc);
+  if (h_out) memcpy(h_out, hs, (size_t)n * 32);
 
   /* MSMs */
   g1_jac mA, mB1, mC, mH;
@@ -507,6 +511,13 @@ int ref_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, co
   g1_msm(&mC, (const g1_aff*)s[8].p, wit + nPub + 1, nVars - nPub - 1);
   g1_msm(&mH, (const g1_aff*)s[9].p, hs, n);
   free(hs);
+  if (msm_out) {
+    g1_to_std_aff(msm_out, &mA);
+    g1_to_std_aff(msm_out + 64, &mB1);
+    g2_to_std_aff(msm_out + 128, &mB2);
+    g1_to_std_aff(msm_out + 256, &mC);
+    g1_to_std_aff(msm_out + 320, &mH);
+  }
 
   /* assembly */
   fe r, sv;
@@ -558,6 +569,11 @@ int ref_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, co
   g2_to_std_aff(proof + 64, &pb);
   g1_to_std_aff(proof + 192, &pc);
   return 0;
+}
+
+int ref_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, const uint8_t* rs, uint8_t* proof,
+              int threads) {
+  return ref_prove_ex(zk, zlen, wt, wlen, rs, proof, threads, NULL, NULL);
 }
 
 /* stand-alone MSM for cross-checks: bases mont affine, scalars std -> std affine out */

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# The GPU tests run with bench.py's hardware-queue count (HIP reads it once, at its first call; the
+# GPU boxes export 4): proof slots of the batch prover then really overlap, so the tests exercise the
+# benchmarked concurrency (tests/test_gpu_metric.py).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "28")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd")
 for p in (ROOT, PKG_DIR):
