@@ -65,7 +65,8 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx);
  * enabled: 0 off, 1 on, 2 on + serialized (a proof's G2 and assembly work is put on its main
  * stream, so with one slot every kernel runs alone and its events time it in isolation). */
 int zkfl_ctx_set_profiling(zkfl_ctx* ctx, int enabled);
-/* name: "msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove".  Synchronises the device.
+/* name: "msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove", "witness" (full-prove
+ * slots).  Synchronises the device.
  * total_ms: summed event time; units: summed algorithmic units (MSM entries, NTT elements...);
  * median_ms (nullable): median single-launch time, robust to a one-off stalled dispatch. */
 int zkfl_ctx_profile(zkfl_ctx* ctx, const char* name, double* total_ms, uint64_t* launches, double* units,
@@ -144,6 +145,18 @@ int zkfl_witness_compute(zkfl_ctx* ctx, const zkfl_wprog* prog, size_t n, const 
 /* n witnesses computed straight into device-resident witnesses for `key` (no host round trip). */
 int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const zkfl_key* key, size_t n,
                                   const uint8_t* inputs, zkfl_witness** out);
+
+/* Full prove, pipelined (snarkjs `groth16.fullProve(input, wasm, zkey)` for a batch; the
+ * reference's per-client loop `generate_witness.cjs` + `groth16 prove`,
+ * tests/full_system_simulation.mjs:758-776 and :1298-1343).  Each proof slot computes its witness
+ * on its own stream straight into HBM and proves it on the same stream, so witness generation
+ * of one client overlaps the MSMs of the others; nothing returns to the host but the proof and
+ * the public signals.  inputs: n x n_inputs x 32 B std (zkfl_wprog_parse_inputs per input.json);
+ * rs: n x 64 B or NULL (CSPRNG); proofs_out: n x 256 B; pubs_out: n x nPublic x 32 B or NULL.
+ * A witness whose asserts fail gives ZKFL_E_CONSTRAINT naming the first such index (its proof
+ * bytes are zeroed, the others are valid); an input >= r gives ZKFL_E_ARG before any work. */
+int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                                  const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out);
 
 /* Verification (replaces `snarkjs groth16 verify <vkey> <public> <proof>`,
  * tests/full_system_simulation.mjs:865-868; snarkjs groth16_verify, restated in

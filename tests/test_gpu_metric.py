@@ -108,3 +108,56 @@ def test_metric_batch_verifies_on_gpu(metric, gpu_ctx):
     assert ok[3] is False and ok[4] is False and all(ok[:3]) and all(ok[5:])
     for r_ in res:
         r_.close()
+
+
+def test_metric_full_prove_pipeline(metric):
+    """zkfl_groth16_full_prove_batch: input vectors -> witness on each slot's stream -> proof, at
+    20 slots; equals witness-then-prove proof by proof (same r, s), public signals included."""
+    from zkfl import circuits, clients, native, wprog
+    _, _, key, wp, wts = metric
+    b = circuits.build("sgd_verified", *PARAMS)
+    objs = [clients.Client(cid, 128, 4, 7, clients.JsLcg(12345 + cid)).training_input(128, 1000, 100000000)[0]
+            for cid in (1, 2, 3, 4)]
+    import json
+    image = wprog.compile_program(b)
+    parsed = [native.parse_inputs(image, json.dumps(o)) for o in objs]
+    assert parsed == [wprog.input_bytes(b, o) for o in objs]
+    n = 24
+    rs = [_le(secrets.randbelow(R)) + _le(secrets.randbelow(R)) for _ in range(n)]
+    key.set_slots(20)
+    out = key.full_prove_batch(wp, [parsed[i % 4] for i in range(n)], b"".join(rs))
+    key.set_slots(3)
+    res = [key.upload(w) for w in wts]
+    for i, (proof, pub) in enumerate(out):
+        assert proof == key.prove_resident(res[i % 4], rs[i])
+        assert [str(x) for x in pub] == [objs[i % 4][k] for k in ("client_id", "round", "root_D", "root_G",
+                                                                    "root_W", "tauSquared")]
+    for r_ in res:
+        r_.close()
+
+
+def test_full_prove_constraint_failure_and_recovery(gpu_ctx):
+    """One unsatisfiable witness in a batch: ZKFL_E_CONSTRAINT names it; the key keeps working."""
+    from zkfl import circuits, clients, native, wprog, zkey
+    b = circuits.build("sgd_verified", 8, 4, 3, 1000)
+    zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
+    key = native.ProvingKey(gpu_ctx, zk)
+    wp = native.WitnessProgram(gpu_ctx, wprog.compile_program(b))
+    good = [clients.Client(c, 8, 4, 3, clients.JsLcg(12345 + c)).training_input(8, 1000, 100000000)[0]
+            for c in (1, 2, 3)]
+    bad = dict(good[1])
+    bad["remainder"] = list(bad["remainder"])
+    bad["remainder"][0] = str(int(bad["remainder"][0]) + 1)
+    key.set_slots(4)
+    with pytest.raises(native.ZkflError) as e:
+        key.full_prove_batch(wp, [wprog.input_bytes(b, x) for x in (good[0], good[2], bad, good[1], good[0])])
+    assert e.value.code == -7 and "witness 2" in str(e.value)
+    with pytest.raises(native.ZkflError) as e:          # input >= r: rejected before any work
+        key.full_prove_batch(wp, [b"\xff" * 32 + wprog.input_bytes(b, good[0])[32:]])
+    assert e.value.code == -1
+    rs = _le(5) + _le(6)
+    (p, pub), = key.full_prove_batch(wp, [wprog.input_bytes(b, good[0])], rs)
+    assert p == key.prove(wp.compute([wprog.input_bytes(b, good[0])])[0], rs)[0]
+    assert [str(x) for x in pub][:2] == [good[0]["client_id"], good[0]["round"]]
+    wp.close()
+    key.close()

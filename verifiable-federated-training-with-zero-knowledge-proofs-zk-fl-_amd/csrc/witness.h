@@ -29,4 +29,14 @@ int wprog_image_inputs_json(const uint8_t* img, size_t len, const char* json, st
 int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_host, hipStream_t st,
               std::string& err);
 
+// Host check that every input value is < r (the ZKFL_E_ARG case of wprog_run).
+bool wprog_inputs_ok(const WProg* p, size_t n, const uint8_t* inputs, std::string& err);
+
+// Asynchronous form for pipelines (the full-prove slots): m witnesses from device inputs d_in
+// (m x n_inputs x 8 u32 std) through the Montgomery scratch W (m x n_wires Fr) into d_outs[j]
+// (a device array of m device pointers); d_fail[j] ends as 0xFFFFFFFF or the index of the first
+// failed assert.  Nothing is synchronised; inputs must already be checked < r.
+hipError_t wprog_enqueue(const WProg* p, size_t m, const uint32_t* d_in, Fr* W, Fr* const* d_outs, uint32_t* d_fail,
+                         hipStream_t st);
+
 }  // namespace zkfl

@@ -617,15 +617,40 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
   return ZKFL_OK;
 }
 
-int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_host, hipStream_t st,
-              std::string& err) {
-  if (n == 0) return ZKFL_OK;
-  const uint32_t n_in = p->n_pub_in + p->n_prv_in, nw = p->n_wires;
+bool wprog_inputs_ok(const WProg* p, size_t n, const uint8_t* inputs, std::string& err) {
+  const uint32_t n_in = p->n_pub_in + p->n_prv_in;
   for (size_t i = 0; i < n * n_in; i++)
     if (!lt_r_host(reinterpret_cast<const uint32_t*>(inputs + 32 * i))) {
       err = "witness input " + std::to_string(i % n_in) + " of witness " + std::to_string(i / n_in) + " is not < r";
-      return ZKFL_E_ARG;
+      return false;
     }
+  return true;
+}
+
+hipError_t wprog_enqueue(const WProg* p, size_t m, const uint32_t* d_in, Fr* W, Fr* const* d_outs, uint32_t* d_fail,
+                         hipStream_t st) {
+  const uint32_t n_in = p->n_pub_in + p->n_prv_in, nw = p->n_wires;
+  hipError_t e = hipMemsetAsync(W, 0, m * (size_t)nw * 32, st);
+  if (e == hipSuccess) e = hipMemsetAsync(d_fail, 0xFF, m * 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_wit_inputs, dim3(zk_grid(m * (n_in + 1), 64)), dim3(64), 0, st, m, nw, p->in_first, n_in, d_in,
+                     W);
+  for (uint32_t L = 0; L < p->n_levels; L++) {
+    const uint32_t op0 = p->level_ptr[L], cnt = p->level_ptr[L + 1] - op0;
+    if (cnt) hipLaunchKernelGGL(k_wit_level, dim3(zk_grid(m * cnt, 64)), dim3(64), 0, st, p->view, m, op0, cnt, W);
+  }
+  if (p->n_asserts)
+    hipLaunchKernelGGL(k_wit_asserts, dim3(zk_grid(m * p->n_asserts, 64)), dim3(64), 0, st, p->view, m, p->n_asserts,
+                       (const Fr*)W, d_fail);
+  hipLaunchKernelGGL(k_wit_out, dim3(zk_grid(m * nw, 256)), dim3(256), 0, st, m, nw, (const Fr*)W, d_outs);
+  return hipGetLastError();
+}
+
+int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_host, hipStream_t st,
+              std::string& err) {
+  if (n == 0) return ZKFL_OK;
+  if (!wprog_inputs_ok(p, n, inputs, err)) return ZKFL_E_ARG;
+  const uint32_t n_in = p->n_pub_in + p->n_prv_in, nw = p->n_wires;
   // chunk so the Montgomery scratch stays bounded (M: 8.4 MB per witness)
   const size_t per = (size_t)nw * 32;
   size_t chunk = (size_t)(2048ull << 20) / (per ? per : 1);
@@ -642,24 +667,9 @@ int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_h
   int rc = ZKFL_OK;
   for (size_t off = 0; off < n && e == hipSuccess && rc == ZKFL_OK; off += chunk) {
     const size_t m = (n - off < chunk) ? n - off : chunk;
-    e = hipMemsetAsync(W, 0, m * per, st);
-    if (e == hipSuccess && n_in)
-      e = hipMemcpyAsync(d_in, inputs + off * n_in * 32, m * n_in * 32, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemsetAsync(d_fail, 0xFF, m * 4, st);
+    if (n_in) e = hipMemcpyAsync(d_in, inputs + off * n_in * 32, m * n_in * 32, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(d_outs, outs_host + off, m * sizeof(Fr*), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) break;
-    hipLaunchKernelGGL(k_wit_inputs, dim3(zk_grid(m * (n_in + 1), 64)), dim3(64), 0, st, m, nw, p->in_first, n_in,
-                       d_in, W);
-    for (uint32_t L = 0; L < p->n_levels; L++) {
-      const uint32_t op0 = p->level_ptr[L], cnt = p->level_ptr[L + 1] - op0;
-      if (cnt) hipLaunchKernelGGL(k_wit_level, dim3(zk_grid(m * cnt, 64)), dim3(64), 0, st, p->view, m, op0, cnt, W);
-    }
-    if (p->n_asserts)
-      hipLaunchKernelGGL(k_wit_asserts, dim3(zk_grid(m * p->n_asserts, 64)), dim3(64), 0, st, p->view, m,
-                         p->n_asserts, (const Fr*)W, d_fail);
-    hipLaunchKernelGGL(k_wit_out, dim3(zk_grid(m * nw, 256)), dim3(256), 0, st, m, nw, (const Fr*)W,
-                       (Fr* const*)d_outs);
-    e = hipGetLastError();
+    if (e == hipSuccess) e = wprog_enqueue(p, m, d_in, W, (Fr* const*)d_outs, d_fail, st);
     if (e == hipSuccess) e = hipMemcpyAsync(fails.data(), d_fail, m * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     for (size_t j = 0; e == hipSuccess && j < m; j++)

@@ -434,6 +434,16 @@ struct ProofSlot {
   uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128)
   bool busy = false;
   size_t out_index = 0;
+  // full-prove pipeline (zkfl_groth16_full_prove_batch): the witness engine runs on the slot's
+  // stream straight into wit_d, ahead of the proof that consumes it
+  bool full = false;           // the in-flight proof came from full-prove (check wit fail at wait)
+  size_t wit_n_in = 0, wit_n_wires = 0;
+  Fr* wit_W = nullptr;         // [n_wires] Montgomery scratch of the witness engine
+  Fr* wit_d = nullptr;         // [n_wires] std-form witness = the proof's scalars
+  uint32_t* wit_in = nullptr;  // [n_inputs x 8]
+  uint32_t* wit_fail = nullptr;
+  Fr** wit_outs = nullptr;     // [1] = wit_d
+  uint8_t* wit_pinned = nullptr;  // fail flag (16) | public signals (nPub x 32) | inputs (n_in x 32)
 };
 
 struct zkfl_key {
@@ -474,10 +484,12 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->extra, s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
+  void* ptrs[] = {s->extra, s->abc,    s->abc_head, s->abc_tail, s->h,        s->res,     s->resB2,
+                  s->d_rs,  s->d_proof, s->wit_W,    s->wit_d,    s->wit_in,   s->wit_fail, s->wit_outs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
+  if (s->wit_pinned) (void)hipHostFree(s->wit_pinned);
   for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2})
@@ -643,6 +655,65 @@ int wait_slot(ProofSlot* s, uint8_t* proof_out) {
   HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
   if (proof_out) memcpy(proof_out, s->pinned, 256);
   s->busy = false;
+  return ZKFL_OK;
+}
+
+// Witness buffers of a slot for the full-prove pipeline (allocated on first use, kept).
+hipError_t slot_witness_buffers(const zkfl_key* k, ProofSlot* s, size_t n_in) {
+  if (s->wit_d && s->wit_n_in == n_in && s->wit_n_wires == k->nVars) return hipSuccess;
+  for (void* p : {(void*)s->wit_W, (void*)s->wit_d, (void*)s->wit_in, (void*)s->wit_fail, (void*)s->wit_outs})
+    if (p) (void)hipFree(p);
+  if (s->wit_pinned) (void)hipHostFree(s->wit_pinned);
+  s->wit_W = s->wit_d = nullptr;
+  s->wit_in = s->wit_fail = nullptr;
+  s->wit_outs = nullptr;
+  s->wit_pinned = nullptr;
+  s->wit_n_in = s->wit_n_wires = 0;
+  const size_t nw = k->nVars;
+  ZK_CHECK(hipMalloc(&s->wit_W, nw * 32));
+  ZK_CHECK(hipMalloc(&s->wit_d, nw * 32));
+  ZK_CHECK(hipMalloc(&s->wit_in, n_in * 32 + 16));
+  ZK_CHECK(hipMalloc(&s->wit_fail, 16));
+  ZK_CHECK(hipMalloc(&s->wit_outs, sizeof(Fr*)));
+  ZK_CHECK(hipHostMalloc(&s->wit_pinned, 16 + (size_t)k->nPub * 32 + n_in * 32));
+  ZK_CHECK(hipMemcpy(s->wit_outs, &s->wit_d, sizeof(Fr*), hipMemcpyHostToDevice));
+  s->wit_n_in = n_in;
+  s->wit_n_wires = nw;
+  return hipSuccess;
+}
+
+// input vector -> witness (slot stream) -> public signals + fail flag D2H -> proof (same stream)
+int enqueue_full_proof(zkfl_ctx* ctx, zkfl_key* k, const WProg* prog, ProofSlot* s, const uint8_t* input,
+                       size_t n_in, const uint32_t rs_host[16]) {
+  HIP_TRY(slot_witness_buffers(k, s, n_in), "full-prove witness buffers");
+  hipStream_t st = s->st_main;
+  uint8_t* pin_fail = s->wit_pinned;
+  uint8_t* pin_pub = s->wit_pinned + 16;
+  uint8_t* pin_in = pin_pub + (size_t)k->nPub * 32;
+  memcpy(pin_in, input, n_in * 32);
+  int pw = ctx->prof.begin("witness", st);
+  if (n_in) HIP_TRY(hipMemcpyAsync(s->wit_in, pin_in, n_in * 32, hipMemcpyHostToDevice, st), "upload inputs");
+  HIP_TRY(wprog_enqueue(prog, 1, s->wit_in, s->wit_W, s->wit_outs, s->wit_fail, st), "witness");
+  ctx->prof.end(pw, st, 1.0);
+  HIP_TRY(hipMemcpyAsync(pin_fail, s->wit_fail, 4, hipMemcpyDeviceToHost, st), "witness status");
+  if (k->nPub)
+    HIP_TRY(hipMemcpyAsync(pin_pub, s->wit_d + 1, (size_t)k->nPub * 32, hipMemcpyDeviceToHost, st), "public signals");
+  int rc = enqueue_proof(ctx, k, s, s->wit_d, rs_host, 0);
+  s->full = true;
+  return rc;
+}
+
+// Wait for a full-prove slot: proof and public signals out; *failed_assert = the witness's first
+// failed assert (0xFFFFFFFF: none), in which case the proof bytes are zeroed.
+int wait_full_slot(const zkfl_key* k, ProofSlot* s, uint8_t* proof_out, uint8_t* pub_out, uint32_t* failed_assert) {
+  int rc = wait_slot(s, proof_out);
+  s->full = false;
+  if (rc) return rc;
+  uint32_t f;
+  memcpy(&f, s->wit_pinned, 4);
+  *failed_assert = f;
+  if (f != 0xFFFFFFFFu && proof_out) memset(proof_out, 0, 256);
+  if (pub_out && k->nPub) memcpy(pub_out, s->wit_pinned + 16, (size_t)k->nPub * 32);
   return ZKFL_OK;
 }
 
@@ -1136,6 +1207,7 @@ int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_
     }
     rc = enqueue_proof(ctx, key, s, w[i]->d, rsl, 0);
     if (rc) break;
+    s->full = false;
     s->busy = true;
     s->out_index = i;
   }
@@ -1145,6 +1217,60 @@ int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_
       if (rc == ZKFL_OK) rc = r2;
     }
   }
+  return rc;
+}
+
+int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                                  const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
+  if (!ctx || !key || !prog || (n && (!inputs || !proofs_out))) return fail(ZKFL_E_ARG, "full_prove: null argument");
+  uint32_t nw = 0, n_in32 = 0, npub = 0;
+  wprog_info(prog->p, &nw, &n_in32, &npub);
+  if (nw != key->nVars || npub != key->nPub)
+    return fail(ZKFL_E_MISMATCH, "witness program does not match the proving key (nVars / nPublic)");
+  const size_t n_in = n_in32;
+  {
+    std::string err;
+    if (!wprog_inputs_ok(prog->p, n, inputs, err)) return fail(ZKFL_E_ARG, err);
+  }
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  int rc = ZKFL_OK;
+  size_t bad_index = SIZE_MAX;
+  uint32_t bad_assert = 0;
+  auto drain = [&](ProofSlot* s) {
+    uint32_t f = 0xFFFFFFFFu;
+    int r2 = wait_full_slot(key, s, proofs_out + 256 * s->out_index,
+                            pubs_out ? pubs_out + (size_t)key->nPub * 32 * s->out_index : nullptr, &f);
+    if (r2 == ZKFL_OK && f != 0xFFFFFFFFu && s->out_index < bad_index) {
+      bad_index = s->out_index;
+      bad_assert = f;
+    }
+    return r2;
+  };
+  for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
+    uint32_t rsl[16];
+    rc = get_rs(rs ? rs + 64 * i : nullptr, rsl);
+    if (rc) break;
+    ProofSlot* s = nullptr;
+    rc = get_slot(key, i, &s);
+    if (rc) break;
+    if (s->busy) {
+      rc = s->full ? drain(s) : wait_slot(s, nullptr);
+      if (rc) break;
+    }
+    rc = enqueue_full_proof(ctx, key, prog->p, s, inputs + i * n_in * 32, n_in, rsl);
+    if (rc) break;
+    s->busy = true;
+    s->out_index = i;
+  }
+  for (ProofSlot* s : key->slots) {
+    if (s->busy) {
+      int r2 = s->full ? drain(s) : wait_slot(s, nullptr);
+      if (rc == ZKFL_OK) rc = r2;
+    }
+  }
+  if (rc == ZKFL_OK && bad_index != SIZE_MAX)
+    rc = fail(ZKFL_E_CONSTRAINT, "witness " + std::to_string(bad_index) + ": assert constraint #" +
+                                     std::to_string(bad_assert) + " failed (inputs do not satisfy the circuit)");
   return rc;
 }
 

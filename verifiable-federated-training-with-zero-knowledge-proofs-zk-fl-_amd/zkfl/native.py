@@ -65,6 +65,7 @@ SIGNATURES = {
     "zkfl_wprog_parse_inputs": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, _U8P, C.c_size_t,
                                           C.POINTER(C.c_size_t)]),
     "zkfl_witness_compute_json": (C.c_int, [_P, _P, C.c_char_p, _U8P]),
+    "zkfl_groth16_full_prove_batch": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P, _U8P]),
 }
 
 
@@ -255,6 +256,20 @@ class ProvingKey:
         ob = bytes(out)
         return [ob[256 * i:256 * i + 256] for i in range(n)]
 
+    def full_prove_batch(self, prog: "WitnessProgram", inputs, rs: bytes | None = None):
+        """input vectors (wprog.input_bytes / parse_inputs) -> [(proof 256 B, [public ints])]:
+        witness and proof pipelined per slot on the GPU (zkfl_groth16_full_prove_batch)."""
+        n = len(inputs)
+        buf = prog._inputs(inputs)
+        out = _buf(256 * max(1, n))
+        pubs = _buf(32 * max(1, self.n_public) * max(1, n))
+        check(lib().zkfl_groth16_full_prove_batch(self.ctx.h, self.h, prog.h, n, buf, rs, out, pubs))
+        ob, pb = bytes(out), bytes(pubs)
+        k = self.n_public
+        return [(ob[256 * i:256 * i + 256],
+                 [int.from_bytes(pb[32 * (i * k + j):32 * (i * k + j) + 32], "little") for j in range(k)])
+                for i in range(n)]
+
     def debug_parts(self, wtns: bytes):
         """-> (h list of ints, dict of MSM results as std affine bytes)"""
         h = _buf(32 * self.domain_size)
@@ -287,8 +302,11 @@ class ResidentWitness:
             pass
 
 
-def parse_inputs(image: bytes, input_json: str, cap: int = 1 << 20) -> bytes:
-    """circom input.json -> flattened input vector via the program's signal table (host only)."""
+def parse_inputs(image: bytes, input_json: str, cap: int | None = None) -> bytes:
+    """circom input.json -> flattened input vector via the program's signal table (host only).
+    cap: room for this many values (default: the image's input count, header word 4 + 5)."""
+    if cap is None:
+        cap = max(1, int.from_bytes(image[16:20], "little") + int.from_bytes(image[20:24], "little"))
     out = _buf(32 * cap)
     n = C.c_size_t()
     check(lib().zkfl_wprog_parse_inputs(image, len(image), input_json.encode(), out, cap, C.byref(n)))
