@@ -92,29 +92,13 @@ def draw_rs(n):
 def timed_run(key, warm_w, steps_w, rs, ctx, dist):
     """W untimed steps, then exactly K timed steps (K x slots proofs in one batch call) bracketed
     by barrier + synchronize on both sides; returns (max-over-ranks elapsed seconds, proofs)."""
-
-    def barrier_sync():
-        ctx.synchronize()
-        if dist is not None:
-            import torch
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            dist.barrier()
-
     if warm_w:
         key.prove_batch(warm_w)
-    barrier_sync()
+    _barrier(ctx, dist)
     t_start = time.perf_counter()
     proofs = key.prove_batch(steps_w, rs)      # K steps x `slots` proofs, `slots` in flight
-    barrier_sync()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        import torch
-        dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed, proofs
+    _barrier(ctx, dist)
+    return _max_over_ranks(time.perf_counter() - t_start, dist), proofs
 
 
 def verify_all(ctx, zk, proofs, pubs_of):
@@ -127,19 +111,22 @@ def verify_all(ctx, zk, proofs, pubs_of):
     return sum(ok)
 
 
-def end_to_end_leg(key, wp, image, json_inputs, slots, steps):
+def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist):
     """input.json text -> proofs: the C parser (zkfl_wprog_parse_inputs) on the host, then
     zkfl_groth16_full_prove_batch (each slot computes its client's witness on its own stream
-    straight into HBM and proves it there); `steps` x `slots` proofs, host-timed."""
+    straight into HBM and proves it there); `steps` x `slots` proofs per rank, max-over-ranks time."""
     from zkfl import native
     n = steps * slots
     texts = [json_inputs[i % len(json_inputs)] for i in range(n)]
     key.full_prove_batch(wp, [native.parse_inputs(image, t) for t in texts[:slots]])   # warm slot buffers
+    _barrier(ctx, dist)
     t0 = time.perf_counter()
     out = key.full_prove_batch(wp, [native.parse_inputs(image, t) for t in texts])
-    dt = time.perf_counter() - t0
+    _barrier(ctx, dist)
+    dt = _max_over_ranks(time.perf_counter() - t0, dist)
     assert len(out) == n
-    return {"value": round(n / dt, 3), "unit": "proofs/s", "proofs": n,
+    world = dist.get_world_size() if dist is not None else 1
+    return {"value": round(world * n / dt, 3), "unit": "proofs/s", "proofs": world * n,
             "path": "input.json -> C parse (host) -> GPU witness on the slot stream -> GPU proof "
                     "(zkfl_groth16_full_prove_batch)"}
 
@@ -202,6 +189,101 @@ def roofline(prof, key):
                      "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (128 mad x 2.2 + 128 addc x 1.8)"}}
 
 
+def c5_leg(ctx, rank, world, rounds, slots, dist):
+    """BASELINE config 5: `rounds` federated rounds of 8 clients x {training sgd_verified(8,4,3),
+    secure aggregation SecureMaskedUpdate(4,7)} (tests/full_system_simulation.mjs:1278-1343), both
+    keys resident.  Global proof k -> GPU k mod G; each rank pushes its share,
+    input.json text -> C parse -> GPU witness -> proof, through zkfl_groth16_full_prove_multi (the
+    two circuits' proofs interleaved on the device).  Total work is fixed: strong scaling.
+    Every proof is GPU-verified afterwards.  -> report dict (rank 0)."""
+    from zkfl import circuits, clients, groth16, native, wprog, zkey
+    t0 = time.perf_counter()
+    circ = {"train": circuits.build("sgd_verified", 8, 4, 3, 1000), "secagg": circuits.build("secure_masked_update", 4, 7)}
+    keys, progs, images, vks = {}, {}, {}, {}
+    for i, (nm, b) in enumerate(circ.items()):
+        zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0xC5 + i, alpha=3, beta=5, gamma=7, delta=11 + i))
+        keys[nm] = native.ProvingKey(ctx, zk)
+        keys[nm].set_slots(slots)
+        images[nm] = wprog.compile_program(b)
+        progs[nm] = native.WitnessProgram(ctx, images[nm])
+        vks[nm] = groth16.vk_bytes(groth16.export_verification_key(zk, alphabeta=False))
+    jobs = []          # (circuit, input.json text) in the reference's order: per client training, secagg
+    for r in range(rounds + 1):                        # round 0 = warm-up
+        for tr, sa, _ in clients.federated_round(8, rnd=r + 1):
+            jobs += [(r, "train", json.dumps(tr)), (r, "secagg", json.dumps(sa))]
+    mine = [j for k, j in enumerate([j for j in jobs if j[0] > 0]) if k % world == rank]
+    warm = [j for k, j in enumerate([j for j in jobs if j[0] == 0]) if k % world == rank]
+    log(f"[bench r{rank}] c5: keys for {[(nm, b.n_constraints) for nm, b in circ.items()]}, "
+        f"{len(mine)} of {rounds * 16} proofs on this rank ({time.perf_counter() - t0:.1f} s)")
+
+    def run(js):
+        return ctx.full_prove_multi([(keys[nm], progs[nm], native.parse_inputs(images[nm], txt)) for _, nm, txt in js])
+
+    run(warm)
+    _barrier(ctx, dist)
+    t_start = time.perf_counter()
+    out = run(mine)
+    _barrier(ctx, dist)
+    elapsed = _max_over_ranks(time.perf_counter() - t_start, dist)
+    ok = 0
+    for nm in keys:
+        sel = [o for (_, n2, _), o in zip(mine, out) if n2 == nm]
+        if sel:
+            pubs = b"".join(x.to_bytes(32, "little") for _, pub in sel for x in pub)
+            ok += sum(ctx.verify_batch(vks[nm], pubs, b"".join(p for p, _ in sel), keys[nm].n_public))
+    ok = _sum_over_ranks(ok, dist)
+    for x in list(progs.values()) + list(keys.values()):
+        x.close()
+    if ok != rounds * 16:
+        raise SystemExit(f"[bench r{rank}] c5: {rounds * 16 - ok} proofs do not verify")
+    return {"value": round(rounds * 16 / elapsed, 3), "unit": "proofs/s", "proofs": rounds * 16, "verified": ok,
+            "rounds": rounds, "ms_per_round": round(elapsed / rounds * 1e3, 3), "scaling": "strong",
+            "workload": "8 clients x {sgd_verified(8,4,3,1000) training, SecureMaskedUpdate(4,7) secagg} per "
+                        "round, proof k -> GPU k mod G, input.json -> C parse -> GPU witness -> proof "
+                        "(zkfl_groth16_full_prove_multi, both keys resident)",
+            "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
+
+
+def _barrier(ctx, dist):
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+
+
+def _max_over_ranks(x, dist):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum_over_ranks(x, dist):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def report(args, world, elapsed, n_timed_all, verified_all, prof, nprof, key, config, extra):
+    """The bench JSON line (rank 0).  `extra`: roofline / end_to_end / c5 / cpu_baseline fields."""
+    stage_ms = {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()}  # median x launches
+    line = {
+        "metric": METRIC, "value": round(n_timed_all / elapsed, 4), "unit": "proofs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (reference harness seeded client generator)",
+        "config": config, "proofs_timed": n_timed_all, "verified": verified_all,
+        "roofline": roofline(prof, key) if key is not None else None,
+        "stage_ms_isolated_per_proof": stage_ms,
+    }
+    line.update(extra)
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,22 +294,25 @@ def main():
     ap.add_argument("--slots", type=int, default=20, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     ap.add_argument("--e2e-steps", type=int, default=8, help="steps of the input.json -> proof leg (0: skip)")
+    ap.add_argument("--c5-rounds", type=int, default=8, help="federated rounds of the config-5 leg (0: skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    from zkfl import circuits, clients, native, wprog, zkey
+    # libzkfl (and with it /opt/rocm's HIP runtime) is loaded before torch, whose wheel carries its
+    # own libamdhip64 under the same soname: one HIP runtime per process.  torch.distributed is the
+    # control plane only (barrier, max-over-ranks time, counts) over gloo; the proofs of different
+    # ranks are independent, there is no collective on the data path.
+    native.lib()
+    n_dev = native.device_count()
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist_mod
         dist = dist_mod
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend=backend)
-
-    from zkfl import circuits, clients, native, wprog, zkey
+        dist.init_process_group(backend="gloo")
+    device = local_rank % max(1, n_dev)     # ranks beyond the device count share devices (tests)
 
     name, params = CIRCUITS[args.circuit]
     t0 = time.perf_counter()
@@ -239,9 +324,9 @@ def main():
         input_objs.append(client.training_input(batch, precision, 100000000)[0])
     inputs = [wprog.input_bytes(b, x) for x in input_objs]
     log(f"[bench r{rank}] circuit {name}{params}: {b.n_constraints} constraints, {b.n_wires} wires "
-        f"({time.perf_counter() - t0:.1f} s)")
+        f"({time.perf_counter() - t0:.1f} s); device {device} of {n_dev}")
 
-    ctx = native.Context(local_rank)
+    ctx = native.Context(device)
     t0 = time.perf_counter()
     zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
     log(f"[bench r{rank}] dev setup {len(zk) / 1e6:.0f} MB zkey ({time.perf_counter() - t0:.1f} s)")
@@ -265,14 +350,23 @@ def main():
     pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]   # wtns v2: header 76 B, wire 0 = 1
     verified = verify_all(ctx, zk, proofs, lambda i: pubs[i % len(pubs)])
     log(f"[bench r{rank}] {n_timed} proofs in {elapsed:.3f} s; GPU batch verifier: {verified}/{n_timed} valid")
-    if verified != n_timed:
-        raise SystemExit(f"[bench r{rank}] {n_timed - verified} timed proofs do not verify")
+    verified_all = _sum_over_ranks(verified, dist)
+    if verified_all != n_timed * world:
+        raise SystemExit(f"[bench r{rank}] {n_timed * world - verified_all} timed proofs do not verify")
     prof, nprof = roofline_pass(key, ctx, res, args.slots)
     e2e = None
     if args.e2e_steps:
         e2e = end_to_end_leg(key, wp, wprog.compile_program(b), [json.dumps(x) for x in input_objs], args.slots,
-                             args.e2e_steps)
+                             args.e2e_steps, ctx, dist)
         log(f"[bench r{rank}] end to end: {e2e}")
+    for r_ in res:
+        r_.close()
+    wp.close()
+    key.set_slots(1)
+    c5 = None
+    if args.c5_rounds:
+        c5 = c5_leg(ctx, rank, world, args.c5_rounds, min(args.slots, 8), dist)
+        log(f"[bench r{rank}] config 5: {c5}")
     if rank == 0:
         cpu, oracle_match = None, None
         if world == 1 and not args.no_cpu_baseline:
@@ -288,22 +382,11 @@ def main():
                   "global_batch": args.slots * world, "step": f"{args.slots} proofs per GPU (one per slot)",
                   "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}
-        stage_ms = {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()}  # median x launches
-        line = {
-            "metric": METRIC, "value": round(world * n_timed / elapsed, 4), "unit": "proofs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (reference harness seeded client generator)",
-            "config": config, "proofs_timed": n_timed * world, "verified": verified * world,
-            "oracle_match": oracle_match, "roofline": roofline(prof, key),
-            "stage_ms_isolated_per_proof": stage_ms, "end_to_end": e2e, "cpu_baseline": cpu,
-        }
+        line = report(args, world, elapsed, n_timed * world, verified_all, prof, nprof, key, config,
+                      {"oracle_match": oracle_match, "end_to_end": e2e, "c5": c5, "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")
-    for r_ in res:
-        r_.close()
-    wp.close()
     key.close()
     ctx.close()
     if dist is not None:

@@ -101,6 +101,17 @@ int zkfl_groth16_prove_resident(zkfl_ctx* ctx, zkfl_key* key, const zkfl_witness
 int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
                              const uint8_t* rs, uint8_t* proofs_out);
 
+/* Multi-key batch: proof i uses keys[i] and witness w[i] (uploaded for keys[i]); rs: n x 64 B or
+ * NULL; proofs_out: n x 256 B.  Replaces the reference's per-round loop that proves each client's
+ * training update and then its secure-aggregation update with two different zkeys
+ * (tests/full_system_simulation.mjs:1298-1343: `trainAndGenerateProof` -> groth16 prove of
+ * sgd_verified_final.zkey, :773-776; `generateSecureAggregationProof` -> groth16 prove of the
+ * secure_masked_update zkey, :1040-1107).  Every key keeps its own proof slots resident; the jobs
+ * are issued in order, each on the next slot of its key, so proofs of different circuits
+ * overlap on the device. */
+int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_witness* const* w,
+                             const uint8_t* rs, uint8_t* proofs_out);
+
 /* Parity hooks: the deterministic core of one proof.
  * h_out: domain_size x 32 B std (coset evaluations a*b-c, the H-MSM scalars) or NULL;
  * msm_out: A (64) | B1 (64) | B2 (128) | C (64) | H (64) std affine MSM results over the
@@ -157,6 +168,13 @@ int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const z
  * bytes are zeroed, the others are valid); an input >= r gives ZKFL_E_ARG before any work. */
 int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
                                   const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out);
+
+/* Multi-key full prove: job i = (keys[i], progs[i], inputs[i] = that program's input vector);
+ * pubs_out[i] (or pubs_out NULL) receives keys[i]'s nPublic x 32 B.  Same error behaviour as
+ * zkfl_groth16_full_prove_batch; the witness index in a ZKFL_E_CONSTRAINT message is the job index. */
+int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,
+                                  const uint8_t* const* inputs, const uint8_t* rs, uint8_t* proofs_out,
+                                  uint8_t* const* pubs_out);
 
 /* Verification (replaces `snarkjs groth16 verify <vkey> <public> <proof>`,
  * tests/full_system_simulation.mjs:865-868; snarkjs groth16_verify, restated in

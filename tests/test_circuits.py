@@ -150,3 +150,33 @@ def test_metric_circuit_size():
     b = circuits.build("sgd_verified", 128, 4, 7, 1000)
     assert 2 ** 17 < b.n_constraints < 2 ** 18
     assert domain_size_for(b) == 2 ** 18
+
+
+def test_sparse_merkle_tree_equals_padded_tree():
+    """clients.MerkleTree keeps the Poseidon([0]) padding implicit; every node and proof equals the
+    reference's fully padded tree (oracle build_merkle_tree, tests/full_system_simulation.mjs:198-238)."""
+    leaves = [op.vector_hash([i, 2 * i, 3, 4, i % 2]) for i in range(11)]
+    for depth in (4, 5):
+        full = op.build_merkle_tree(leaves, depth)
+        t = clients.merkle_tree(leaves, depth)
+        assert t.root == full[-1][0]
+        for lvl in range(depth + 1):
+            assert [t.node(lvl, j) for j in range(len(full[lvl]))] == full[lvl]
+        for idx in (0, 5, 10):
+            assert clients.merkle_proof(t, idx, depth) == op.merkle_proof(full, idx, depth)
+
+
+def test_federated_round_inputs_satisfy_circuits():
+    """BASELINE config 5 inputs: 8 clients' training and SecureMaskedUpdate(4,7) inputs satisfy their
+    circuits and the 8-way pairwise masks cancel (tests/full_system_simulation.mjs:1278-1343)."""
+    rnd = clients.federated_round(8)
+    sa = circuits.build("secure_masked_update", 4, 7)
+    tr = circuits.build("sgd_verified", 8, 4, 3, 1000)
+    total = [0] * 4
+    for k, (t, s, g) in enumerate(rnd):
+        if k in (0, 7):
+            assert tr.check_all(ow.evaluate(tr, t))
+            assert sa.check_all(ow.evaluate(sa, s))
+        assert s["root_G"] == t["root_G"] and len(s["peer_ids"]) == 7
+        total = [(a + int(m)) % R for a, m in zip(total, s["masked_update"])]
+    assert total == [sum(g[k] for _, _, g in rnd) % R for k in range(4)]

@@ -1,6 +1,7 @@
-"""bench.py's N>1 path (barrier, max-over-ranks timing, weak-scaling value, rank-0 report) on
-2 gloo ranks with a stub prover (CPU).  The GPU prover itself is covered by -m gpu tests; the
-multi-GPU path has no data-path collective (independent proofs per rank)."""
+"""bench.py's N>1 control plane (barrier, max-over-ranks timing, summed verification counts, weak-scaling
+value, rank-0 report) on 2 gloo ranks with a stub prover (CPU).  The same path driving the real
+prover on the GPU is tests/test_gpu_multirank.py; there is no data-path collective (independent
+proofs per rank)."""
 import json
 import os
 import socket
@@ -18,7 +19,7 @@ class _StubKey:
     def __init__(self, rank):
         self.rank = rank
 
-    def prove_batch(self, ws):
+    def prove_batch(self, ws, rs=None):
         time.sleep(0.01 * (1 + self.rank) * len(ws))
         return [bytes(256)] * len(ws)
 
@@ -44,13 +45,14 @@ def _worker(rank, world, port, out_path):
     import bench
     dist.init_process_group("gloo", rank=rank, world_size=world)
     key = _StubKey(rank)
-    elapsed, proofs = bench.timed_run(key, [0], list(range(8)), _StubCtx(), dist)
+    elapsed, proofs = bench.timed_run(key, [0], list(range(8)), None, _StubCtx(), dist)
+    verified = bench._sum_over_ranks(len(proofs), dist)
     prof = {k: (0.0, 0, 0.0, 0.0) for k in bench.PROFILED}
 
     class A:
         steps, warmup, slots = 8, 1, 1
     if rank == 0:
-        rep = bench.report(A, world, elapsed, prof, {"workload": "stub"}, None)
+        rep = bench.report(A, world, elapsed, 8 * world, verified, prof, 1, None, {"workload": "stub"}, {})
         with open(out_path, "w") as f:
             json.dump(rep, f)
     dist.destroy_process_group()
@@ -74,4 +76,4 @@ def test_two_rank_gloo_report(tmp_path):
     assert rep["n_gpus"] == 2 and rep["steps"] == 8 and rep["scaling"] == "weak"
     assert rep["ms_per_step"] >= 8 * 20 / 8 * 0.9
     assert abs(rep["value"] - 2 * 8 / (rep["ms_per_step"] * 8 / 1e3)) < 1e-3 * rep["value"] + 1e-6
-    assert rep["metric"].startswith("Groth16 proofs/sec")
+    assert rep["metric"].startswith("Groth16 proofs/sec") and rep["verified"] == 16

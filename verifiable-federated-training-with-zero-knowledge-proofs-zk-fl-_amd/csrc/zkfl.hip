@@ -433,7 +433,9 @@ struct ProofSlot {
   uint32_t* d_proof = nullptr;  // [64]
   uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128)
   bool busy = false;
-  size_t out_index = 0;
+  size_t job = 0;                 // index of the in-flight proof in its batch
+  uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
+  uint8_t* out_pub = nullptr;     // full-prove: where its public signals go (nullable)
   // full-prove pipeline (zkfl_groth16_full_prove_batch): the witness engine runs on the slot's
   // stream straight into wit_d, ahead of the proof that consumes it
   bool full = false;           // the in-flight proof came from full-prove (check wit fail at wait)
@@ -651,9 +653,9 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   return ZKFL_OK;
 }
 
-int wait_slot(ProofSlot* s, uint8_t* proof_out) {
+int wait_slot(ProofSlot* s) {
   HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
-  if (proof_out) memcpy(proof_out, s->pinned, 256);
+  if (s->out_proof) memcpy(s->out_proof, s->pinned, 256);
   s->busy = false;
   return ZKFL_OK;
 }
@@ -705,16 +707,91 @@ int enqueue_full_proof(zkfl_ctx* ctx, zkfl_key* k, const WProg* prog, ProofSlot*
 
 // Wait for a full-prove slot: proof and public signals out; *failed_assert = the witness's first
 // failed assert (0xFFFFFFFF: none), in which case the proof bytes are zeroed.
-int wait_full_slot(const zkfl_key* k, ProofSlot* s, uint8_t* proof_out, uint8_t* pub_out, uint32_t* failed_assert) {
-  int rc = wait_slot(s, proof_out);
+int wait_full_slot(const zkfl_key* k, ProofSlot* s, uint32_t* failed_assert) {
+  int rc = wait_slot(s);
   s->full = false;
   if (rc) return rc;
   uint32_t f;
   memcpy(&f, s->wit_pinned, 4);
   *failed_assert = f;
-  if (f != 0xFFFFFFFFu && proof_out) memset(proof_out, 0, 256);
-  if (pub_out && k->nPub) memcpy(pub_out, s->wit_pinned + 16, (size_t)k->nPub * 32);
+  if (f != 0xFFFFFFFFu && s->out_proof) memset(s->out_proof, 0, 256);
+  if (s->out_pub && k->nPub) memcpy(s->out_pub, s->wit_pinned + 16, (size_t)k->nPub * 32);
   return ZKFL_OK;
+}
+
+// One proof of a batch.  Either a device-resident witness (w) or a witness-program input vector
+// (prog + input: the full-prove pipeline).  Jobs of one batch may use different keys.
+struct Job {
+  zkfl_key* key = nullptr;
+  const Fr* w = nullptr;
+  const WProg* prog = nullptr;
+  const uint8_t* input = nullptr;
+  size_t n_in = 0;
+  const uint8_t* rs = nullptr;  // 64 B or nullptr (CSPRNG)
+  uint8_t* proof_out = nullptr;
+  uint8_t* pub_out = nullptr;
+};
+
+// The batch scheduler behind every prove entry point: job i goes to the next slot of its key
+// (round robin per key), a busy slot is drained first, so up to max_slots proofs per key are in
+// flight and proofs of different keys (e.g. the training and secure-aggregation circuits of one
+// federated round) overlap on the device.  job(i, Job&) fills the i-th job.
+template <class GetJob>
+int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  std::vector<std::pair<zkfl_key*, size_t>> cursor;  // per key: proofs issued in this batch
+  int rc = ZKFL_OK;
+  size_t bad_index = SIZE_MAX;
+  uint32_t bad_assert = 0;
+  auto drain = [&](zkfl_key* k, ProofSlot* s) {
+    if (!s->full) return wait_slot(s);
+    uint32_t f = 0xFFFFFFFFu;
+    int r2 = wait_full_slot(k, s, &f);
+    if (r2 == ZKFL_OK && f != 0xFFFFFFFFu && s->job < bad_index) {
+      bad_index = s->job;
+      bad_assert = f;
+    }
+    return r2;
+  };
+  for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
+    Job J;
+    rc = job(i, J);
+    if (rc) break;
+    uint32_t rsl[16];
+    rc = get_rs(J.rs, rsl);
+    if (rc) break;
+    size_t c = 0;
+    while (c < cursor.size() && cursor[c].first != J.key) c++;
+    if (c == cursor.size()) cursor.push_back({J.key, 0});
+    ProofSlot* s = nullptr;
+    rc = get_slot(J.key, cursor[c].second++, &s);
+    if (rc) break;
+    if (s->busy) {
+      rc = drain(J.key, s);
+      if (rc) break;
+    }
+    s->job = i;
+    s->out_proof = J.proof_out;
+    s->out_pub = J.pub_out;
+    if (J.prog) {
+      rc = enqueue_full_proof(ctx, J.key, J.prog, s, J.input, J.n_in, rsl);
+    } else {
+      rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
+      s->full = false;
+    }
+    if (rc) break;
+    s->busy = true;
+  }
+  for (auto& kc : cursor)
+    for (ProofSlot* s : kc.first->slots)
+      if (s->busy) {
+        int r2 = drain(kc.first, s);
+        if (rc == ZKFL_OK) rc = r2;
+      }
+  if (rc == ZKFL_OK && bad_index != SIZE_MAX)
+    rc = fail(ZKFL_E_CONSTRAINT, "witness " + std::to_string(bad_index) + ": assert constraint #" +
+                                     std::to_string(bad_assert) + " failed (inputs do not satisfy the circuit)");
+  return rc;
 }
 
 hipError_t msm_run_any(const MsmBases<FqOps>& b, MsmScratch<FqOps>& s, MsmTail<FqOps>& t, const uint32_t* sc,
@@ -913,7 +990,8 @@ int zkfl_ctx_profile_reset(zkfl_ctx* ctx) {
 
 int zkfl_ctx_synchronize(zkfl_ctx* ctx) {
   if (!ctx) return fail(ZKFL_E_ARG, "null ctx");
-  HIP_TRY(hipStreamSynchronize(ctx->st), "sync");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "sync");  // every stream of this process: the proof slots' too
   return ZKFL_OK;
 }
 
@@ -1189,89 +1267,85 @@ int zkfl_key_set_slots(zkfl_key* key, int slots) {
 int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
                              const uint8_t* rs, uint8_t* proofs_out) {
   if (!ctx || !key || (!w && n) || (!proofs_out && n)) return fail(ZKFL_E_ARG, "null argument");
-  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   for (size_t i = 0; i < n; i++) {
     if (!w[i] || w[i]->key != key) return fail(ZKFL_E_MISMATCH, "witness uploaded for another key");
   }
-  int rc = ZKFL_OK;
-  for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
-    uint32_t rsl[16];
-    rc = get_rs(rs ? rs + 64 * i : nullptr, rsl);
-    if (rc) break;
-    ProofSlot* s = nullptr;
-    rc = get_slot(key, i, &s);
-    if (rc) break;
-    if (s->busy) {
-      rc = wait_slot(s, proofs_out + 256 * s->out_index);
-      if (rc) break;
-    }
-    rc = enqueue_proof(ctx, key, s, w[i]->d, rsl, 0);
-    if (rc) break;
-    s->full = false;
-    s->busy = true;
-    s->out_index = i;
-  }
-  for (ProofSlot* s : key->slots) {
-    if (s->busy) {
-      int r2 = wait_slot(s, proofs_out + 256 * s->out_index);
-      if (rc == ZKFL_OK) rc = r2;
-    }
-  }
-  return rc;
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    J.key = key;
+    J.w = w[i]->d;
+    J.rs = rs ? rs + 64 * i : nullptr;
+    J.proof_out = proofs_out + 256 * i;
+    return ZKFL_OK;
+  });
 }
 
-int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
-                                  const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
-  if (!ctx || !key || !prog || (n && (!inputs || !proofs_out))) return fail(ZKFL_E_ARG, "full_prove: null argument");
+int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_witness* const* w,
+                             const uint8_t* rs, uint8_t* proofs_out) {
+  if (!ctx || (n && (!keys || !w || !proofs_out))) return fail(ZKFL_E_ARG, "prove_multi: null argument");
+  for (size_t i = 0; i < n; i++) {
+    if (!keys[i] || keys[i]->ctx != ctx) return fail(ZKFL_E_ARG, "prove_multi: key of another context");
+    if (!w[i] || w[i]->key != keys[i]) return fail(ZKFL_E_MISMATCH, "prove_multi: witness uploaded for another key");
+  }
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    J.key = keys[i];
+    J.w = w[i]->d;
+    J.rs = rs ? rs + 64 * i : nullptr;
+    J.proof_out = proofs_out + 256 * i;
+    return ZKFL_OK;
+  });
+}
+
+static int full_prove_check(const zkfl_ctx* ctx, const zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                            const uint8_t* inputs, size_t* n_in) {
+  if (!key || !prog || (n && !inputs)) return fail(ZKFL_E_ARG, "full_prove: null argument");
+  if (key->ctx != ctx || prog->ctx != ctx) return fail(ZKFL_E_ARG, "full_prove: key/program of another context");
   uint32_t nw = 0, n_in32 = 0, npub = 0;
   wprog_info(prog->p, &nw, &n_in32, &npub);
   if (nw != key->nVars || npub != key->nPub)
     return fail(ZKFL_E_MISMATCH, "witness program does not match the proving key (nVars / nPublic)");
-  const size_t n_in = n_in32;
-  {
-    std::string err;
-    if (!wprog_inputs_ok(prog->p, n, inputs, err)) return fail(ZKFL_E_ARG, err);
+  *n_in = n_in32;
+  std::string err;
+  if (!wprog_inputs_ok(prog->p, n, inputs, err)) return fail(ZKFL_E_ARG, err);
+  return ZKFL_OK;
+}
+
+int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                                  const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
+  if (!ctx || (n && !proofs_out)) return fail(ZKFL_E_ARG, "full_prove: null argument");
+  size_t n_in = 0;
+  int rc = full_prove_check(ctx, key, prog, n, inputs, &n_in);
+  if (rc) return rc;
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    J.key = key;
+    J.prog = prog->p;
+    J.input = inputs + i * n_in * 32;
+    J.n_in = n_in;
+    J.rs = rs ? rs + 64 * i : nullptr;
+    J.proof_out = proofs_out + 256 * i;
+    J.pub_out = pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr;
+    return ZKFL_OK;
+  });
+}
+
+int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,
+                                  const uint8_t* const* inputs, const uint8_t* rs, uint8_t* proofs_out,
+                                  uint8_t* const* pubs_out) {
+  if (!ctx || (n && (!keys || !progs || !inputs || !proofs_out))) return fail(ZKFL_E_ARG, "full_prove_multi: null argument");
+  std::vector<size_t> n_in(n);
+  for (size_t i = 0; i < n; i++) {
+    int rc = full_prove_check(ctx, keys[i], progs[i], 1, inputs[i], &n_in[i]);
+    if (rc) return fail(rc, "job " + std::to_string(i) + ": " + g_err);
   }
-  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-  int rc = ZKFL_OK;
-  size_t bad_index = SIZE_MAX;
-  uint32_t bad_assert = 0;
-  auto drain = [&](ProofSlot* s) {
-    uint32_t f = 0xFFFFFFFFu;
-    int r2 = wait_full_slot(key, s, proofs_out + 256 * s->out_index,
-                            pubs_out ? pubs_out + (size_t)key->nPub * 32 * s->out_index : nullptr, &f);
-    if (r2 == ZKFL_OK && f != 0xFFFFFFFFu && s->out_index < bad_index) {
-      bad_index = s->out_index;
-      bad_assert = f;
-    }
-    return r2;
-  };
-  for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
-    uint32_t rsl[16];
-    rc = get_rs(rs ? rs + 64 * i : nullptr, rsl);
-    if (rc) break;
-    ProofSlot* s = nullptr;
-    rc = get_slot(key, i, &s);
-    if (rc) break;
-    if (s->busy) {
-      rc = s->full ? drain(s) : wait_slot(s, nullptr);
-      if (rc) break;
-    }
-    rc = enqueue_full_proof(ctx, key, prog->p, s, inputs + i * n_in * 32, n_in, rsl);
-    if (rc) break;
-    s->busy = true;
-    s->out_index = i;
-  }
-  for (ProofSlot* s : key->slots) {
-    if (s->busy) {
-      int r2 = s->full ? drain(s) : wait_slot(s, nullptr);
-      if (rc == ZKFL_OK) rc = r2;
-    }
-  }
-  if (rc == ZKFL_OK && bad_index != SIZE_MAX)
-    rc = fail(ZKFL_E_CONSTRAINT, "witness " + std::to_string(bad_index) + ": assert constraint #" +
-                                     std::to_string(bad_assert) + " failed (inputs do not satisfy the circuit)");
-  return rc;
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    J.key = keys[i];
+    J.prog = progs[i]->p;
+    J.input = inputs[i];
+    J.n_in = n_in[i];
+    J.rs = rs ? rs + 64 * i : nullptr;
+    J.proof_out = proofs_out + 256 * i;
+    J.pub_out = pubs_out ? pubs_out[i] : nullptr;
+    return ZKFL_OK;
+  });
 }
 
 int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, const uint8_t* rs,
@@ -1296,8 +1370,12 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   ProofSlot* s = nullptr;
   rc = get_slot(key, 0, &s);
   uint32_t zeros[16] = {0};
-  if (rc == ZKFL_OK) rc = enqueue_proof(ctx, key, s, w->d, zeros, 1);
-  if (rc == ZKFL_OK) rc = wait_slot(s, nullptr);
+  if (rc == ZKFL_OK && s->busy) rc = wait_slot(s);
+  if (rc == ZKFL_OK) {
+    s->out_proof = s->out_pub = nullptr;
+    rc = enqueue_proof(ctx, key, s, w->d, zeros, 1);
+  }
+  if (rc == ZKFL_OK) rc = wait_slot(s);
   hipStream_t st = s ? s->st_main : ctx->st;
   uint32_t* d_o = nullptr;
   if (rc == ZKFL_OK && msm_out) {

@@ -42,20 +42,49 @@ def gradient_commitment(grad_field, client_id, rnd) -> int:
     return poseidon_hash([vector_hash(grad_field), poseidon_hash([client_id, rnd])])
 
 
-def merkle_tree(leaves, depth):
-    zero = poseidon_hash([0])
-    level = list(leaves) + [zero] * ((1 << depth) - len(leaves))
-    tree = [level]
-    while len(level) > 1:
-        level = [poseidon_hash([level[i], level[i + 1]]) for i in range(0, len(level), 2)]
-        tree.append(level)
-    return tree
+class MerkleTree:
+    """buildMerkleTree (tests/full_system_simulation.mjs:198-223) with the padding kept implicit.
+
+    The reference pads the leaves to 2^depth with Poseidon([0]) and hashes every level.  Here level
+    l stores only the nodes above real leaves; any other node is the zero-subtree hash z_l
+    (z_0 = Poseidon([0]), z_{l+1} = Poseidon([z_l, z_l])), the value the full tree holds there.
+    So depth 16 (BASELINE config 3) costs ~n hashes per level instead of 2^16."""
+
+    def __init__(self, leaves, depth):
+        self.depth = depth
+        self.zeros = [poseidon_hash([0])]
+        for _ in range(depth):
+            self.zeros.append(poseidon_hash([self.zeros[-1], self.zeros[-1]]))
+        level = list(leaves)
+        if len(level) > 1 << depth:
+            raise ValueError("more leaves than 2^depth")
+        self.levels = [level]
+        for lvl in range(depth):
+            nxt = []
+            for i in range(0, len(level), 2):
+                right = level[i + 1] if i + 1 < len(level) else self.zeros[lvl]
+                nxt.append(poseidon_hash([level[i], right]))
+            self.levels.append(nxt)
+            level = nxt
+
+    def node(self, lvl, j):
+        level = self.levels[lvl]
+        return level[j] if j < len(level) else self.zeros[lvl]
+
+    @property
+    def root(self):
+        return self.node(self.depth, 0)
 
 
-def merkle_proof(tree, idx, depth):
+def merkle_tree(leaves, depth) -> MerkleTree:
+    return MerkleTree(leaves, depth)
+
+
+def merkle_proof(tree: MerkleTree, idx, depth):
+    """getMerkleProof (tests/full_system_simulation.mjs:225-238)."""
     sib, path = [], []
     for lvl in range(depth):
-        sib.append(tree[lvl][idx ^ 1])
+        sib.append(tree.node(lvl, idx ^ 1))
         path.append(idx % 2)
         idx //= 2
     return sib, path
@@ -76,7 +105,7 @@ class Client:
         self.c0 = n - self.c1
         leaves = [vector_hash(feats[i] + [labels[i]]) for i in range(n)]
         self.tree = merkle_tree(leaves, depth)
-        self.root_D = self.tree[-1][0]
+        self.root_D = self.tree.root
 
     def verified_gradient(self, weights, batch, precision):
         """_computeVerifiedGradient (:511-553)."""
@@ -157,3 +186,19 @@ def secagg_input(client_id, peer_ids, gradient, rnd, tau_sq, root_D, root_W):
         "gradient": [str(g) for g in g_field], "master_key": str(master),
         "shared_keys": [str(k) for k in keys],
     }
+
+
+def federated_round(n_clients=8, rnd=1, first_id=1, tau_sq=100000000, batch=8, dim=4, depth=3, precision=1000):
+    """One round of the reference simulation (tests/full_system_simulation.mjs:1278-1343) at N clients:
+    per client the sgd_verified(batch, dim, depth, precision) input.json (trainAndGenerateProof,
+    :401-477) and the SecureMaskedUpdate(dim, N-1) input.json (generateSecureAggregationProof,
+    :558-637) built on the gradient the training input commits to, with the pairwise keys of
+    :1321-1336.  -> [(training input, secagg input, gradient)] in client order."""
+    ids = list(range(first_id, first_id + n_clients))
+    out = []
+    for cid in ids:
+        c = Client(cid, batch, dim, depth, JsLcg(12345 + cid))
+        tr, grad = c.training_input(batch, precision, tau_sq, rnd=rnd)
+        sa = secagg_input(cid, [j for j in ids if j != cid], grad, rnd, tau_sq, c.root_D, int(tr["root_W"]))
+        out.append((tr, sa, grad))
+    return out

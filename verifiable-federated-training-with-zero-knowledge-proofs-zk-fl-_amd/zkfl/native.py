@@ -66,6 +66,9 @@ SIGNATURES = {
                                           C.POINTER(C.c_size_t)]),
     "zkfl_witness_compute_json": (C.c_int, [_P, _P, C.c_char_p, _U8P]),
     "zkfl_groth16_full_prove_batch": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P, _U8P]),
+    "zkfl_groth16_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.c_char_p, _U8P]),
+    "zkfl_groth16_full_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_char_p),
+                                                C.c_char_p, _U8P, C.POINTER(_U8P)]),
 }
 
 
@@ -95,6 +98,14 @@ def lib():
 def check(rc):
     if rc != ZKFL_OK:
         raise ZkflError(rc, lib().zkfl_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (0 when there is no GPU or no driver)."""
+    n = C.c_int(0)
+    if lib().zkfl_device_count(C.byref(n)) != ZKFL_OK:
+        return 0
+    return n.value
 
 
 def _buf(n):
@@ -193,6 +204,39 @@ class Context:
         res = (C.c_int32 * max(1, n))()
         check(lib().zkfl_groth16_verify_batch(self.h, vk, len(vk), n, publics, npub, proofs, res))
         return [bool(res[i]) for i in range(n)]
+
+    # multi-key batches (one federated round: several circuits' proofs interleaved on one device)
+    def prove_multi(self, jobs, rs: bytes | None = None) -> list:
+        """jobs: [(ProvingKey, ResidentWitness)] -> [proof 256 B] (zkfl_groth16_prove_multi)."""
+        n = len(jobs)
+        keys = (_P * max(1, n))(*[k.h for k, _ in jobs])
+        ws = (_P * max(1, n))(*[w.h for _, w in jobs])
+        out = _buf(256 * max(1, n))
+        check(lib().zkfl_groth16_prove_multi(self.h, n, keys, ws, rs, out))
+        ob = bytes(out)
+        return [ob[256 * i:256 * i + 256] for i in range(n)]
+
+    def full_prove_multi(self, jobs, rs: bytes | None = None) -> list:
+        """jobs: [(ProvingKey, WitnessProgram, input vector bytes)] -> [(proof, [public ints])]
+        (zkfl_groth16_full_prove_multi: witness + proof per slot, keys interleaved)."""
+        n = len(jobs)
+        for k, wp, inp in jobs:
+            if len(inp) != 32 * wp.n_inputs:
+                raise ZkflError(-1, f"expected {wp.n_inputs} input values (32 B each)")
+        keys = (_P * max(1, n))(*[k.h for k, _, _ in jobs])
+        progs = (_P * max(1, n))(*[wp.h for _, wp, _ in jobs])
+        ins = (C.c_char_p * max(1, n))(*[inp for _, _, inp in jobs])
+        pub_bufs = [_buf(32 * max(1, k.n_public)) for k, _, _ in jobs]
+        pubs = (_U8P * max(1, n))(*[C.cast(b, _U8P) for b in pub_bufs])
+        out = _buf(256 * max(1, n))
+        check(lib().zkfl_groth16_full_prove_multi(self.h, n, keys, progs, ins, rs, out, pubs))
+        ob = bytes(out)
+        res = []
+        for i, (k, _, _) in enumerate(jobs):
+            pb = bytes(pub_bufs[i])
+            res.append((ob[256 * i:256 * i + 256],
+                        [int.from_bytes(pb[32 * j:32 * j + 32], "little") for j in range(k.n_public)]))
+        return res
 
     def pairing(self, g1: bytes, g2: bytes, final_exp: bool = True) -> bytes:
         """e(P_i, Q_i) for n pairs (std affine); 384 B std Fq12 each (toObject order)."""
