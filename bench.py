@@ -244,6 +244,69 @@ def c5_leg(ctx, rank, world, rounds, slots, dist):
             "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
 
 
+POS_RP = (56, 57, 56, 60, 60, 63, 64, 63, 60, 66, 60, 65, 70, 60, 64, 68)     # circomlib R_P, t = 2..17
+MAC_PEAK_PER_S = 1024 * 32 * 2.4e9 / (2.2 + 1.8)   # v_mad_u64_u32 + v_addc pairs/s (ISA issue rates)
+
+
+def pos_macs(t):
+    """Multiply-add pairs of one csrc/poseidon.h permutation of width t: S-boxes are 3 Montgomery
+    products (128 pairs each); an MDS row is groups of <= 5 products with one reduction (64 per
+    product + 64); every round applies t rows except the last (row 0 only)."""
+    rp = POS_RP[t - 2]
+    sbox = 3 * 128 * (8 * t + rp)
+    row = sum(64 * g + 64 for g in [5] * (t // 5) + ([t % 5] if t % 5 else []))
+    return sbox + row * ((8 + rp - 1) * t + 1)
+
+
+def merkle_leg(ctx, rank, log2n=20, ln=5):
+    """computeDatasetCommitment (tests/full_system_simulation.mjs:309-335) on the GPU
+    for 2^log2n samples of `ln` values (DIM 4 features + label): vectorHash leaves (Poseidon t = ln+1)
+    then the depth-log2n Poseidon(2) tree, zkfl_dataset_commit.  Reports hashes/s of the kernels
+    (HIP events) and of the whole call (PCIe in and out included), the VALU roofline of the tree
+    kernel, and checks sampled nodes against the host-side Python Poseidon.  -> dict"""
+    import numpy as np
+    n, depth = 1 << log2n, log2n
+    raw = np.random.default_rng(rank).integers(0, 2**63, size=(n * ln, 4), dtype=np.uint64)
+    raw[:, 3] &= np.uint64((1 << 60) - 1)        # < 2^252 < r
+    values = raw.tobytes()
+    ctx.dataset_commit_raw(values[:32 * ln * 1024], 1024, ln, 10)        # tables + warm-up
+    ctx.profile_reset()
+    ctx.set_profiling(True)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tree = ctx.dataset_commit_raw(values, n, ln, depth)
+    dt = (time.perf_counter() - t0) / reps
+    ctx.set_profiling(False)
+    vh_ms, _, vh_units, vh_med = ctx.profile("vector_hash")
+    mk_ms, _, mk_units, mk_med = ctx.profile("merkle")
+    ctx.profile_reset()
+    from zkfl.clients import vector_hash       # the host-side Python Poseidon (zkfl/field.py)
+    from zkfl.field import poseidon_hash
+    node = lambda lvl, j: int.from_bytes(tree[32 * ((2 << depth) - (2 << (depth - lvl)) + j):][:32], "little")  # noqa: E731
+    val = lambda i, k: int.from_bytes(values[32 * (i * ln + k):][:32], "little")  # noqa: E731
+    rnd = np.random.default_rng(7)
+    for i in [0, n - 1] + [int(x) for x in rnd.integers(0, n, 3)]:
+        assert node(0, i) == vector_hash([val(i, k) for k in range(ln)]), "leaf"
+    for lvl in range(1, depth + 1):
+        j = int(rnd.integers(0, 1 << (depth - lvl)))
+        assert node(lvl, j) == poseidon_hash([node(lvl - 1, 2 * j), node(lvl - 1, 2 * j + 1)]), "node"
+    hashes = n + (n - 1)
+    mk_s = mk_med / 1e3
+    achieved_macs = (n - 1) * pos_macs(3) / mk_s
+    return {"samples": n, "values_per_sample": ln, "depth": depth, "hashes": hashes,
+            "kernel_hashes_per_s": round(hashes / ((vh_med + mk_med) / 1e3)),
+            "call_hashes_per_s": round(hashes / dt), "call_ms": round(dt * 1e3, 3),
+            "vector_hash_ms": round(vh_med, 3), "tree_ms": round(mk_med, 3),
+            "tree_roofline": {"bound": "valu", "achieved": round(achieved_macs / 1e12, 3),
+                              "peak": round(MAC_PEAK_PER_S / 1e12, 3), "unit": "T mad+addc pairs/s",
+                              "frac": round(achieved_macs / MAC_PEAK_PER_S, 4),
+                              "per_hash_pairs": pos_macs(3),
+                              "hbm_bytes_per_hash": 96, "hbm_GBps": round((n - 1) * 96 / mk_s / 1e9, 2)},
+            "path": "zkfl_dataset_commit: values (host) -> vectorHash leaves -> Poseidon(2) levels -> padded tree (host)",
+            "checked": "sampled leaves and one node per level == host Poseidon (zkfl/field.py)"}
+
+
 def _barrier(ctx, dist):
     ctx.synchronize()
     if dist is not None:
@@ -295,6 +358,7 @@ def main():
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     ap.add_argument("--e2e-steps", type=int, default=8, help="steps of the input.json -> proof leg (0: skip)")
     ap.add_argument("--c5-rounds", type=int, default=8, help="federated rounds of the config-5 leg (0: skip)")
+    ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -367,6 +431,10 @@ def main():
     if args.c5_rounds:
         c5 = c5_leg(ctx, rank, world, args.c5_rounds, min(args.slots, 8), dist)
         log(f"[bench r{rank}] config 5: {c5}")
+    merkle = None
+    if args.merkle_log2n:
+        merkle = merkle_leg(ctx, rank, args.merkle_log2n)
+        log(f"[bench r{rank}] dataset commitment: {merkle}")
     if rank == 0:
         cpu, oracle_match = None, None
         if world == 1 and not args.no_cpu_baseline:
@@ -383,7 +451,8 @@ def main():
                   "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}
         line = report(args, world, elapsed, n_timed * world, verified_all, prof, nprof, key, config,
-                      {"oracle_match": oracle_match, "end_to_end": e2e, "c5": c5, "cpu_baseline": cpu})
+                      {"oracle_match": oracle_match, "end_to_end": e2e, "c5": c5, "dataset_commit": merkle,
+                       "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")

@@ -197,6 +197,33 @@ int zkfl_pairing(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, 
 /* Parity hook: the Miller-loop value before the final exponentiation, same layout. */
 int zkfl_debug_miller_loop(zkfl_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* out);
 
+/* Poseidon hashing and Merkle trees on the GPU: the reference's data/server side
+ * (tests/full_system_simulation.mjs:139-238, circomlibjs `poseidon` [ext]), bit-identical to
+ * circomlib Poseidon (src/circuits/lib/poseidon.circom:35-96).  Values are 32 B std-form LE, < r
+ * (ZKFL_E_ARG otherwise); circomlibjs reduces wider integers mod r, callers do that first.
+ *
+ * zkfl_poseidon_params (host only, no device): circomlib's constants for width t = 2..17 as the
+ * Grain LFSR generates them -- (8 + R_P) * t raw round constants and the 2t Cauchy points x|y of the
+ * MDS M[i][j] = 1/(x_i + y_j), std form -- and R_P.  Either output may be NULL. */
+int zkfl_poseidon_params(uint32_t t, uint8_t* consts_out, uint8_t* xy_out, uint32_t* rp_out);
+/* out[i] = Poseidon(inputs[i*arity .. +arity)), arity 1..16 (circomlibjs poseidon(inputs)). */
+int zkfl_poseidon_batch(zkfl_ctx* ctx, uint32_t arity, size_t n, const uint8_t* inputs, uint8_t* out);
+/* out[i] = vectorHash(values[i*len .. +len)), len 1..256: Poseidon of <= 16 values, else Poseidon of
+ * the 16-value chunk hashes (vectorHash, tests/full_system_simulation.mjs:139-156; VectorHash,
+ * src/circuits/training/vector_hash.circom:46-89). */
+int zkfl_vector_hash_batch(zkfl_ctx* ctx, uint32_t len, size_t n, const uint8_t* values, uint8_t* out);
+/* buildMerkleTree(leafHashes, depth) (tests/full_system_simulation.mjs:198-223): n <= 2^depth leaves
+ * padded with Poseidon([0]), depth <= ZKFL_MERKLE_MAX_DEPTH.  tree_out: (2^(depth+1) - 1) x 32 B, the
+ * reference's `tree` array flattened -- level 0 (2^depth padded leaves) first, the root last, so
+ * getMerkleProof (:225-238) reads tree_out[level_offset(l) + (idx >> l ^ 1)]. */
+#define ZKFL_MERKLE_MAX_DEPTH 30
+int zkfl_merkle_build(zkfl_ctx* ctx, const uint8_t* leaves, size_t n, uint32_t depth, uint8_t* tree_out);
+/* computeDatasetCommitment (tests/full_system_simulation.mjs:309-335) without leaving the device:
+ * leaf i = vectorHash(values[i*len .. +len)) (features[i] || label[i]), then buildMerkleTree;
+ * root_D = the last 32 B of tree_out. */
+int zkfl_dataset_commit(zkfl_ctx* ctx, const uint8_t* values, size_t n, uint32_t len, uint32_t depth,
+                        uint8_t* tree_out);
+
 /* Dev-ceremony fixed-base multiplications: out[i] = scalars[i] * generator, mont affine. */
 int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
 int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);

@@ -72,3 +72,17 @@ def test_node_addon_loads():
     out = subprocess.run([node, "-e", js, addon], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "1"
+
+
+def test_poseidon_params_host_generator_matches_oracle():
+    """The library's native Grain-LFSR generator (csrc/merkle.hip, host code, no device) yields
+    circomlib's constants for every width t = 2..17: the round constants and the MDS matrix
+    M[i][j] = 1/(x_i + y_j) equal oracle/poseidon.py's (pinned by the reference fixture)."""
+    from oracle import poseidon as op
+    for t in range(2, 18):
+        consts, xs, ys, rp = native.poseidon_params(t)
+        C, M = op.constants(t)
+        assert rp == op.N_ROUNDS_P[t - 2]
+        assert consts == list(C)
+        assert [[pow(x + y, op.R - 2, op.R) for y in ys] for x in xs] == [list(r) for r in M]
+    assert native.lib().zkfl_poseidon_params(18, None, None, None) == -1

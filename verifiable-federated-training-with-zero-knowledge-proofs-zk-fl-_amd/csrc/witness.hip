@@ -23,15 +23,13 @@
 
 #include "common.h"
 #include "field.h"
+#include "host_parse.h"
 #include "witness.h"
 #include "zkfl.h"
 
 namespace zkfl {
 
 namespace {
-
-enum : uint32_t { K_LC = 0, K_MUL = 1, K_INV = 2, K_BITS = 3, K_POS = 4 };
-constexpr int MAX_T = 17;
 
 struct PosWidth {
   uint32_t rp;
@@ -168,263 +166,6 @@ int hip_err(hipError_t e, const char* where, std::string& err) {
   return e == hipErrorOutOfMemory ? ZKFL_E_OOM : ZKFL_E_DEVICE;
 }
 
-bool lt_r_host(const uint32_t* v) {
-  static const uint32_t Rl[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
-                                 0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
-  for (int i = 7; i >= 0; i--)
-    if (v[i] != Rl[i]) return v[i] < Rl[i];
-  return false;
-}
-
-struct Reader {
-  const uint8_t* p;
-  size_t left;
-  bool ok = true;
-  const uint8_t* take(size_t n) {
-    if (!ok || n > left) {
-      ok = false;
-      return nullptr;
-    }
-    const uint8_t* r = p;
-    p += n;
-    left -= n;
-    return r;
-  }
-  uint32_t u32() {
-    const uint8_t* q = take(4);
-    uint32_t v = 0;
-    if (q) memcpy(&v, q, 4);
-    return v;
-  }
-};
-
-
-struct WSignal {  // one declared input signal (input.json key)
-  std::string name;
-  std::vector<uint32_t> dims;
-  uint32_t first = 0;
-  uint32_t pub = 0;
-};
-
-bool read_signals(Reader& R, std::vector<WSignal>& out) {
-  const uint32_t n = R.u32();
-  if (!R.ok || n > (1u << 20)) return false;
-  for (uint32_t i = 0; i < n; i++) {
-    WSignal sg;
-    const uint32_t len = R.u32();
-    if (!R.ok || len > 4096) return false;
-    const uint8_t* nm = R.take((len + 3) & ~3u);
-    if (!nm) return false;
-    sg.name.assign(reinterpret_cast<const char*>(nm), len);
-    const uint32_t nd = R.u32();
-    if (!R.ok || nd > 16) return false;
-    for (uint32_t d = 0; d < nd; d++) sg.dims.push_back(R.u32());
-    sg.first = R.u32();
-    sg.pub = R.u32();
-    if (!R.ok) return false;
-    out.push_back(std::move(sg));
-  }
-  return true;
-}
-
-// ---------------------------------------------------------------------------
-// input.json -> flattened input signals (host).  The subset circom's witness calculator accepts
-// for these circuits: one object mapping signal names to a number, a decimal (or 0x hex) string,
-// or nested arrays of those; negatives are reduced mod r as circom does.  Extra keys are
-// ignored (as zkfl/r1cs.py::flatten_inputs does).
-// ---------------------------------------------------------------------------
-struct JVal {
-  enum Kind { SCALAR, ARRAY, OBJECT } kind = SCALAR;
-  std::string text;  // scalar literal (string contents or number text)
-  std::vector<JVal> items;
-  std::vector<std::string> keys;
-};
-
-struct JParser {
-  const char* s;
-  const char* e;
-  std::string err;
-  void ws() {
-    while (s < e && (*s == ' ' || *s == '\n' || *s == '\r' || *s == '\t')) s++;
-  }
-  bool fail(const char* m) {
-    if (err.empty()) err = m;
-    return false;
-  }
-  bool str(std::string& out) {
-    if (s >= e || *s != '"') return fail("expected a string");
-    s++;
-    while (s < e && *s != '"') {
-      if (*s == '\\') return fail("escapes are not supported in input strings");
-      out.push_back(*s++);
-    }
-    if (s >= e) return fail("unterminated string");
-    s++;
-    return true;
-  }
-  bool value(JVal& v, int depth) {
-    if (depth > 32) return fail("nesting too deep");
-    ws();
-    if (s >= e) return fail("unexpected end of input");
-    if (*s == '{' || *s == '[') {
-      const bool obj = *s == '{';
-      const char close = obj ? '}' : ']';
-      v.kind = obj ? JVal::OBJECT : JVal::ARRAY;
-      s++;
-      ws();
-      if (s < e && *s == close) {
-        s++;
-        return true;
-      }
-      for (;;) {
-        ws();
-        std::string k;
-        if (obj) {
-          if (!str(k)) return false;
-          ws();
-          if (s >= e || *s != ':') return fail("expected ':'");
-          s++;
-        }
-        JVal c;
-        if (!value(c, depth + 1)) return false;
-        if (obj) v.keys.push_back(k);
-        v.items.push_back(std::move(c));
-        ws();
-        if (s < e && *s == ',') {
-          s++;
-          continue;
-        }
-        if (s < e && *s == close) {
-          s++;
-          return true;
-        }
-        return fail(obj ? "expected ',' or '}'" : "expected ',' or ']'");
-      }
-    }
-    v.kind = JVal::SCALAR;
-    if (*s == '"') return str(v.text);
-    while (s < e && (isalnum((unsigned char)*s) || *s == '-' || *s == '+' || *s == '.')) v.text.push_back(*s++);
-    if (v.text.empty()) return fail("unexpected character");
-    return true;
-  }
-};
-
-// decimal / 0x-hex integer literal (optional sign) -> std-form Fr limbs (mod r)
-bool literal_to_fr(const std::string& t, uint32_t out[8]) {
-  static const uint64_t RL[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
-                                 0x30644e72e131a029ull};
-  size_t i = 0;
-  bool neg = false;
-  if (i < t.size() && (t[i] == '-' || t[i] == '+')) neg = t[i++] == '-';
-  unsigned base = 10;
-  if (i + 1 < t.size() && t[i] == '0' && (t[i + 1] == 'x' || t[i + 1] == 'X')) {
-    base = 16;
-    i += 2;
-  }
-  if (i >= t.size()) return false;
-  uint64_t acc[5] = {0, 0, 0, 0, 0};  // < 16 r + 15 < 2^259 before reduction
-  for (; i < t.size(); i++) {
-    const char ch = t[i];
-    unsigned d;
-    if (ch >= '0' && ch <= '9') d = ch - '0';
-    else if (base == 16 && ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
-    else if (base == 16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
-    else return false;  // fractions / exponents are not field elements
-    unsigned __int128 c = d;
-    for (int k = 0; k < 5; k++) {
-      c += (unsigned __int128)acc[k] * base;
-      acc[k] = (uint64_t)c;
-      c >>= 64;
-    }
-    for (;;) {  // reduce below r
-      bool ge = acc[4] != 0;
-      if (!ge) {
-        ge = true;
-        for (int k = 3; k >= 0; k--)
-          if (acc[k] != RL[k]) {
-            ge = acc[k] > RL[k];
-            break;
-          }
-      }
-      if (!ge) break;
-      uint64_t borrow = 0;
-      for (int k = 0; k < 5; k++) {
-        const unsigned __int128 sub = (unsigned __int128)(k < 4 ? RL[k] : 0) + borrow;
-        borrow = (unsigned __int128)acc[k] < sub ? 1 : 0;
-        acc[k] = (uint64_t)((unsigned __int128)acc[k] - sub);
-      }
-    }
-  }
-  const bool zero = !(acc[0] | acc[1] | acc[2] | acc[3]);
-  if (neg && !zero) {  // r - v
-    uint64_t borrow = 0;
-    for (int k = 0; k < 4; k++) {
-      const unsigned __int128 sub = (unsigned __int128)acc[k] + borrow;
-      borrow = (unsigned __int128)RL[k] < sub ? 1 : 0;
-      acc[k] = (uint64_t)((unsigned __int128)RL[k] - sub);
-    }
-  }
-  for (int k = 0; k < 4; k++) {
-    out[2 * k] = (uint32_t)acc[k];
-    out[2 * k + 1] = (uint32_t)(acc[k] >> 32);
-  }
-  return true;
-}
-
-bool flatten(const JVal& v, const WSignal& sg, size_t dim, std::vector<uint32_t>& out, std::string& err) {
-  if (dim == sg.dims.size()) {
-    if (v.kind != JVal::SCALAR) {
-      err = "input '" + sg.name + "' has too many dimensions";
-      return false;
-    }
-    uint32_t fr[8];
-    if (!literal_to_fr(v.text, fr)) {
-      err = "input '" + sg.name + "': '" + v.text + "' is not an integer";
-      return false;
-    }
-    out.insert(out.end(), fr, fr + 8);
-    return true;
-  }
-  if (v.kind != JVal::ARRAY || v.items.size() != sg.dims[dim]) {
-    std::string shape;
-    for (uint32_t d : sg.dims) shape += (shape.empty() ? "" : ", ") + std::to_string(d);
-    err = "input '" + sg.name + "' has wrong shape, expected (" + shape + ")";
-    return false;
-  }
-  for (const JVal& c : v.items)
-    if (!flatten(c, sg, dim + 1, out, err)) return false;
-  return true;
-}
-
-int inputs_from_json(const std::vector<WSignal>& sigs, const char* json, std::vector<uint32_t>& out,
-                     std::string& err) {
-  if (!json) {
-    err = "null input json";
-    return ZKFL_E_ARG;
-  }
-  JParser P{json, json + strlen(json), ""};
-  JVal root;
-  if (!P.value(root, 0)) {
-    err = "input json: " + P.err;
-    return ZKFL_E_ARG;
-  }
-  P.ws();
-  if (P.s != P.e || root.kind != JVal::OBJECT) {
-    err = "input json: expected one object of signal names";
-    return ZKFL_E_ARG;
-  }
-  for (const WSignal& sg : sigs) {
-    size_t k = 0;
-    while (k < root.keys.size() && root.keys[k] != sg.name) k++;
-    if (k == root.keys.size()) {
-      err = "missing input signal '" + sg.name + "'";
-      return ZKFL_E_ARG;
-    }
-    if (!flatten(root.items[k], sg, 0, out, err)) return ZKFL_E_ARG;
-  }
-  return ZKFL_OK;
-}
-
 }  // namespace
 
 struct WProg {
@@ -448,34 +189,9 @@ int wprog_inputs_json(const WProg* p, const char* json, std::vector<uint32_t>& o
 
 int wprog_image_inputs_json(const uint8_t* img, size_t len, const char* json, std::vector<uint32_t>& out,
                             std::string& err) {
-  // walk the image to its signal table without touching the device
-  Reader R{img, len};
-  const uint8_t* magic = R.take(4);
-  if (!magic || memcmp(magic, "zkwp", 4) != 0 || R.u32() != 2) {
-    err = "witness program: bad magic/version";
-    return ZKFL_E_FORMAT;
-  }
-  uint32_t h[12];
-  for (int i = 0; i < 12; i++) h[i] = R.u32();
-  const uint32_t n_ops = h[5], n_levels = h[6], n_lcs = h[7], n_terms = h[8], n_asserts = h[9], n_tmpl = h[10],
-                 n_widths = h[11];
-  R.take(4ull * (n_levels + 1));
-  R.take(16ull * n_ops);
-  R.take(4ull * (n_lcs + 1));
-  R.take(36ull * n_terms);
-  R.take(4ull * n_asserts);
-  R.take(32ull * n_tmpl);
-  for (uint32_t k = 0; k < n_widths && R.ok; k++) {
-    const uint32_t t = R.u32(), rp = R.u32();
-    if (t > (uint32_t)MAX_T || rp > 128) R.ok = false;
-    else R.take(32ull * ((8 + rp) * t + (size_t)t * t));
-  }
-  std::vector<WSignal> sigs;
-  if (!R.ok || !read_signals(R, sigs)) {
-    err = "witness program: truncated or inconsistent image";
-    return ZKFL_E_FORMAT;
-  }
-  return inputs_from_json(sigs, json, out, err);
+  std::vector<WSignal> sigs;  // the signal table alone, without touching the device
+  int rc = wprog_signals(img, len, sigs, err);
+  return rc ? rc : inputs_from_json(sigs, json, out, err);
 }
 
 void wprog_info(const WProg* p, uint32_t* nw, uint32_t* n_in, uint32_t* n_pub) {
@@ -485,102 +201,24 @@ void wprog_info(const WProg* p, uint32_t* nw, uint32_t* n_in, uint32_t* n_pub) {
 }
 
 int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std::string& err) {
-  Reader R{img, len};
-  const uint8_t* magic = R.take(4);
-  if (!magic || memcmp(magic, "zkwp", 4) != 0 || R.u32() != 2) {
-    err = "witness program: bad magic/version";
-    return ZKFL_E_FORMAT;
-  }
+  WProgHost H;
+  int rc = wprog_parse(img, len, H, err);  // csrc/host_parse.cc: every index validated
+  if (rc) return rc;
   WProg* p = new WProg();
-  p->n_wires = R.u32();
-  p->n_pub_out = R.u32();
-  p->n_pub_in = R.u32();
-  p->n_prv_in = R.u32();
-  p->in_first = R.u32();
-  p->n_ops = R.u32();
-  p->n_levels = R.u32();
-  const uint32_t n_lcs = R.u32(), n_terms = R.u32();
-  p->n_asserts = R.u32();
-  const uint32_t n_tmpl = R.u32(), n_widths = R.u32();
-  const uint8_t* lp = R.take(4ull * (p->n_levels + 1));
-  const uint8_t* ops = R.take(16ull * p->n_ops);
-  const uint8_t* lcp = R.take(4ull * (n_lcs + 1));
-  const uint8_t* tw = R.take(4ull * n_terms);
-  const uint8_t* tc = R.take(32ull * n_terms);
-  const uint8_t* as = R.take(4ull * p->n_asserts);
-  const uint8_t* tm = R.take(32ull * n_tmpl);
-  std::vector<uint8_t> consts;
-  bool ok = R.ok && p->n_wires > 0 && p->in_first == 1 + p->n_pub_out &&
-            (uint64_t)p->in_first + p->n_pub_in + p->n_prv_in <= p->n_wires;
-  for (uint32_t k = 0; k < n_widths && ok; k++) {
-    const uint32_t t = R.u32(), rp = R.u32();
-    if (!R.ok || t < 2 || t > (uint32_t)MAX_T || rp > 128) {
-      ok = false;
-      break;
-    }
-    const size_t nc = (8 + rp) * t, nm = (size_t)t * t;
-    const uint8_t* c = R.take(32 * (nc + nm));
-    if (!c) {
-      ok = false;
-      break;
-    }
-    p->view.width[t] = {rp, (uint32_t)(consts.size() / 32), (uint32_t)(consts.size() / 32 + nc)};
-    consts.insert(consts.end(), c, c + 32 * (nc + nm));
-  }
-  if (ok && !read_signals(R, p->signals)) ok = false;
-  if (ok) {  // the signal table must tile the input range exactly, in declaration order
-    uint64_t next = p->in_first;
-    for (const WSignal& sg : p->signals) {
-      uint64_t cnt = 1;
-      for (uint32_t d : sg.dims) cnt *= d;
-      ok = ok && sg.first == next;
-      next += cnt;
-    }
-    ok = ok && next == (uint64_t)p->in_first + p->n_pub_in + p->n_prv_in && R.left == 0;
-  }
-  if (ok) {
-    // structural validation (device code trusts these indices)
-    p->level_ptr.resize(p->n_levels + 1);
-    memcpy(p->level_ptr.data(), lp, 4ull * (p->n_levels + 1));
-    std::vector<uint32_t> lcv(n_lcs + 1), twv(n_terms), asv(p->n_asserts), tmv(8ull * n_tmpl);
-    memcpy(lcv.data(), lcp, lcv.size() * 4);
-    memcpy(twv.data(), tw, twv.size() * 4);
-    memcpy(asv.data(), as, asv.size() * 4);
-    memcpy(tmv.data(), tm, tmv.size() * 4);
-    ok = p->level_ptr[0] == 0 && p->level_ptr[p->n_levels] == p->n_ops && lcv[0] == 0 && lcv[n_lcs] == n_terms;
-    for (uint32_t i = 0; ok && i < p->n_levels; i++) ok = p->level_ptr[i] <= p->level_ptr[i + 1];
-    for (uint32_t i = 0; ok && i < n_lcs; i++) ok = lcv[i] <= lcv[i + 1];
-    for (uint32_t i = 0; ok && i < n_terms; i++) ok = (twv[i] & 0x7FFFFFFFu) < p->n_wires;
-    for (uint32_t i = 0; ok && i < p->n_asserts; i++) ok = (uint64_t)asv[i] + 3 <= n_lcs;
-    for (uint32_t i = 0; ok && i < p->n_ops; i++) {
-      uint32_t o[4];
-      memcpy(o, ops + 16ull * i, 16);
-      const uint32_t kind = o[0], outw = o[1], lc0 = o[2], aux = o[3];
-      uint64_t nout = 1, nlc = 1;
-      if (kind == K_MUL) nlc = 2;
-      else if (kind == K_BITS) nout = aux, ok = aux >= 1 && aux <= 254;
-      else if (kind == K_POS) {
-        const uint32_t t = aux & 0xFF, tid = aux >> 8;
-        ok = t >= 2 && t <= (uint32_t)MAX_T && tid < n_tmpl && p->view.width[t].rp != 0 &&
-             tmv[8ull * tid] == 8 * t + p->view.width[t].rp;  // n_sbox = R_F t + R_P
-        if (ok) {
-          uint32_t live = 0;
-          for (int q = 1; q < 8; q++) live += __builtin_popcount(tmv[8ull * tid + q]);
-          nout = 3ull * live;
-          nlc = t - 1;
-        }
-      } else ok = ok && (kind == K_LC || kind == K_INV);
-      // outputs: never the constant wire, never an input signal
-      const uint64_t in_end = (uint64_t)p->in_first + p->n_pub_in + p->n_prv_in;
-      ok = ok && (uint64_t)lc0 + nlc <= n_lcs && (uint64_t)outw + nout <= p->n_wires && outw >= 1 &&
-           ((uint64_t)outw + nout <= p->in_first || outw >= in_end);
-    }
-  }
-  if (!ok) {
-    wprog_free(p);
-    err = "witness program: truncated or inconsistent image";
-    return ZKFL_E_FORMAT;
-  }
+  p->n_wires = H.n_wires;
+  p->n_pub_out = H.n_pub_out;
+  p->n_pub_in = H.n_pub_in;
+  p->n_prv_in = H.n_prv_in;
+  p->in_first = H.in_first;
+  p->n_ops = H.n_ops;
+  p->n_levels = H.n_levels;
+  p->n_asserts = H.n_asserts;
+  p->level_ptr = std::move(H.level_ptr);
+  p->signals = std::move(H.signals);
+  for (int t = 0; t <= MAX_T; t++) p->view.width[t] = {H.width[t].rp, H.width[t].c_off, H.width[t].m_off};
+  const uint32_t n_lcs = H.n_lcs, n_terms = H.n_terms, n_tmpl = H.n_tmpl;
+  const uint8_t *ops = H.ops, *lcp = H.lc_ptr, *tw = H.term_wire, *tc = H.term_coef, *as = H.asserts, *tm = H.tmpl;
+  std::vector<uint8_t>& consts = H.consts;
   struct Up {
     const void* src;
     size_t bytes;
@@ -620,7 +258,7 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
 bool wprog_inputs_ok(const WProg* p, size_t n, const uint8_t* inputs, std::string& err) {
   const uint32_t n_in = p->n_pub_in + p->n_prv_in;
   for (size_t i = 0; i < n * n_in; i++)
-    if (!lt_r_host(reinterpret_cast<const uint32_t*>(inputs + 32 * i))) {
+    if (!fr_lt_r(reinterpret_cast<const uint32_t*>(inputs + 32 * i))) {
       err = "witness input " + std::to_string(i % n_in) + " of witness " + std::to_string(i / n_in) + " is not < r";
       return false;
     }

@@ -29,7 +29,9 @@
 
 #include "curve.h"
 #include "glv.h"
+#include "host_parse.h"
 #include "field.h"
+#include "merkle.h"
 #include "msm_api.h"
 #include "ntt.h"
 #include "prof.h"
@@ -71,58 +73,10 @@ bool lt_r(const uint32_t* v) {  // v < r
   return false;
 }
 
-// ---------------------------------------------------------------------------
-// iden3 binfile reader
-// ---------------------------------------------------------------------------
-struct Section {
-  size_t off = 0, size = 0;
-  bool present = false;
-};
-
-int read_binfile(const uint8_t* buf, size_t len, const char* magic, std::vector<Section>& secs) {
-  if (!buf || len < 12) return fail(ZKFL_E_FORMAT, "file too short");
-  if (memcmp(buf, magic, 4) != 0) return fail(ZKFL_E_FORMAT, std::string("bad magic, expected ") + magic);
-  uint32_t nsec;
-  memcpy(&nsec, buf + 8, 4);
-  size_t off = 12;
-  secs.assign(16, Section());
-  for (uint32_t i = 0; i < nsec; i++) {
-    if (off + 12 > len) return fail(ZKFL_E_FORMAT, "truncated section header");
-    uint32_t typ;
-    uint64_t size;
-    memcpy(&typ, buf + off, 4);
-    memcpy(&size, buf + off + 4, 8);
-    off += 12;
-    if (off + size > len) return fail(ZKFL_E_FORMAT, "truncated section");
-    if (typ < secs.size() && !secs[typ].present) {
-      secs[typ].off = off;
-      secs[typ].size = size;
-      secs[typ].present = true;
-    }
-    off += size;
-  }
-  return ZKFL_OK;
-}
-
-struct WtnsView {
-  const uint8_t* data = nullptr;  // nWitness x 32 B std
-  uint32_t n = 0;
-};
-
 int parse_wtns(const uint8_t* buf, size_t len, WtnsView& out) {
-  std::vector<Section> s;
-  int rc = read_binfile(buf, len, "wtns", s);
-  if (rc) return rc;
-  if (!s[1].present || !s[2].present) return fail(ZKFL_E_FORMAT, "wtns: missing section");
-  const uint8_t* h = buf + s[1].off;
-  uint32_t n8;
-  memcpy(&n8, h, 4);
-  if (n8 != 32 || s[1].size < 4 + 32 + 4) return fail(ZKFL_E_FORMAT, "wtns: n8 != 32");
-  if (memcmp(h + 4, R_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "wtns: prime is not bn128 r");
-  memcpy(&out.n, h + 36, 4);
-  if (s[2].size != (size_t)out.n * 32) return fail(ZKFL_E_FORMAT, "wtns: section 2 size");
-  out.data = buf + s[2].off;
-  return ZKFL_OK;
+  std::string err;
+  int rc = wtns_parse(buf, len, out, err);  // csrc/host_parse.cc
+  return rc ? fail(rc, err) : ZKFL_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -412,6 +366,7 @@ struct zkfl_ctx {
   hipStream_t st = nullptr;  // primitives, key loading, verification
   Profiler prof;
   VkDev* vk = nullptr;       // last prepared verification key (reused while the vk bytes repeat)
+  PosTables* pos = nullptr;  // Poseidon constants of every width (first hashing call)
 };
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
@@ -905,6 +860,64 @@ int run_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out, b
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+namespace {
+
+int pos_ready(zkfl_ctx* ctx) {
+  if (ctx->pos) return ZKFL_OK;
+  std::string err;
+  int rc = pos_tables_create(&ctx->pos, ctx->st, err);
+  return rc ? fail(rc, err) : ZKFL_OK;
+}
+
+int check_fr_array(const uint8_t* v, size_t count, const char* what) {
+  for (size_t i = 0; i < count; i++) {
+    uint32_t w[8];
+    memcpy(w, v + 32 * i, 32);
+    if (!lt_r(w)) return fail(ZKFL_E_ARG, std::string(what) + " " + std::to_string(i) + " is not < r");
+  }
+  return ZKFL_OK;
+}
+
+// device scratch of one hashing call, freed on every exit path
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  hipError_t get(void** out, size_t bytes) {
+    *out = nullptr;
+    hipError_t e = hipMalloc(out, bytes ? bytes : 32);
+    if (e == hipSuccess) p.push_back(*out);
+    return e;
+  }
+};
+
+
+// leaves (device, Montgomery) -> full padded tree (host, std)
+int tree_from_device_leaves(zkfl_ctx* ctx, DevBufs& B, const Fr* d_leaves, size_t n, uint32_t depth,
+                            uint8_t* tree_out) {
+  hipStream_t st = ctx->st;
+  const size_t nodes = ((size_t)2 << depth) - 1;
+  Fr *d_work, *d_tree;
+  HIP_TRY(B.get((void**)&d_work, merkle_work_size(n, depth) * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_tree, nodes * 32), "alloc");
+  int pi = ctx->prof.begin("merkle", st);
+  HIP_TRY(merkle_build(ctx->pos, d_leaves, n, depth, d_tree, d_work, st), "merkle");
+  ctx->prof.end(pi, st, (double)(merkle_work_size(n, depth) - n));
+  HIP_TRY(hipMemcpyAsync(tree_out, d_tree, nodes * 32, hipMemcpyDeviceToHost, st), "download");
+  HIP_TRY(hipStreamSynchronize(st), "sync");
+  return ZKFL_OK;
+}
+
+int tree_args(zkfl_ctx* ctx, size_t n, uint32_t depth, const void* in, const void* out) {
+  if (!ctx || !out || (n && !in)) return fail(ZKFL_E_ARG, "merkle: null argument");
+  if (depth > ZKFL_MERKLE_MAX_DEPTH) return fail(ZKFL_E_ARG, "merkle: depth must be <= 30");
+  if (n > ((size_t)1 << depth)) return fail(ZKFL_E_ARG, "merkle: more leaves than 2^depth");
+  return ZKFL_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int zkfl_version(void) { return 1; }
@@ -960,6 +973,7 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->st);
   ctx->prof.reset();
   vk_free(ctx->vk);
+  pos_tables_free(ctx->pos);
   (void)hipStreamDestroy(ctx->st);
   delete ctx;
   return ZKFL_OK;
@@ -997,109 +1011,21 @@ int zkfl_ctx_synchronize(zkfl_ctx* ctx) {
 
 int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out) {
   if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
-  std::vector<Section> s;
-  int rc = read_binfile(buf, len, "zkey", s);
-  if (rc) return rc;
-  for (int i = 1; i <= 9; i++)
-    if (!s[i].present) return fail(ZKFL_E_FORMAT, "zkey: missing section " + std::to_string(i));
-  uint32_t proto;
-  memcpy(&proto, buf + s[1].off, 4);
-  if (proto != 1) return fail(ZKFL_E_FORMAT, "zkey: not a groth16 key");
-  const uint8_t* h = buf + s[2].off;
-  uint32_t n8q, n8r;
-  memcpy(&n8q, h, 4);
-  if (n8q != 32 || memcmp(h + 4, Q_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "zkey: q is not bn128");
-  memcpy(&n8r, h + 36, 4);
-  if (n8r != 32 || memcmp(h + 40, R_LIMBS, 32) != 0) return fail(ZKFL_E_PRIME, "zkey: r is not bn128");
-  uint32_t nVars, nPub, dom;
-  memcpy(&nVars, h + 72, 4);
-  memcpy(&nPub, h + 76, 4);
-  memcpy(&dom, h + 80, 4);
-  const uint8_t* pts = h + 84;  // alpha1 64, beta1 64, beta2 128, gamma2 128, delta1 64, delta2 128
-  if (s[2].size < 84 + 64 * 3 + 128 * 3) return fail(ZKFL_E_FORMAT, "zkey: header size");
-  int logn = 0;
-  while ((1u << logn) < dom) logn++;
-  if ((1u << logn) != dom || logn > 28 || dom < 2) return fail(ZKFL_E_FORMAT, "zkey: domain size");
-  if (nVars < nPub + 1) return fail(ZKFL_E_FORMAT, "zkey: nVars < nPublic+1");
-  const size_t nC = nVars - nPub - 1;
-  if (s[3].size != (size_t)(nPub + 1) * 64 || s[5].size != (size_t)nVars * 64 || s[6].size != (size_t)nVars * 64 ||
-      s[7].size != (size_t)nVars * 128 || s[8].size != nC * 64 || s[9].size != (size_t)dom * 64)
-    return fail(ZKFL_E_MISMATCH, "zkey: section sizes do not match header");
-  // coefficients -> CSR
-  const uint8_t* cs = buf + s[4].off;
-  uint32_t ncoef;
-  memcpy(&ncoef, cs, 4);
-  if (s[4].size != 4 + (size_t)ncoef * 44) return fail(ZKFL_E_FORMAT, "zkey: coefficient section size");
-  std::vector<uint32_t> rowptr(2 * ((size_t)dom + 1), 0);
-  for (uint32_t i = 0; i < ncoef; i++) {
-    uint32_t mcs[3];
-    memcpy(mcs, cs + 4 + (size_t)i * 44, 12);
-    if (mcs[0] > 1 || mcs[1] >= dom || mcs[2] >= nVars) return fail(ZKFL_E_FORMAT, "zkey: coefficient out of range");
-    rowptr[mcs[0] * ((size_t)dom + 1) + mcs[1] + 1]++;
-  }
-  for (int m = 0; m < 2; m++) {
-    uint32_t* rp = rowptr.data() + m * ((size_t)dom + 1);
-    for (size_t j = 0; j < dom; j++) rp[j + 1] += rp[j];
-  }
-  // B rows are stored after A rows in one array: offset B by nnz(A)
-  const uint32_t nA = rowptr[dom];
-  for (size_t j = 0; j <= dom; j++) rowptr[dom + 1 + j] += nA;
-  std::vector<uint32_t> fill(rowptr.begin(), rowptr.end());
-  std::vector<uint32_t> cols(ncoef);
-  std::vector<uint32_t> coefs((size_t)ncoef * 8);
-  for (uint32_t i = 0; i < ncoef; i++) {
-    const uint8_t* e = cs + 4 + (size_t)i * 44;
-    uint32_t mcs[3];
-    memcpy(mcs, e, 12);
-    uint32_t pos = fill[mcs[0] * ((size_t)dom + 1) + mcs[1]]++;
-    cols[pos] = mcs[2];
-    memcpy(&coefs[(size_t)pos * 8], e + 12, 32);
-  }
-  // coefficient dictionary: pack col | index << cshift when both fit one u32
-  uint32_t cshift = 0;
+  ZkeyHost z;
   {
-    uint32_t colbits = 1;
-    while (colbits < 32 && (1ull << colbits) < nVars) colbits++;
-    struct K32 {
-      uint32_t v[8];
-      bool operator==(const K32& o) const { return memcmp(v, o.v, 32) == 0; }
-    };
-    struct H32 {
-      size_t operator()(const K32& k) const {
-        uint64_t h = 0x9E3779B97F4A7C15ull;
-        for (uint32_t x : k.v) h = (h ^ x) * 0x100000001B3ull;
-        return (size_t)(h ^ (h >> 29));
-      }
-    };
-    std::unordered_map<K32, uint32_t, H32> idx;
-    std::vector<uint32_t> dict;
-    std::vector<uint32_t> packed(ncoef);
-    bool ok = colbits < 32;
-    for (uint32_t p = 0; p < ncoef && ok; p++) {
-      K32 key;
-      memcpy(key.v, &coefs[(size_t)p * 8], 32);
-      auto it = idx.find(key);
-      uint32_t id;
-      if (it == idx.end()) {
-        id = (uint32_t)idx.size();
-        if ((uint64_t)id >= (1ull << (32 - colbits))) {
-          ok = false;
-          break;
-        }
-        idx.emplace(key, id);
-        dict.insert(dict.end(), &coefs[(size_t)p * 8], &coefs[(size_t)p * 8] + 8);
-      } else {
-        id = it->second;
-      }
-      packed[p] = cols[p] | (id << colbits);
-    }
-    if (ok && ncoef) {
-      cshift = colbits;
-      cols.swap(packed);
-      coefs.swap(dict);
-    }
+    std::string err;
+    int rc = zkey_parse(buf, len, z, err);  // csrc/host_parse.cc: header, sections, CSR + dictionary
+    if (rc) return fail(rc, err);
   }
-
+  const uint32_t nVars = z.nVars, nPub = z.nPub, dom = z.dom;
+  const int logn = z.logn;
+  const size_t nC = z.nC;
+  const size_t ncoef = z.ncoef;
+  const uint32_t cshift = z.cshift;
+  const std::vector<uint32_t>& rowptr = z.rowptr;
+  const std::vector<uint32_t>& cols = z.cols;
+  const std::vector<uint32_t>& coefs = z.coefs;
+  const uint8_t* pts = z.pts;
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   hipStream_t st = ctx->st;
   zkfl_key* k = new zkfl_key();
@@ -1180,11 +1106,11 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       if (d_img) (void)hipFree(d_img);
       return e;
     };
-    hipError_t e = build(k->bA, 64, buf + s[5].off, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
-    if (e == hipSuccess) e = build(k->bB1, 64, buf + s[6].off, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false);
-    if (e == hipSuccess) e = build(k->bB2, 128, buf + s[7].off, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false);
-    if (e == hipSuccess) e = build(k->bC, 64, buf + s[8].off, nC, nPub + 1, {{delta1, X + 3}}, false);
-    if (e == hipSuccess) e = build(k->bH, 64, buf + s[9].off, dom, 0, {}, true);
+    hipError_t e = build(k->bA, 64, z.secA, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
+    if (e == hipSuccess) e = build(k->bB1, 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false);
+    if (e == hipSuccess) e = build(k->bB2, 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false);
+    if (e == hipSuccess) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
+    if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, true);
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
@@ -1644,6 +1570,101 @@ int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const z
   }
   for (size_t j = 0; j < n; j++) out[j] = ws[j];
   return ZKFL_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Poseidon / vectorHash / Merkle trees (csrc/merkle.hip)
+// ---------------------------------------------------------------------------
+int zkfl_poseidon_params(uint32_t t, uint8_t* consts_out, uint8_t* xy_out, uint32_t* rp_out) {
+  if (t < 2 || t > 17) return fail(ZKFL_E_ARG, "poseidon width t must be in 2..17");
+  pos_params_raw(t, consts_out, xy_out);
+  if (rp_out) *rp_out = pos_rp(t);
+  return ZKFL_OK;
+}
+
+int zkfl_poseidon_batch(zkfl_ctx* ctx, uint32_t arity, size_t n, const uint8_t* inputs, uint8_t* out) {
+  if (!ctx || (n && (!inputs || !out))) return fail(ZKFL_E_ARG, "poseidon_batch: null argument");
+  if (arity < 1 || arity > POS_MAX_ARITY) return fail(ZKFL_E_ARG, "poseidon arity must be in 1..16");
+  int rc = check_fr_array(inputs, n * arity, "poseidon input");
+  if (rc || !n) return rc;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  if ((rc = pos_ready(ctx))) return rc;
+  DevBufs B;
+  Fr *d_in, *d_out;
+  HIP_TRY(B.get((void**)&d_in, n * arity * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_out, n * 32), "alloc");
+  hipStream_t st = ctx->st;
+  HIP_TRY(hipMemcpyAsync(d_in, inputs, n * arity * 32, hipMemcpyHostToDevice, st), "upload");
+  int pi = ctx->prof.begin("poseidon", st);
+  HIP_TRY(poseidon_batch(ctx->pos, arity, n, d_in, d_out, st), "poseidon");
+  ctx->prof.end(pi, st, (double)n);
+  HIP_TRY(hipMemcpyAsync(out, d_out, n * 32, hipMemcpyDeviceToHost, st), "download");
+  HIP_TRY(hipStreamSynchronize(st), "sync");
+  return ZKFL_OK;
+}
+
+int zkfl_vector_hash_batch(zkfl_ctx* ctx, uint32_t len, size_t n, const uint8_t* values, uint8_t* out) {
+  if (!ctx || (n && (!values || !out))) return fail(ZKFL_E_ARG, "vector_hash_batch: null argument");
+  if (len < 1 || len > VHASH_CHUNK * VHASH_CHUNK) return fail(ZKFL_E_ARG, "vector length must be in 1..256");
+  int rc = check_fr_array(values, n * len, "vector value");
+  if (rc || !n) return rc;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  if ((rc = pos_ready(ctx))) return rc;
+  DevBufs B;
+  Fr *d_in, *d_out, *d_s;
+  const size_t nch = (len + VHASH_CHUNK - 1) / VHASH_CHUNK;
+  HIP_TRY(B.get((void**)&d_in, n * len * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_out, n * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_s, n * nch * 32), "alloc");
+  hipStream_t st = ctx->st;
+  HIP_TRY(hipMemcpyAsync(d_in, values, n * len * 32, hipMemcpyHostToDevice, st), "upload");
+  int pi = ctx->prof.begin("vector_hash", st);
+  HIP_TRY(vector_hash_batch(ctx->pos, len, n, d_in, d_out, false, d_s, st), "vector hash");
+  ctx->prof.end(pi, st, (double)n);
+  HIP_TRY(hipMemcpyAsync(out, d_out, n * 32, hipMemcpyDeviceToHost, st), "download");
+  HIP_TRY(hipStreamSynchronize(st), "sync");
+  return ZKFL_OK;
+}
+
+int zkfl_merkle_build(zkfl_ctx* ctx, const uint8_t* leaves, size_t n, uint32_t depth, uint8_t* tree_out) {
+  int rc = tree_args(ctx, n, depth, leaves, tree_out);
+  if (rc) return rc;
+  if ((rc = check_fr_array(leaves, n, "leaf"))) return rc;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  if ((rc = pos_ready(ctx))) return rc;
+  DevBufs B;
+  Fr *d_raw, *d_leaves;
+  HIP_TRY(B.get((void**)&d_raw, n * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_leaves, n * 32), "alloc");
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(d_raw, leaves, n * 32, hipMemcpyHostToDevice, ctx->st), "upload");
+    HIP_TRY(fr_to_mont_batch(d_raw, n, d_leaves, ctx->st), "leaves");
+  }
+  return tree_from_device_leaves(ctx, B, d_leaves, n, depth, tree_out);
+}
+
+int zkfl_dataset_commit(zkfl_ctx* ctx, const uint8_t* values, size_t n, uint32_t len, uint32_t depth,
+                        uint8_t* tree_out) {
+  int rc = tree_args(ctx, n, depth, values, tree_out);
+  if (rc) return rc;
+  if (len < 1 || len > VHASH_CHUNK * VHASH_CHUNK) return fail(ZKFL_E_ARG, "vector length must be in 1..256");
+  if ((rc = check_fr_array(values, n * len, "sample value"))) return rc;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  if ((rc = pos_ready(ctx))) return rc;
+  DevBufs B;
+  Fr *d_in, *d_leaves, *d_s;
+  const size_t nch = (len + VHASH_CHUNK - 1) / VHASH_CHUNK;
+  HIP_TRY(B.get((void**)&d_in, n * len * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_leaves, n * 32), "alloc");
+  HIP_TRY(B.get((void**)&d_s, n * nch * 32), "alloc");
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(d_in, values, n * len * 32, hipMemcpyHostToDevice, ctx->st), "upload");
+    int pi = ctx->prof.begin("vector_hash", ctx->st);
+    HIP_TRY(vector_hash_batch(ctx->pos, len, n, d_in, d_leaves, true, d_s, ctx->st), "leaf hashes");
+    ctx->prof.end(pi, ctx->st, (double)n);
+  }
+  return tree_from_device_leaves(ctx, B, d_leaves, n, depth, tree_out);
 }
 
 }  // extern "C"

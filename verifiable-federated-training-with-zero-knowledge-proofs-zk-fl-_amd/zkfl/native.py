@@ -66,6 +66,11 @@ SIGNATURES = {
                                           C.POINTER(C.c_size_t)]),
     "zkfl_witness_compute_json": (C.c_int, [_P, _P, C.c_char_p, _U8P]),
     "zkfl_groth16_full_prove_batch": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P, _U8P]),
+    "zkfl_poseidon_params": (C.c_int, [C.c_uint32, _U8P, _U8P, C.POINTER(C.c_uint32)]),
+    "zkfl_poseidon_batch": (C.c_int, [_P, C.c_uint32, C.c_size_t, C.c_char_p, _U8P]),
+    "zkfl_vector_hash_batch": (C.c_int, [_P, C.c_uint32, C.c_size_t, C.c_char_p, _U8P]),
+    "zkfl_merkle_build": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, _U8P]),
+    "zkfl_dataset_commit": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, _U8P]),
     "zkfl_groth16_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_groth16_full_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_char_p),
                                                 C.c_char_p, _U8P, C.POINTER(_U8P)]),
@@ -98,6 +103,35 @@ def lib():
 def check(rc):
     if rc != ZKFL_OK:
         raise ZkflError(rc, lib().zkfl_last_error().decode(errors="replace"))
+
+
+def _frs(values) -> bytes:
+    return b"".join(int(v).to_bytes(32, "little") for v in values)
+
+
+def _ints(b: bytes) -> list:
+    return [int.from_bytes(b[i:i + 32], "little") for i in range(0, len(b), 32)]
+
+
+def _levels(flat, depth):
+    out, pos = [], 0
+    for lvl in range(depth + 1):
+        w = 1 << (depth - lvl)
+        out.append(flat[pos:pos + w])
+        pos += w
+    return out
+
+
+def poseidon_params(t: int):
+    """Host only (no device): circomlib's raw constants for width t from the library's own Grain
+    LFSR -> (round constants, x points, y points, R_P)."""
+    c = _buf(32 * (8 + 70) * t)     # R_P <= 70 for t <= 17
+    xy = _buf(64 * t)
+    rp = C.c_uint32()
+    check(lib().zkfl_poseidon_params(t, c, xy, C.byref(rp)))
+    consts = _ints(bytes(c))[:(8 + rp.value) * t]
+    pts = _ints(bytes(xy))
+    return consts, pts[:t], pts[t:], rp.value
 
 
 def device_count() -> int:
@@ -204,6 +238,47 @@ class Context:
         res = (C.c_int32 * max(1, n))()
         check(lib().zkfl_groth16_verify_batch(self.h, vk, len(vk), n, publics, npub, proofs, res))
         return [bool(res[i]) for i in range(n)]
+
+    # Poseidon / vectorHash / Merkle trees (the reference's data and server side)
+    def poseidon_batch(self, rows) -> list:
+        """[[ints] * arity] -> [Poseidon(row)] (circomlibjs poseidon, on the GPU)."""
+        if not rows:
+            return []
+        arity = len(rows[0])
+        assert all(len(r) == arity for r in rows)
+        out = _buf(32 * len(rows))
+        check(lib().zkfl_poseidon_batch(self.h, arity, len(rows), _frs(v for r in rows for v in r), out))
+        return _ints(bytes(out))
+
+    def vector_hash_batch(self, vectors) -> list:
+        """[[ints] * len] -> [vectorHash(v)] (tests/full_system_simulation.mjs:139-156)."""
+        if not vectors:
+            return []
+        ln = len(vectors[0])
+        assert all(len(v) == ln for v in vectors)
+        out = _buf(32 * len(vectors))
+        check(lib().zkfl_vector_hash_batch(self.h, ln, len(vectors), _frs(x for v in vectors for x in v), out))
+        return _ints(bytes(out))
+
+    def merkle_build(self, leaves, depth: int) -> list:
+        """buildMerkleTree(leaves, depth) -> the reference's `tree` (list of padded levels of ints)."""
+        out = _buf(32 * ((2 << depth) - 1))
+        check(lib().zkfl_merkle_build(self.h, _frs(leaves), len(leaves), depth, out))
+        return _levels(_ints(bytes(out)), depth)
+
+    def dataset_commit(self, samples, depth: int) -> list:
+        """computeDatasetCommitment: leaves = vectorHash(sample) on the device, then the tree."""
+        ln = len(samples[0]) if samples else 1
+        assert all(len(v) == ln for v in samples)
+        flat = self.dataset_commit_raw(_frs(x for v in samples for x in v), len(samples), ln, depth)
+        return _levels(_ints(flat), depth)
+
+    def dataset_commit_raw(self, values: bytes, n: int, ln: int, depth: int) -> bytes:
+        """Byte form: values n x ln x 32 B std -> the flattened padded tree ((2^(depth+1) - 1) x 32 B)."""
+        assert len(values) == 32 * n * ln
+        out = _buf(32 * ((2 << depth) - 1))
+        check(lib().zkfl_dataset_commit(self.h, values, n, ln, depth, out))
+        return bytes(out)
 
     # multi-key batches (one federated round: several circuits' proofs interleaved on one device)
     def prove_multi(self, jobs, rs: bytes | None = None) -> list:
