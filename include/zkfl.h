@@ -169,6 +169,12 @@ int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const z
 int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
                                   const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out);
 
+/* snarkjs `groth16.fullProve(input, wasm, zkey)` for one input.json text: parsed against the loaded
+ * program's signal table, then the full-prove pipeline above with n = 1.  pub_out: nPublic x 32 B
+ * or NULL.  Errors as zkfl_wprog_parse_inputs (ZKFL_E_ARG) and zkfl_groth16_full_prove_batch. */
+int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, const char* input_json,
+                                 const uint8_t* rs, uint8_t proof_out[256], uint8_t* pub_out);
+
 /* Multi-key full prove: job i = (keys[i], progs[i], inputs[i] = that program's input vector);
  * pubs_out[i] (or pubs_out NULL) receives keys[i]'s nPublic x 32 B.  Same error behaviour as
  * zkfl_groth16_full_prove_batch; the witness index in a ZKFL_E_CONSTRAINT message is the job index. */

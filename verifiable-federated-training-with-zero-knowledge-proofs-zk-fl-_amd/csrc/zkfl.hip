@@ -1253,6 +1253,18 @@ int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog
   });
 }
 
+int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, const char* input_json,
+                                 const uint8_t* rs, uint8_t proof_out[256], uint8_t* pub_out) {
+  if (!ctx || !key || !prog || !input_json || !proof_out) return fail(ZKFL_E_ARG, "full_prove_json: null argument");
+  std::vector<uint32_t> v;
+  std::string err;
+  int rc = wprog_inputs_json(prog->p, input_json, v, err);  // the loaded program's signal table
+  if (rc) return fail(rc, err);
+  v.resize(v.size() + 8);  // never empty (a circuit without inputs still proves one witness)
+  return zkfl_groth16_full_prove_batch(ctx, key, prog, 1, reinterpret_cast<const uint8_t*>(v.data()), rs, proof_out,
+                                       pub_out);
+}
+
 int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,
                                   const uint8_t* const* inputs, const uint8_t* rs, uint8_t* proofs_out,
                                   uint8_t* const* pubs_out) {

@@ -1,33 +1,50 @@
 #!/usr/bin/env node
-// snarkjs-compatible CLI/API shim over the N-API addon (zkfl.node -> libzkfl.so -> HIP).
+// snarkjs-compatible CLI/API over the N-API addon (zkfl.node -> libzkfl.so -> HIP).
 //
-// CLI (same argument order and files as the reference's execSync strings,
-// tests/full_system_simulation.mjs:773-776):
-//   node snarkjs_shim.js groth16 prove <circuit_final.zkey> <witness.wtns> <proof.json> <public.json>
-//   node snarkjs_shim.js groth16 verify <verification_key.json> <public.json> <proof.json>
-//   node snarkjs_shim.js wtns calculate <circuit.zkwp> <input.json> <witness.wtns>
-//     (snarkjs wtns calculate / generate_witness.cjs, :758-767; the .zkwp witness program image
-//      from `python -m zkfl compile` plays the role of the circuit's .wasm)
-//     (:865-868; exit 0 + "OK!" when valid, exit 1 + "Invalid proof" otherwise)
-// API (snarkjs shape):
-//   const { groth16 } = require('./snarkjs_shim.js');
-//   const { proof, publicSignals } = await groth16.prove(zkeyFileOrBuffer, wtnsFileOrBuffer);
-//   const ok = await groth16.verify(vKeyObject, publicSignals, proof);
-//   const wtnsBuffer = await wtns.calculate(inputObject, zkwpFileOrBuffer);
+// Installed as the `snarkjs` bin of package.json, so the reference harness's command strings resolve
+// to it unchanged (`npx snarkjs ...` with cwd = the circuit directory):
+//   snarkjs groth16 prove <circuit_final.zkey> <witness.wtns> <proof.json> <public.json>
+//       (tests/full_system_simulation.mjs:773-776)
+//   snarkjs groth16 verify <verification_key.json> <public.json> <proof.json>
+//       (:865-868; exit 0 + "OK!" when valid, exit 1 + "Invalid proof" otherwise)
+//   snarkjs groth16 fullprove <input.json> <circuit.wasm> <circuit_final.zkey> <proof.json> <public.json>
+//   snarkjs wtns calculate <circuit.wasm> <input.json> <witness.wtns>   (tests/test_secureagg.cjs:108-118)
+//   snarkjs zkey export verificationkey <circuit_final.zkey> <vkey.json>  (:732-735)
+//   snarkjs r1cs info <circuit.r1cs>                                    (tests/test_verified_gradient.mjs:351-356)
+// "circuit.wasm" is the witness-program image `python -m zkfl compile --circom-layout` writes under
+// the .wasm name (magic "zkwp"); a real circom .wasm is accepted when `<circuit>.zkwp` sits beside it.
+//
+// API (snarkjs shape, Promise-based):
+//   const { groth16, wtns, zKey, r1cs } = require('zkfl-snarkjs');
+//   const { proof, publicSignals } = await groth16.fullProve(input, 'c_js/c.wasm', 'c_final.zkey');
+//   const { proof, publicSignals } = await groth16.prove('c_final.zkey', 'w.wtns');
+//   const ok = await groth16.verify(vKey, publicSignals, proof);
+//   const wtnsBuffer = await wtns.calculate(input, 'c_js/c.wasm');
+//   const vKey = await zKey.exportVerificationKey('c_final.zkey');
+//   const info = await r1cs.info('c.r1cs');
 'use strict';
 const fs = require('fs');
 const path = require('path');
 
 const addon = require(path.join(__dirname, 'zkfl.node'));
 
+const Q = BigInt('21888242871839275222246405745257275088696311157297823662689037894645226208583');
 let ctx = null;
 const keys = new Map();
+const progs = new Map();
 
-function leToDec(buf, off) {
+function context() {
+  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
+  return ctx;
+}
+
+function leToBig(buf, off) {
   let v = BigInt(0);
   for (let i = 31; i >= 0; i--) v = (v << BigInt(8)) | BigInt(buf[off + i]);
-  return v.toString();
+  return v;
 }
+
+function leToDec(buf, off) { return leToBig(buf, off).toString(); }
 
 function proofToJson(p) {
   const v = [];
@@ -41,20 +58,64 @@ function proofToJson(p) {
   };
 }
 
+function publicToJson(buf) {
+  const pub = [];
+  for (let i = 0; i < buf.length / 32; i++) pub.push(leToDec(buf, 32 * i));
+  return pub;
+}
+
 function read(x) { return Buffer.isBuffer(x) ? x : fs.readFileSync(x); }
 
-async function prove(zkey, wtns) {
-  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
+function key(zkey) {
   const id = Buffer.isBuffer(zkey) ? zkey : path.resolve(zkey);
-  let key = keys.get(id);
-  if (!key) {
-    key = addon.loadKey(ctx, read(zkey));
-    keys.set(id, key);
+  let k = keys.get(id);
+  if (!k) {
+    k = addon.loadKey(context(), read(zkey));
+    keys.set(id, k);
   }
-  const r = await addon.prove(ctx, key, read(wtns));
-  const pub = [];
-  for (let i = 0; i < r.publicSignals.length / 32; i++) pub.push(leToDec(r.publicSignals, 32 * i));
-  return { proof: proofToJson(r.proof), publicSignals: pub };
+  return k;
+}
+
+// The circuit's witness program: the image itself, or a compiled .zkwp beside a circom .wasm.
+function programImage(wasm) {
+  if (Buffer.isBuffer(wasm)) return wasm;
+  const buf = fs.readFileSync(wasm);
+  if (buf.length >= 4 && buf.toString('latin1', 0, 4) === 'zkwp') return buf;
+  const stem = path.basename(wasm).replace(/\.wasm$/, '');
+  for (const d of [path.dirname(wasm), path.dirname(path.dirname(wasm))]) {
+    const cand = path.join(d, stem + '.zkwp');
+    if (fs.existsSync(cand)) return fs.readFileSync(cand);
+  }
+  throw new Error(`${wasm}: a circom WASM witness calculator; compile the circuit with ` +
+                  '`python -m zkfl compile --circom-layout` (or place <circuit>.zkwp beside it)');
+}
+
+function program(wasm) {
+  const id = Buffer.isBuffer(wasm) ? wasm : path.resolve(wasm);
+  let p = progs.get(id);
+  if (!p) {
+    p = addon.loadProgram(context(), programImage(wasm));
+    progs.set(id, p);
+  }
+  return p;
+}
+
+function inputText(input) {
+  if (typeof input === 'string') return input;
+  return JSON.stringify(input, (k, v) => (typeof v === 'bigint' ? v.toString() : v));
+}
+
+async function prove(zkey, wtnsFile) {
+  const r = await addon.prove(context(), key(zkey), read(wtnsFile));
+  return { proof: proofToJson(r.proof), publicSignals: publicToJson(r.publicSignals) };
+}
+
+// snarkjs groth16.fullProve(input, wasmFile, zkeyFileName): the witness is computed on the GPU
+// straight into HBM and proven there (zkfl_groth16_full_prove_json); nothing but the proof and
+// the public signals comes back.
+async function fullProve(input, wasmFile, zkeyFileName) {
+  const r = await addon.fullProve(context(), key(zkeyFileName), program(wasmFile), inputText(input));
+  return { proof: proofToJson(r.proof), publicSignals: publicToJson(r.publicSignals) };
 }
 
 function decToLe(x) {
@@ -84,58 +145,137 @@ function vkBuffer(vk) {
 }
 
 async function verify(vk, publicSignals, proof) {
-  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
   const pr = Buffer.concat([g1Buf(proof.pi_a), g2Buf(proof.pi_b), g1Buf(proof.pi_c)]);
   const pub = Buffer.concat(publicSignals.map(decToLe).concat([Buffer.alloc(0)]));
-  return addon.verify(ctx, vkBuffer(vk), pub, pr);
+  return addon.verify(context(), vkBuffer(vk), pub, pr);
 }
 
-const progs = new Map();
+async function wtnsCalculate(input, wasm) {
+  return addon.witness(context(), program(wasm), inputText(input));
+}
 
-async function wtnsCalculate(input, zkwp) {
-  if (ctx === null) ctx = addon.createContext(parseInt(process.env.LOCAL_RANK || '0', 10));
-  const id = Buffer.isBuffer(zkwp) ? zkwp : path.resolve(zkwp);
-  let prog = progs.get(id);
-  if (!prog) {
-    prog = addon.loadProgram(ctx, read(zkwp));
-    progs.set(id, prog);
+// --- iden3 binfile readers for the setup-side commands (SURVEY.md Appendix A) ---
+function sections(buf, magic) {
+  if (buf.length < 12 || buf.toString('latin1', 0, 4) !== magic) throw new Error(`not a ${magic} file`);
+  const n = buf.readUInt32LE(8);
+  const out = {};
+  let off = 12;
+  for (let i = 0; i < n; i++) {
+    if (off + 12 > buf.length) throw new Error('truncated section header');
+    const type = buf.readUInt32LE(off);
+    const size = Number(buf.readBigUInt64LE(off + 4));
+    off += 12;
+    if (size > buf.length - off) throw new Error('truncated section');
+    if (!(type in out)) out[type] = buf.subarray(off, off + size);
+    off += size;
   }
-  const text = typeof input === 'string' ? input : JSON.stringify(input, (k, v) => (typeof v === 'bigint' ? v.toString() : v));
-  return addon.witness(ctx, prog, text);
+  return out;
 }
 
-module.exports = { groth16: { prove, verify }, wtns: { calculate: wtnsCalculate }, addon, proofToJson, vkBuffer };
+function modpow(b, e, m) {
+  let r = BigInt(1);
+  b %= m;
+  while (e > BigInt(0)) {
+    if (e & BigInt(1)) r = (r * b) % m;
+    b = (b * b) % m;
+    e >>= BigInt(1);
+  }
+  return r;
+}
+
+// snarkjs `zkey export verificationkey`: zkey section 2 points are Montgomery form over q.
+async function exportVerificationKey(zkeyFile) {
+  const s = sections(read(zkeyFile), 'zkey');
+  const h = s[2];
+  if (!h || h.length < 84 + 64 * 3 + 128 * 3 || !s[3]) throw new Error('zkey: header');
+  const rinv = modpow(BigInt(2) ** BigInt(256) % Q, Q - BigInt(2), Q);
+  const fq = (b, o) => ((leToBig(b, o) * rinv) % Q);
+  const g1 = (b, o) => {
+    const x = fq(b, o), y = fq(b, o + 32);
+    return x === BigInt(0) && y === BigInt(0) ? ['0', '1', '0'] : [x.toString(), y.toString(), '1'];
+  };
+  const g2 = (b, o) => [[fq(b, o).toString(), fq(b, o + 32).toString()],
+    [fq(b, o + 64).toString(), fq(b, o + 96).toString()], ['1', '0']];
+  const nPublic = h.readUInt32LE(76);
+  const p = 84;  // alpha1 64 | beta1 64 | beta2 128 | gamma2 128 | delta1 64 | delta2 128
+  const vk = {
+    protocol: 'groth16', curve: 'bn128', nPublic,
+    vk_alpha_1: g1(h, p), vk_beta_2: g2(h, p + 128), vk_gamma_2: g2(h, p + 256), vk_delta_2: g2(h, p + 448),
+  };
+  const gt = addon.pairing(context(), g1Buf(vk.vk_alpha_1), g2Buf(vk.vk_beta_2));   // e(alpha1, beta2) on the GPU
+  const v = [];
+  for (let i = 0; i < 12; i++) v.push(leToDec(gt, 32 * i));
+  vk.vk_alphabeta_12 = [0, 1].map((i) => [0, 1, 2].map((j) => v.slice(6 * i + 2 * j, 6 * i + 2 * j + 2)));
+  vk.IC = [];
+  for (let i = 0; i <= nPublic; i++) vk.IC.push(g1(s[3], 64 * i));
+  return vk;
+}
+
+// snarkjs `r1cs info`: header section 1 of the .r1cs (iden3 r1cs v1)
+async function r1csInfo(r1csFile) {
+  const h = sections(read(r1csFile), 'r1cs')[1];
+  if (!h || h.length < 4) throw new Error('r1cs: header');
+  const n8 = h.readUInt32LE(0);
+  const o = 4 + n8;
+  return {
+    curve: 'bn-128', nVars: h.readUInt32LE(o), nOutputs: h.readUInt32LE(o + 4), nPubInputs: h.readUInt32LE(o + 8),
+    nPrvInputs: h.readUInt32LE(o + 12), nLabels: Number(h.readBigUInt64LE(o + 16)), nConstraints: h.readUInt32LE(o + 24),
+  };
+}
+
+module.exports = {
+  groth16: { prove, fullProve, verify },
+  wtns: { calculate: wtnsCalculate },
+  zKey: { exportVerificationKey },
+  r1cs: { info: r1csInfo },
+  addon, proofToJson, vkBuffer,
+};
+
+function done(p) {
+  p.then((code) => process.exit(code || 0)).catch((e) => { console.error('[ERROR] snarkJS: ' + e.message); process.exit(1); });
+}
 
 if (require.main === module) {
-  const [cmd, sub, zkeyF, wtnsF, proofF, publicF] = process.argv.slice(2);
-  if (cmd === 'groth16' && sub === 'prove' && publicF) {
-    prove(zkeyF, wtnsF).then(({ proof, publicSignals }) => {
-      fs.writeFileSync(proofF, JSON.stringify(proof, null, 1));
-      fs.writeFileSync(publicF, JSON.stringify(publicSignals, null, 1));
-      process.exit(0);
-    }).catch((e) => { console.error(e.message); process.exit(1); });
-  } else if (cmd === 'groth16' && sub === 'verify' && proofF) {
-    // argument order: verify <vkey.json> <public.json> <proof.json>
-    const [vkF, pubF, prF] = [zkeyF, wtnsF, proofF];
+  const a = process.argv.slice(2).filter((x) => !x.startsWith('-'));
+  const [cmd, sub] = a;
+  const w = (f, o) => fs.writeFileSync(f, JSON.stringify(o, null, 1));
+  if (cmd === 'groth16' && sub === 'prove' && a.length >= 6) {
+    done(prove(a[2], a[3]).then(({ proof, publicSignals }) => { w(a[4], proof); w(a[5], publicSignals); }));
+  } else if (cmd === 'groth16' && sub === 'fullprove' && a.length >= 7) {
+    done(fullProve(fs.readFileSync(a[2], 'utf8'), a[3], a[4]).then(({ proof, publicSignals }) => {
+      w(a[5], proof);
+      w(a[6], publicSignals);
+    }));
+  } else if (cmd === 'groth16' && sub === 'verify' && a.length >= 5) {
     const rd = (f) => JSON.parse(fs.readFileSync(f, 'utf8'));
-    verify(rd(vkF), rd(pubF), rd(prF)).then((ok) => {
-      if (ok) { console.log('[INFO]  snarkJS: OK!'); process.exit(0); }
+    done(verify(rd(a[2]), rd(a[3]), rd(a[4])).then((ok) => {
+      if (ok) { console.log('[INFO]  snarkJS: OK!'); return 0; }
       console.error('[ERROR] snarkJS: Invalid proof');
-      process.exit(1);
-    }).catch((e) => { console.error(e.message); process.exit(1); });
-  } else if (cmd === 'wtns' && sub === 'calculate' && proofF) {
-    // argument order: wtns calculate <circuit.zkwp> <input.json> <out.wtns>
-    const [progF, inputF, outF] = [zkeyF, wtnsF, proofF];
-    wtnsCalculate(fs.readFileSync(inputF, 'utf8'), progF).then((w) => {
-      fs.writeFileSync(outF, w);
-      process.exit(0);
-    }).catch((e) => { console.error(e.message); process.exit(1); });
-  } else if (cmd === 'version') {
-    console.log('zkfl ' + addon.version());
+      return 1;
+    }));
+  } else if (cmd === 'wtns' && sub === 'calculate' && a.length >= 5) {
+    done(wtnsCalculate(fs.readFileSync(a[3], 'utf8'), a[2]).then((buf) => fs.writeFileSync(a[4], buf)));
+  } else if (cmd === 'zkey' && sub === 'export' && a[2] === 'verificationkey' && a.length >= 5) {
+    done(exportVerificationKey(a[3]).then((vk) => w(a[4], vk)));
+  } else if (cmd === 'r1cs' && sub === 'info' && a.length >= 3) {
+    done(r1csInfo(a[2]).then((i) => {
+      console.log(`[INFO]  snarkJS: Curve: ${i.curve}`);
+      console.log(`[INFO]  snarkJS: # of Wires: ${i.nVars}`);
+      console.log(`[INFO]  snarkJS: # of Constraints: ${i.nConstraints}`);
+      console.log(`[INFO]  snarkJS: # of Private Inputs: ${i.nPrvInputs}`);
+      console.log(`[INFO]  snarkJS: # of Public Inputs: ${i.nPubInputs}`);
+      console.log(`[INFO]  snarkJS: # of Labels: ${i.nLabels}`);
+      console.log(`[INFO]  snarkJS: # of Outputs: ${i.nOutputs}`);
+    }));
+  } else if (cmd === 'version' || process.argv.includes('--version')) {
+    console.log('zkfl-snarkjs (libzkfl ABI ' + addon.version() + ')');
   } else {
-    console.error('usage: snarkjs_shim.js groth16 prove <zkey> <wtns> <proof.json> <public.json>\n' +
-                  '       snarkjs_shim.js groth16 verify <vkey.json> <public.json> <proof.json>\n' +
-                  '       snarkjs_shim.js wtns calculate <circuit.zkwp> <input.json> <out.wtns>');
+    console.error('usage: snarkjs groth16 prove <zkey> <wtns> <proof.json> <public.json>\n' +
+                  '       snarkjs groth16 fullprove <input.json> <circuit.wasm> <zkey> <proof.json> <public.json>\n' +
+                  '       snarkjs groth16 verify <vkey.json> <public.json> <proof.json>\n' +
+                  '       snarkjs wtns calculate <circuit.wasm> <input.json> <out.wtns>\n' +
+                  '       snarkjs zkey export verificationkey <zkey> <vkey.json>\n' +
+                  '       snarkjs r1cs info <circuit.r1cs>');
     process.exit(99);
   }
 }

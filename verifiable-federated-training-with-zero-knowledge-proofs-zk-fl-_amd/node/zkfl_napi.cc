@@ -16,6 +16,9 @@
 //   verify(ctx, vkBuffer, publicBuffer, proofBuffer) -> Promise<boolean>   (zkfl_groth16_verify)
 //   loadProgram(ctx, zkwpBuffer) -> prog                                   (zkfl_wprog_load)
 //   witness(ctx, prog, inputJsonString) -> Promise<Buffer(.wtns)>          (zkfl_witness_compute_json)
+//   fullProve(ctx, key, prog, inputJsonString[, rsBuffer])
+//       -> Promise<{proof: Buffer(256), publicSignals: Buffer}>           (zkfl_groth16_full_prove_json)
+//   pairing(ctx, g1Buffer(64), g2Buffer(128)) -> Buffer(384)              (zkfl_pairing, vk_alphabeta_12)
 #include <node_api.h>
 
 #include <cstring>
@@ -321,6 +324,106 @@ napi_value Witness(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+// snarkjs groth16.fullProve: input.json -> witness on the GPU -> proof, one call (the witness never
+// leaves the device; tests/full_system_simulation.mjs:758-776 as two child processes in the reference)
+struct FullProveWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  zkfl_ctx* ctx = nullptr;
+  zkfl_key* key = nullptr;
+  zkfl_wprog* prog = nullptr;
+  std::string json;
+  std::vector<uint8_t> rs, pub;
+  uint8_t proof[256];
+  uint32_t npub = 0;
+  int rc = 0;
+  std::string err;
+};
+
+void full_prove_execute(napi_env, void* data) {
+  FullProveWork* w = static_cast<FullProveWork*>(data);
+  uint32_t nv = 0, dom = 0;
+  zkfl_key_info(w->key, &nv, &w->npub, &dom);
+  w->pub.resize((size_t)w->npub * 32 + 32);
+  w->rc = zkfl_groth16_full_prove_json(w->ctx, w->key, w->prog, w->json.c_str(), w->rs.empty() ? nullptr : w->rs.data(),
+                                       w->proof, w->pub.data());
+  if (w->rc) w->err = zkfl_last_error();
+}
+
+void full_prove_complete(napi_env env, napi_status, void* data) {
+  FullProveWork* w = static_cast<FullProveWork*>(data);
+  if (w->rc) {
+    napi_value msg, err;
+    std::string m = "zkfl fullProve failed (" + std::to_string(w->rc) + "): " + w->err;
+    napi_create_string_utf8(env, m.c_str(), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_reject_deferred(env, w->deferred, err);
+  } else {
+    napi_value obj, proof, pub;
+    void* p;
+    napi_create_buffer_copy(env, 256, w->proof, &p, &proof);
+    napi_create_buffer_copy(env, (size_t)w->npub * 32, w->pub.data(), &p, &pub);
+    napi_create_object(env, &obj);
+    napi_set_named_property(env, obj, "proof", proof);
+    napi_set_named_property(env, obj, "publicSignals", pub);
+    napi_resolve_deferred(env, w->deferred, obj);
+  }
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+napi_value FullProve(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *key = nullptr, *prog = nullptr, *rs = nullptr;
+  size_t jlen = 0, rslen = 0;
+  if (argc < 4 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_value_external(env, argv[1], &key) != napi_ok ||
+      napi_get_value_external(env, argv[2], &prog) != napi_ok ||
+      napi_get_value_string_utf8(env, argv[3], nullptr, 0, &jlen) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "fullProve(ctx, key, prog, inputJsonString[, rsBuffer])");
+    return nullptr;
+  }
+  FullProveWork* w = new FullProveWork();
+  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->key = static_cast<zkfl_key*>(key);
+  w->prog = static_cast<zkfl_wprog*>(prog);
+  w->json.resize(jlen + 1);
+  napi_get_value_string_utf8(env, argv[3], &w->json[0], jlen + 1, &jlen);
+  w->json.resize(jlen);
+  if (argc >= 5 && napi_get_buffer_info(env, argv[4], &rs, &rslen) == napi_ok && rslen == 64)
+    w->rs.assign(static_cast<uint8_t*>(rs), static_cast<uint8_t*>(rs) + 64);
+  napi_value promise, name;
+  napi_create_promise(env, &w->deferred, &promise);
+  napi_create_string_utf8(env, "zkfl_full_prove", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, nullptr, name, full_prove_execute, full_prove_complete, w, &w->work);
+  napi_queue_async_work(env, w->work);
+  return promise;
+}
+
+napi_value Pairing(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *g1 = nullptr, *g2 = nullptr;
+  size_t l1 = 0, l2 = 0;
+  if (argc < 3 || napi_get_value_external(env, argv[0], &ctx) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &g1, &l1) != napi_ok || napi_get_buffer_info(env, argv[2], &g2, &l2) != napi_ok ||
+      l1 != 64 || l2 != 128) {
+    napi_throw_type_error(env, nullptr, "pairing(ctx, g1Buffer(64), g2Buffer(128))");
+    return nullptr;
+  }
+  uint8_t gt[384];
+  int rc = zkfl_pairing(static_cast<zkfl_ctx*>(ctx), 1, static_cast<const uint8_t*>(g1),
+                        static_cast<const uint8_t*>(g2), gt);
+  if (rc) return throw_err(env, rc);
+  napi_value buf;
+  void* p;
+  napi_create_buffer_copy(env, 384, gt, &p, &buf);
+  return buf;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -332,6 +435,8 @@ napi_value Init(napi_env env, napi_value exports) {
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"loadProgram", nullptr, LoadProgram, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"witness", nullptr, Witness, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"fullProve", nullptr, FullProve, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"pairing", nullptr, Pairing, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

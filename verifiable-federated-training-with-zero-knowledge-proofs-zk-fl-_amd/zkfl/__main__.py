@@ -2,6 +2,9 @@
 
     python -m zkfl compile <circuit> [params..] [-o DIR]    circom <c>.circom --r1cs --wasm
         -> DIR/<name>.r1cs, DIR/<name>.zkwp (witness program: the .wasm's role)
+        --circom-layout: also DIR/<name>_js/<name>.wasm (the witness-program image under circom's
+        name) + DIR/<name>_js/generate_witness.cjs, so the harness's
+        `node <name>_js/generate_witness.cjs <name>_js/<name>.wasm in.json out.wtns` runs unchanged
     python -m zkfl info <circuit> [params..]                 snarkjs r1cs info (tests/test_verified_gradient.mjs:351-356)
     python -m zkfl setup <circuit> [params..] [-o DIR]       snarkjs groth16 setup + zkey contribute + zkey export
         -> DIR/<name>_final.zkey, DIR/verification_key.json  verificationkey (tests/full_system_simulation.mjs:713-735)
@@ -46,6 +49,15 @@ def cmd_compile(args):
         f.write(b.r1cs_bytes())
     with open(os.path.join(args.out, name + ".zkwp"), "wb") as f:
         f.write(wprog.compile_program(b))
+    if args.circom_layout:
+        js = os.path.join(args.out, name + "_js")
+        os.makedirs(js, exist_ok=True)
+        with open(os.path.join(js, name + ".wasm"), "wb") as f:
+            f.write(wprog.compile_program(b))
+        gen = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "node", "generate_witness.cjs")
+        with open(os.path.join(js, "generate_witness.cjs"), "w") as f:
+            f.write("// written by `python -m zkfl compile --circom-layout`: circom's generate_witness.cjs over libzkfl\n"
+                    f"require({json.dumps(gen)}).main(process.argv.slice(2));\n")
     print(f"template instances: {args.circuit}{tuple(args.params)}")
     print(f"non-linear constraints: {b.n_constraints}")
     print(f"wires: {b.n_wires}")
@@ -126,7 +138,10 @@ def main(argv=None):
         if out:
             sp.add_argument("-o", "--out", default=".")
 
-    circuit_args(sub.add_parser("compile"), out=True)
+    sp = sub.add_parser("compile")
+    circuit_args(sp, out=True)
+    sp.add_argument("--circom-layout", action="store_true",
+                    help="also write <name>_js/<name>.wasm + generate_witness.cjs (circom's output layout)")
     circuit_args(sub.add_parser("info"))
     circuit_args(sub.add_parser("setup"), out=True)
     sp = sub.add_parser("export-vk")

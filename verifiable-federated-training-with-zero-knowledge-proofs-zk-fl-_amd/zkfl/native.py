@@ -71,6 +71,7 @@ SIGNATURES = {
     "zkfl_vector_hash_batch": (C.c_int, [_P, C.c_uint32, C.c_size_t, C.c_char_p, _U8P]),
     "zkfl_merkle_build": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, _U8P]),
     "zkfl_dataset_commit": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, _U8P]),
+    "zkfl_groth16_full_prove_json": (C.c_int, [_P, _P, _P, C.c_char_p, C.c_char_p, _U8P, _U8P]),
     "zkfl_groth16_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_groth16_full_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_char_p),
                                                 C.c_char_p, _U8P, C.POINTER(_U8P)]),
@@ -388,6 +389,13 @@ class ProvingKey:
         return [(ob[256 * i:256 * i + 256],
                  [int.from_bytes(pb[32 * (i * k + j):32 * (i * k + j) + 32], "little") for j in range(k)])
                 for i in range(n)]
+
+    def full_prove_json(self, prog: "WitnessProgram", input_json: str, rs: bytes | None = None):
+        """snarkjs groth16.fullProve for one input.json text -> (proof 256 B, [public ints])."""
+        out = _buf(256)
+        pub = _buf(32 * max(1, self.n_public))
+        check(lib().zkfl_groth16_full_prove_json(self.ctx.h, self.h, prog.h, input_json.encode(), rs, out, pub))
+        return bytes(out), _ints(bytes(pub))[:self.n_public]
 
     def debug_parts(self, wtns: bytes):
         """-> (h list of ints, dict of MSM results as std affine bytes)"""
