@@ -175,6 +175,17 @@ int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog
 int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, const char* input_json,
                                  const uint8_t* rs, uint8_t proof_out[256], uint8_t* pub_out);
 
+/* snarkjs `groth16.fullProve` over n input.json texts (the reference runs one fullProve /
+ * `generate_witness.cjs` + `groth16 prove` pair per client, tests/full_system_simulation.mjs:758-776):
+ * host worker threads parse the texts against the program's signal table ahead of the slot
+ * scheduler (at most 64 parsed vectors held), so parsing overlaps the proofs in flight; then the
+ * zkfl_groth16_full_prove_batch pipeline.  Errors: a text that does not parse or does not fill
+ * the program's inputs gives ZKFL_E_ARG naming its index (proofs before it are complete);
+ * otherwise as zkfl_groth16_full_prove_batch. */
+int zkfl_groth16_full_prove_json_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                                       const char* const* input_jsons, const uint8_t* rs, uint8_t* proofs_out,
+                                       uint8_t* pubs_out);
+
 /* Multi-key full prove: job i = (keys[i], progs[i], inputs[i] = that program's input vector);
  * pubs_out[i] (or pubs_out NULL) receives keys[i]'s nPublic x 32 B.  Same error behaviour as
  * zkfl_groth16_full_prove_batch; the witness index in a ZKFL_E_CONSTRAINT message is the job index. */

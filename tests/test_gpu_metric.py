@@ -136,6 +136,49 @@ def test_metric_full_prove_pipeline(metric):
         r_.close()
 
 
+def test_metric_full_prove_json_batch(metric):
+    """zkfl_groth16_full_prove_json_batch: input.json texts parsed by host threads while earlier
+    proofs run; 44 proofs at 20 slots equal the vector pipeline's (same r, s) proof by proof."""
+    import json
+    from zkfl import circuits, clients, wprog
+    _, _, key, wp, _ = metric
+    b = circuits.build("sgd_verified", *PARAMS)
+    objs = [clients.Client(cid, 128, 4, 7, clients.JsLcg(12345 + cid)).training_input(128, 1000, 100000000)[0]
+            for cid in (1, 2, 3, 4)]
+    texts = [json.dumps(o) for o in objs]
+    n = 44
+    rs = [_le(secrets.randbelow(R)) + _le(secrets.randbelow(R)) for _ in range(n)]
+    key.set_slots(20)
+    got = key.full_prove_json_batch(wp, [texts[i % 4] for i in range(n)], b"".join(rs))
+    want = key.full_prove_batch(wp, [wprog.input_bytes(b, objs[i % 4]) for i in range(n)], b"".join(rs))
+    key.set_slots(3)
+    assert got == want
+
+
+def test_full_prove_json_batch_errors(gpu_ctx):
+    """A malformed / incomplete text at index k: ZKFL_E_ARG naming input k; the key keeps working."""
+    import json
+    from zkfl import circuits, clients, native, wprog, zkey
+    b = circuits.build("sgd_verified", 8, 4, 3, 1000)
+    zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(tau=98, alpha=2, beta=3, gamma=4, delta=5))
+    key = native.ProvingKey(gpu_ctx, zk)
+    wp = native.WitnessProgram(gpu_ctx, wprog.compile_program(b))
+    good = [json.dumps(clients.Client(c, 8, 4, 3, clients.JsLcg(12345 + c)).training_input(8, 1000, 100000000)[0])
+            for c in (1, 2)]
+    missing = json.loads(good[0])
+    del missing["remainder"]
+    key.set_slots(4)
+    for bad in ('{"client_id": 1', json.dumps(missing)):
+        with pytest.raises(native.ZkflError) as e:
+            key.full_prove_json_batch(wp, [good[0], good[1], good[0], bad, good[1]])
+        assert e.value.code == -1 and "input 3" in str(e.value)
+    rs = _le(5) + _le(6)
+    (p, pub), = key.full_prove_json_batch(wp, [good[1]], rs)
+    assert (p, pub) == key.full_prove_batch(wp, [native.parse_inputs(wprog.compile_program(b), good[1])], rs)[0]
+    wp.close()
+    key.close()
+
+
 def test_full_prove_constraint_failure_and_recovery(gpu_ctx):
     """One unsatisfiable witness in a batch: ZKFL_E_CONSTRAINT names it; the key keeps working."""
     from zkfl import circuits, clients, native, wprog, zkey

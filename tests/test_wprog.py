@@ -179,3 +179,23 @@ def test_c_input_json_parser_values_and_errors():
     with pytest.raises(native.ZkflError) as e:
         native.parse_inputs(img[:-8], '{"left": 1, "right": 2}')
     assert e.value.code == -2
+
+
+def test_c_input_json_parser_literal_sweep():
+    """Chunked literal reduction (host_parse.cc literal_to_fr): every digit count from 1 to 200,
+    decimal and hex, both signs, values around multiples of r and powers of two, == Python mod r."""
+    import random
+    from zkfl import native
+    b = circuits.build("poseidon_hash2")
+    img = wprog.compile_program(b)
+    rnd = random.Random(7)
+    vals = [0, 1, R - 1, R, R + 1, 2 * R - 1, 5 * R + 7, 2 ** 256 - 1, 2 ** 254, 10 ** 18 - 1, 10 ** 18,
+            10 ** 36, 16 ** 15 - 1, 16 ** 15, 2 ** 320 + 3, 2 ** 640 - 1, (2 ** 256 // R) * R, (2 ** 320 // R) * R - 1]
+    vals += [rnd.randrange(10 ** (d - 1), 10 ** d) for d in range(1, 201)]
+    vals += [rnd.randrange(16 ** (d - 1), 16 ** d) for d in range(1, 120, 3)]
+    for i in range(0, len(vals), 2):
+        x, y = vals[i], vals[(i + 1) % len(vals)]
+        for lx, ly in ((str(x), "-" + str(y)), (hex(x), "-" + hex(y)), ("-" + str(x), "+" + hex(y).upper().replace("0X", "0x"))):
+            text = '{"left": "%s", "right": "%s"}' % (lx, ly)
+            want = b"".join((int(v, 0) % R).to_bytes(32, "little") for v in (lx, ly))
+            assert native.parse_inputs(img, text) == want, text

@@ -303,7 +303,9 @@ ZK_DEV Fp<PR> fp_from_mont(const Fp<PR>& a) {
 template <class PR>
 ZK_DEV Fp<PR> fp_pow(const Fp<PR>& a, const uint32_t e[8]) {
   Fp<PR> r = fp_one<PR>();
-  for (int i = 7; i >= 0; i--) {
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {  // constant limb index: e stays in registers
+#pragma unroll 1
     for (int b = 31; b >= 0; b--) {
       r = fp_sqr<PR>(r);
       if ((e[i] >> b) & 1u) r = fp_mul<PR>(r, a);

@@ -160,7 +160,10 @@ struct JParser {
   }
 };
 
-// decimal / 0x-hex integer literal (optional sign) -> std-form Fr limbs (mod r)
+// decimal / 0x-hex integer literal (optional sign) -> std-form Fr limbs (mod r).  Digits are
+// consumed in chunks of 18 (decimal) / 15 (hex) into a value kept below r: acc = acc * base^len +
+// chunk (< r * 2^60 < 2^314), then reduced with a quotient estimated from its top 128 bits over
+// r's top word plus one (never above the true quotient, at most 2 short), and <= 3 subtractions.
 bool literal_to_fr(const std::string& t, uint32_t out[8]) {
   static const uint64_t RL[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
                                  0x30644e72e131a029ull};
@@ -173,38 +176,49 @@ bool literal_to_fr(const std::string& t, uint32_t out[8]) {
     i += 2;
   }
   if (i >= t.size()) return false;
-  uint64_t acc[5] = {0, 0, 0, 0, 0};  // < 16 r + 15 < 2^259 before reduction
-  for (; i < t.size(); i++) {
-    const char ch = t[i];
-    unsigned d;
-    if (ch >= '0' && ch <= '9') d = ch - '0';
-    else if (base == 16 && ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
-    else if (base == 16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
-    else return false;  // fractions / exponents are not field elements
-    unsigned __int128 c = d;
+  const size_t per = base == 10 ? 18 : 15;  // base^per <= 2^60
+  uint64_t acc[5] = {0, 0, 0, 0, 0};
+  auto ge_r = [&]() {
+    if (acc[4]) return true;
+    for (int k = 3; k >= 0; k--)
+      if (acc[k] != RL[k]) return acc[k] > RL[k];
+    return true;
+  };
+  auto sub_qr = [&](uint64_t q) {  // acc -= q * r
+    unsigned __int128 prod = 0;
+    uint64_t borrow = 0;
     for (int k = 0; k < 5; k++) {
-      c += (unsigned __int128)acc[k] * base;
+      prod += (unsigned __int128)(k < 4 ? RL[k] : 0) * q;
+      const uint64_t p = (uint64_t)prod;
+      prod >>= 64;
+      const unsigned __int128 sub = (unsigned __int128)p + borrow;
+      borrow = (unsigned __int128)acc[k] < sub ? 1 : 0;
+      acc[k] = (uint64_t)((unsigned __int128)acc[k] - sub);
+    }
+  };
+  while (i < t.size()) {
+    const size_t take = t.size() - i < per ? t.size() - i : per;
+    uint64_t v = 0, m = 1;
+    for (size_t j = 0; j < take; j++, i++) {
+      const char ch = t[i];
+      unsigned d;
+      if (ch >= '0' && ch <= '9') d = ch - '0';
+      else if (base == 16 && ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+      else if (base == 16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+      else return false;  // fractions / exponents are not field elements
+      v = v * base + d;
+      m *= base;
+    }
+    unsigned __int128 c = v;  // acc < r before: acc * m + v < 2^314
+    for (int k = 0; k < 5; k++) {
+      c += (unsigned __int128)acc[k] * m;
       acc[k] = (uint64_t)c;
       c >>= 64;
     }
-    for (;;) {  // reduce below r
-      bool ge = acc[4] != 0;
-      if (!ge) {
-        ge = true;
-        for (int k = 3; k >= 0; k--)
-          if (acc[k] != RL[k]) {
-            ge = acc[k] > RL[k];
-            break;
-          }
-      }
-      if (!ge) break;
-      uint64_t borrow = 0;
-      for (int k = 0; k < 5; k++) {
-        const unsigned __int128 sub = (unsigned __int128)(k < 4 ? RL[k] : 0) + borrow;
-        borrow = (unsigned __int128)acc[k] < sub ? 1 : 0;
-        acc[k] = (uint64_t)((unsigned __int128)acc[k] - sub);
-      }
-    }
+    const unsigned __int128 top = ((unsigned __int128)acc[4] << 64) | acc[3];
+    const uint64_t q = (uint64_t)(top / ((unsigned __int128)RL[3] + 1));
+    if (q) sub_qr(q);
+    while (ge_r()) sub_qr(1);
   }
   const bool zero = !(acc[0] | acc[1] | acc[2] | acc[3]);
   if (neg && !zero) {  // r - v

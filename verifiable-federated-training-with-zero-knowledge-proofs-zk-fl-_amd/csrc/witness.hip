@@ -61,38 +61,73 @@ ZK_DEV Fr lc_eval(const ProgView& P, const Fr* w, uint32_t lc) {
   return acc;
 }
 
-// circomlib Poseidon permutation (zkfl/field.py::poseidon_perm_trace), width t, trace writes
-__device__ __attribute__((noinline)) void pos_run(const ProgView& P, Fr* w, uint32_t out, uint32_t lc0, uint32_t t,
-                                                   const uint32_t* live) {
-  Fr st[MAX_T], ns[MAX_T];
-  st[0] = fp_zero<FrP>();
-  for (uint32_t i = 1; i < t; i++) st[i] = lc_eval(P, w, lc0 + i - 1);
-  const PosWidth pw = P.width[t];
-  const Fr* C = P.consts + pw.c_off;
-  const Fr* M = P.consts + pw.m_off;
-  const uint32_t rounds = 8 + pw.rp;
-  uint32_t k = out, sb = 0;
+// circomlib Poseidon permutation (zkfl/field.py::poseidon_perm_trace) of width T for one K_POS op
+// per group of T lanes: lane i of a group holds state element i (8 VGPRs, no scratch), applies
+// the ARK constant and, in full rounds or for i = 0, the S-box (writing x^2, x^4, x^5 when the
+// template marks that S-box live), then computes MDS row i from the group's state read with
+// cross-lane shuffles, 4 products per Montgomery reduction.  The latency of a round is one row,
+// not T rows (one lane per permutation), and nothing is spilled.  Every lane of the wave executes
+// the shuffles; lanes without a job compute on zeros and store nothing.
+__global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t op0, uint32_t cnt, uint32_t T,
+                                                Fr* W) {
+  const uint32_t lane = threadIdx.x, G = 64 / T;
+  const uint32_t g = lane / T, i = lane - g * T;
+  const size_t job = (size_t)blockIdx.x * G + g;
+  const bool active = g < G && job < n * cnt;
+  const size_t jj = active ? job : 0;
+  const uint4 op = P.ops[op0 + (uint32_t)(jj % cnt)];
+  Fr* w = W + (jj / cnt) * P.n_wires;
+  const uint32_t gb = (g < G ? g : 0) * T;  // the group's first lane
+  Fr st = (active && i > 0) ? lc_eval(P, w, op.z + i - 1) : fp_zero<FrP>();
+  const PosWidth pw = P.width[T];
+  const Fr* __restrict__ C = P.consts + pw.c_off;
+  const Fr* __restrict__ Mrow = P.consts + pw.m_off + (size_t)i * T;
+  uint32_t lw[7], pre[7];  // live S-box bitmap of the op's template and its word prefix counts
+  const uint32_t* live = P.tmpl + 8 * (op.w >> 8) + 1;
+  uint32_t acc_live = 0;
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    lw[q] = active ? live[q] : 0u;
+    pre[q] = acc_live;
+    acc_live += __popc(lw[q]);
+  }
+  const uint32_t rp = pw.rp, rounds = 8 + rp;
   for (uint32_t r = 0; r < rounds; r++) {
-    for (uint32_t i = 0; i < t; i++) st[i] = fp_add(st[i], C[r * t + i]);
-    const uint32_t nl = (r < 4 || r >= 4 + pw.rp) ? t : 1;
-    for (uint32_t i = 0; i < nl; i++, sb++) {
-      Fr x2 = fp_sqr(st[i]);
-      Fr x4 = fp_sqr(x2);
-      Fr x5 = fp_mul(x4, st[i]);
-      if ((live[sb >> 5] >> (sb & 31)) & 1u) {
+    st = fp_add(st, C[r * T + i]);
+    const bool full = r < 4 || r >= 4 + rp;
+    if (full || i == 0) {
+      const uint32_t sb = r < 4 ? r * T + i : (r < 4 + rp ? 4 * T + (r - 4) : 4 * T + rp + (r - 4 - rp) * T + i);
+      const Fr x2 = fp_sqr(st), x4 = fp_sqr(x2), x5 = fp_mul(x4, st);
+      const uint32_t q = sb >> 5, bit = sb & 31;
+      uint32_t word = 0, rank = 0;
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+        if ((uint32_t)k == q) {
+          word = lw[k];
+          rank = pre[k];
+        }
+      if ((word >> bit) & 1u) {
+        const uint32_t k = op.y + 3 * (rank + __popc(word & ((1u << bit) - 1u)));
         w[k] = x2;
         w[k + 1] = x4;
         w[k + 2] = x5;
-        k += 3;
       }
-      st[i] = x5;
+      st = x5;
     }
-    for (uint32_t i = 0; i < t; i++) {
-      Fr acc = fp_mul(M[i * t], st[0]);
-      for (uint32_t j = 1; j < t; j++) acc = fp_add(acc, fp_mul(M[i * t + j], st[j]));
-      ns[i] = acc;
+    Fr acc = fp_zero<FrP>();
+    for (uint32_t j0 = 0; j0 < T; j0 += 4) {
+      Fr x[4], y[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t j = j0 + k;
+        const uint32_t src = gb + (j < T ? j : 0);
+#pragma unroll
+        for (int v = 0; v < 8; v++) x[k].v[v] = __shfl((int)st.v[v], (int)src);
+        y[k] = j < T ? Mrow[j] : fp_zero<FrP>();
+      }
+      acc = fp_add(acc, fp_mul_sum4(x, y));
     }
-    for (uint32_t i = 0; i < t; i++) st[i] = ns[i];
+    st = acc;
   }
 }
 
@@ -133,11 +168,20 @@ __global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t
     case K_BITS: {
       Fr v = fp_from_mont(lc_eval(P, w, op.z));
       const Fr one = fp_one<FrP>(), zero = fp_zero<FrP>();
-      for (uint32_t i = 0; i < op.w; i++) w[op.y + i] = ((v.v[i >> 5] >> (i & 31)) & 1u) ? one : zero;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; q++) {  // constant limb index: v stays in registers
+#pragma unroll 1
+        for (uint32_t b = 0; b < 32 && q * 32 + b < op.w; b++) {
+          const uint32_t bit = (v.v[q] >> b) & 1u;
+          Fr o;
+#pragma unroll
+          for (int k = 0; k < 8; k++) o.v[k] = bit ? one.v[k] : zero.v[k];  // per-limb select, no stack copy
+          w[op.y + q * 32 + b] = o;
+        }
+      }
       break;
     }
-    default:  // K_POS
-      pos_run(P, w, op.y, op.z, op.w & 0xFFu, P.tmpl + 8 * (op.w >> 8) + 1);
+    default:  // K_POS ops run in k_wit_pos (wprog_load groups them per level and width)
       break;
   }
 }
@@ -173,6 +217,10 @@ struct WProg {
   uint32_t n_wires = 0, n_pub_out = 0, n_pub_in = 0, n_prv_in = 0, in_first = 0;
   uint32_t n_ops = 0, n_levels = 0, n_asserts = 0;
   std::vector<uint32_t> level_ptr;
+  struct Seg {
+    uint32_t op0, cnt, t;  // t = 0: k_wit_level ops; else K_POS ops of width t (k_wit_pos)
+  };
+  std::vector<Seg> segs;        // launch order: level by level
   ProgView view = {};
   std::vector<void*> allocs;
 };
@@ -217,7 +265,25 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
   p->signals = std::move(H.signals);
   for (int t = 0; t <= MAX_T; t++) p->view.width[t] = {H.width[t].rp, H.width[t].c_off, H.width[t].m_off};
   const uint32_t n_lcs = H.n_lcs, n_terms = H.n_terms, n_tmpl = H.n_tmpl;
-  const uint8_t *ops = H.ops, *lcp = H.lc_ptr, *tw = H.term_wire, *tc = H.term_coef, *as = H.asserts, *tm = H.tmpl;
+  const uint8_t *lcp = H.lc_ptr, *tw = H.term_wire, *tc = H.term_coef, *as = H.asserts, *tm = H.tmpl;
+  // Ops of a level are independent: regroup each level as [other ops][K_POS by width] so the
+  // Poseidon permutations run in k_wit_pos lane groups of their width.
+  std::vector<uint4> ops_v(p->n_ops);
+  for (uint32_t L = 0; L < p->n_levels; L++) {
+    const uint32_t a = p->level_ptr[L], b = p->level_ptr[L + 1];
+    uint32_t o = a;
+    for (uint32_t t = 0; t <= (uint32_t)MAX_T; t++) {
+      const uint32_t first = o;
+      for (uint32_t q = a; q < b; q++) {
+        uint4 op;
+        memcpy(&op, H.ops + 16ull * q, 16);
+        const uint32_t opt = op.x == K_POS ? (op.w & 0xFFu) : 0u;
+        if (opt == t) ops_v[o++] = op;
+      }
+      if (o > first) p->segs.push_back({first, o - first, t});
+    }
+  }
+  const uint8_t* ops = reinterpret_cast<const uint8_t*>(ops_v.data());
   std::vector<uint8_t>& consts = H.consts;
   struct Up {
     const void* src;
@@ -273,9 +339,12 @@ hipError_t wprog_enqueue(const WProg* p, size_t m, const uint32_t* d_in, Fr* W, 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_wit_inputs, dim3(zk_grid(m * (n_in + 1), 64)), dim3(64), 0, st, m, nw, p->in_first, n_in, d_in,
                      W);
-  for (uint32_t L = 0; L < p->n_levels; L++) {
-    const uint32_t op0 = p->level_ptr[L], cnt = p->level_ptr[L + 1] - op0;
-    if (cnt) hipLaunchKernelGGL(k_wit_level, dim3(zk_grid(m * cnt, 64)), dim3(64), 0, st, p->view, m, op0, cnt, W);
+  for (const WProg::Seg& g : p->segs) {
+    if (g.t == 0)
+      hipLaunchKernelGGL(k_wit_level, dim3(zk_grid(m * g.cnt, 64)), dim3(64), 0, st, p->view, m, g.op0, g.cnt, W);
+    else
+      hipLaunchKernelGGL(k_wit_pos, dim3(zk_grid(m * g.cnt, 64 / g.t)), dim3(64), 0, st, p->view, m, g.op0, g.cnt, g.t,
+                         W);
   }
   if (p->n_asserts)
     hipLaunchKernelGGL(k_wit_asserts, dim3(zk_grid(m * p->n_asserts, 64)), dim3(64), 0, st, p->view, m, p->n_asserts,

@@ -21,9 +21,13 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1263,6 +1267,104 @@ int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog*
   v.resize(v.size() + 8);  // never empty (a circuit without inputs still proves one witness)
   return zkfl_groth16_full_prove_batch(ctx, key, prog, 1, reinterpret_cast<const uint8_t*>(v.data()), rs, proof_out,
                                        pub_out);
+}
+
+// input.json texts -> input vectors on host worker threads, ahead of the slot scheduler that
+// consumes them (at most AHEAD parsed vectors held), so parsing overlaps the proofs in flight.
+namespace {
+struct JsonParsePool {
+  static constexpr size_t AHEAD = 64;
+  const WProg* prog;
+  const char* const* texts;
+  size_t n, n_in;
+  std::vector<std::vector<uint32_t>> vec;
+  std::vector<std::string> err;
+  std::vector<int> rc;
+  std::vector<uint8_t> done;
+  std::atomic<size_t> next{0};
+  size_t consumed = 0;
+  bool stop = false;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::thread> th;
+
+  JsonParsePool(const WProg* p, const char* const* t, size_t count, size_t nin)
+      : prog(p), texts(t), n(count), n_in(nin), vec(count), err(count), rc(count, 0), done(count, 0) {
+    const unsigned hw = std::max(2u, std::thread::hardware_concurrency());
+    const size_t workers = std::min<size_t>({count, (size_t)hw / 2, 8});
+    for (size_t w = 0; w < workers; w++) th.emplace_back([this] { work(); });
+  }
+  ~JsonParsePool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void work() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || i < consumed + AHEAD; });
+        if (stop) return;
+      }
+      std::vector<uint32_t> v;
+      std::string e;
+      int r = texts[i] ? wprog_inputs_json(prog, texts[i], v, e) : ZKFL_E_ARG;
+      if (!texts[i]) e = "null input json";
+      if (r == ZKFL_OK && v.size() != n_in * 8) {
+        r = ZKFL_E_ARG;
+        e = "input json does not fill the program's inputs";
+      }
+      v.resize(n_in * 8 + 8);  // never empty
+      {
+        std::lock_guard<std::mutex> g(mu);
+        vec[i] = std::move(v);
+        err[i] = std::move(e);
+        rc[i] = r;
+        done[i] = 1;
+      }
+      cv.notify_all();
+    }
+  }
+  // Job i's vector (blocks until parsed); job i-1's vector is released (its slot copied it).
+  int get(size_t i, const uint8_t** out) {
+    std::unique_lock<std::mutex> g(mu);
+    if (i > 0) std::vector<uint32_t>().swap(vec[i - 1]);
+    consumed = i;
+    cv.notify_all();
+    cv.wait(g, [&] { return done[i] != 0; });
+    if (rc[i]) return fail(rc[i], "input " + std::to_string(i) + ": " + err[i]);
+    *out = reinterpret_cast<const uint8_t*>(vec[i].data());
+    return ZKFL_OK;
+  }
+};
+}  // namespace
+
+int zkfl_groth16_full_prove_json_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
+                                       const char* const* input_jsons, const uint8_t* rs, uint8_t* proofs_out,
+                                       uint8_t* pubs_out) {
+  if (!ctx || (n && (!input_jsons || !proofs_out))) return fail(ZKFL_E_ARG, "full_prove_json_batch: null argument");
+  size_t n_in = 0;
+  int rc = full_prove_check(ctx, key, prog, 0, nullptr, &n_in);
+  if (rc || n == 0) return rc;
+  JsonParsePool pool(prog->p, input_jsons, n, n_in);
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    const uint8_t* in = nullptr;
+    int r = pool.get(i, &in);  // parsed values are < r by construction
+    if (r) return r;
+    J.key = key;
+    J.prog = prog->p;
+    J.input = in;
+    J.n_in = n_in;
+    J.rs = rs ? rs + 64 * i : nullptr;
+    J.proof_out = proofs_out + 256 * i;
+    J.pub_out = pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr;
+    return ZKFL_OK;
+  });
 }
 
 int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,

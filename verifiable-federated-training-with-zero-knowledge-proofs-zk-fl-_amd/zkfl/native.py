@@ -73,6 +73,8 @@ SIGNATURES = {
     "zkfl_dataset_commit": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, _U8P]),
     "zkfl_groth16_full_prove_json": (C.c_int, [_P, _P, _P, C.c_char_p, C.c_char_p, _U8P, _U8P]),
     "zkfl_groth16_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.c_char_p, _U8P]),
+    "zkfl_groth16_full_prove_json_batch": (C.c_int, [_P, _P, _P, C.c_size_t, C.POINTER(C.c_char_p), C.c_char_p, _U8P,
+                                                     _U8P]),
     "zkfl_groth16_full_prove_multi": (C.c_int, [_P, C.c_size_t, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_char_p),
                                                 C.c_char_p, _U8P, C.POINTER(_U8P)]),
 }
@@ -384,6 +386,20 @@ class ProvingKey:
         out = _buf(256 * max(1, n))
         pubs = _buf(32 * max(1, self.n_public) * max(1, n))
         check(lib().zkfl_groth16_full_prove_batch(self.ctx.h, self.h, prog.h, n, buf, rs, out, pubs))
+        ob, pb = bytes(out), bytes(pubs)
+        k = self.n_public
+        return [(ob[256 * i:256 * i + 256],
+                 [int.from_bytes(pb[32 * (i * k + j):32 * (i * k + j) + 32], "little") for j in range(k)])
+                for i in range(n)]
+
+    def full_prove_json_batch(self, prog: "WitnessProgram", texts, rs: bytes | None = None):
+        """input.json texts -> [(proof 256 B, [public ints])]: parsed by host threads while earlier
+        proofs run (zkfl_groth16_full_prove_json_batch)."""
+        n = len(texts)
+        arr = (C.c_char_p * max(1, n))(*[t.encode() if isinstance(t, str) else t for t in texts])
+        out = _buf(256 * max(1, n))
+        pubs = _buf(32 * max(1, self.n_public) * max(1, n))
+        check(lib().zkfl_groth16_full_prove_json_batch(self.ctx.h, self.h, prog.h, n, arr, rs, out, pubs))
         ob, pb = bytes(out), bytes(pubs)
         k = self.n_public
         return [(ob[256 * i:256 * i + 256],
