@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build an A/B variant of libzkfl.so with extra compile flags (CPU side, before gpurun):
+#   bash tools/build_ab.sh NAME "-DKNOB=VALUE ..."   ->  build_ab/NAME/libzkfl.so
+# then on the box: ZKFL_LIB=build_ab/NAME/libzkfl.so python bench.py ...  (tools/sweep_env.sh)
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+PKG=$R/verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd
+NAME=$1; FLAGS=${2:-}
+OUT=$R/build_ab/$NAME
+mkdir -p "$OUT"
+CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$R/include -I$PKG/csrc -Wno-unused-result $FLAGS"
+pids=()
+for s in zkfl ntt msm_g1 msm_g2 verify witness merkle; do
+  $CXX -c -o "$OUT/$s.o" "$PKG/csrc/$s.hip" & pids+=($!)
+done
+g++ -O2 -fPIC -std=c++17 -I"$R/include" -I"$PKG/csrc" -c -o "$OUT/host_parse.o" "$PKG/csrc/host_parse.cc" & pids+=($!)
+for p in "${pids[@]}"; do wait "$p"; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libzkfl.so" "$OUT"/*.o
+rm -f "$OUT"/*.o
+echo "built $OUT/libzkfl.so ($FLAGS)"

@@ -54,6 +54,12 @@ namespace zkfl {
 #ifndef MSM_G2_PREFETCH
 #define MSM_G2_PREFETCH 0
 #endif
+// 1: the next entry's base is fetched straight into LDS (global_load_lds_dwordx4, 4 x 16 B per
+// lane, double-buffered, 8 KB per wave) while the current one is added, so the gather latency is
+// hidden without holding the point in VGPRs (which spilled / cost occupancy: MSM_G*_PREFETCH).
+#ifndef MSM_LDS_PF
+#define MSM_LDS_PF 1
+#endif
 #ifndef MSM_G2_TAIL_WAVES
 #define MSM_G2_TAIL_WAVES 2
 #endif
@@ -72,6 +78,16 @@ struct MsmIO {
   using S = F;
   static constexpr int LANES = 1;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return p[i]; }
+  // the 16-B piece q < 4 of this lane's share of base i, and a share rebuilt from its pieces
+  // (G1: the whole 64-B point; the LDS-DMA prefetch of k_msm_accumulate)
+  static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
+    return reinterpret_cast<const uint4*>(p + i) + q;
+  }
+  static ZK_DEV Affine<F> from_pieces(const uint4 (&u)[4]) {
+    Affine<F> a;
+    memcpy(&a, u, sizeof(a));
+    return a;
+  }
   static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return p[i]; }
   static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<F>& v) { p[i] = v; }
 };
@@ -83,6 +99,16 @@ struct MsmIO<Fq2PairOps> {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
     const uint32_t h = pair_half();
     return {q[h], q[2 + h]};
+  }
+  // lane 2k+h holds x.c_h, y.c_h: pieces 0, 1 = x.c_h, 2, 3 = y.c_h
+  static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
+    return reinterpret_cast<const uint4*>(p + i) + 2 * pair_half() + (q & 1) + (q >> 1) * 4;
+  }
+  static ZK_DEV Affine<Fq2PairOps> from_pieces(const uint4 (&u)[4]) {
+    Affine<Fq2PairOps> a;
+    memcpy(&a.x, &u[0], 32);
+    memcpy(&a.y, &u[2], 32);
+    return a;
   }
   static ZK_DEV XYZZ<Fq2PairOps> ld(const XYZZ<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
@@ -104,6 +130,14 @@ struct MsmIOSameLayout {
   using S = FqOps;
   static constexpr int LANES = 1;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return reinterpret_cast<const Affine<F>*>(p)[i]; }
+  static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
+    return reinterpret_cast<const uint4*>(p + i) + q;
+  }
+  static ZK_DEV Affine<F> from_pieces(const uint4 (&u)[4]) {
+    Affine<F> a;
+    memcpy(&a, u, sizeof(a));
+    return a;
+  }
   static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return reinterpret_cast<const XYZZ<F>*>(p)[i]; }
   static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<F>& v) { reinterpret_cast<XYZZ<F>*>(p)[i] = v; }
 };
@@ -265,11 +299,34 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     k1 = keys[p0 + 1];
     v1 = vals[p0 + 1];
   }
+#if MSM_LDS_PF
+  // lane l's piece q of buffer b lands at pf[b][q][l] (an LDS-DMA writes base + lane x 16 B)
+  __shared__ uint4 pf[2][4][64];
+  const uint32_t ln = threadIdx.x;
+  auto fetch = [&](uint32_t idx, int b) {
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)IO::piece(bases, idx, q),
+                                       (__attribute__((address_space(3))) void*)&pf[b][q][0], 16, 0, 0);
+  };
+  fetch(v0 & 0x7FFFFFFFu, 0);
+  uint32_t it = 0;
+#else
   Affine<F> a = IO::ld_aff(bases, v0 & 0x7FFFFFFFu);
+#endif
   for (uint32_t p = (uint32_t)p0; p < p1; p++) {
+#if MSM_LDS_PF
+    const int b = it++ & 1;
+    uint4 u[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) u[q] = pf[b][q][ln];  // the compiler waits for the DMA (vmcnt)
+    const Affine<F> a = IO::from_pieces(u);
+    if (p + 1 < p1) fetch(v1 & 0x7FFFFFFFu, b ^ 1);
+#else
     Affine<F> an;
-    uint32_t k2 = 0, v2 = 0;
     if (PF && p + 1 < p1) an = IO::ld_aff(bases, v1 & 0x7FFFFFFFu);
+#endif
+    uint32_t k2 = 0, v2 = 0;
     if (p + 2 < p1) {
       k2 = keys[p + 2];
       v2 = vals[p + 2];
@@ -288,8 +345,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     v0 = v1;
     v1 = v2;
     k1 = k2;
+#if !MSM_LDS_PF
     if (PF) a = an;
     else if (p + 1 < p1) a = IO::ld_aff(bases, v0 & 0x7FFFFFFFu);
+#endif
   }
   if (!slot0) item_key[2 * c] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
   if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
@@ -395,7 +454,7 @@ k_msm_wsum(const MsmTailArgs<S> ta, int level) {
   XYZZ<S>* __restrict__ out_a = l0 ? ta.red_a[yb] : ta.out[yb];
   XYZZ<S>* __restrict__ out_s = l0 ? ta.red_s[yb] : ta.red_s[yb] + MSM_RB;
   using IO = MsmIO<F>;
-  __shared__ XYZZ<S> sh[MSM_RB];
+  __shared__ XYZZ<S> sh[MSM_RB], shy[MSM_RB];
   const int t = threadIdx.x / IO::LANES;
   const bool same = in_a == in_s;
   // serial fold of items [(blk*RB + t)*Q, +Q)
@@ -410,9 +469,11 @@ k_msm_wsum(const MsmTailArgs<S> ta, int level) {
     if (k >= 1) W = xyzz_add<F>(W, R);
   }
   if (same) y = R;
+  if (Q > 1) {  // (Q = 1: W is infinity)
 #pragma unroll 1
-  for (int k = 0; k < log2g; k++) W = xyzz_dbl<F>(W);
-  y = xyzz_add<F>(y, W);  // this lane's item: group of Q*g buckets
+    for (int k = 0; k < log2g; k++) W = xyzz_dbl<F>(W);
+    y = xyzz_add<F>(y, W);  // this lane's item: group of Q*g buckets
+  }
 #pragma unroll 1
   for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
     IO::st(sh, t, R);
@@ -420,22 +481,27 @@ k_msm_wsum(const MsmTailArgs<S> ta, int level) {
     if (t + d < MSM_RB) R = xyzz_add<F>(R, IO::ld(sh, t + d));
     __syncthreads();
   }
-  XYZZ<F> x = t >= 1 ? R : xyzz_inf<F>();
+  // The tree sums of R_{t>=1} (x) and of a (y) side by side: at step d, lanes [0, d) add x
+  // pairs and lanes [RB/2, RB/2 + d) add y pairs, so both trees cost one tree's latency.
+  IO::st(sh, t, t >= 1 ? R : xyzz_inf<F>());
+  IO::st(shy, t, y);
+  __syncthreads();
+  constexpr int H = MSM_RB / 2;
+  const bool ty = t >= H;
+  const int tt = ty ? t - H : t;
+  XYZZ<S>* tree = ty ? shy : sh;
 #pragma unroll 1
-  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {  // tree sums of R_{t>=1} and of a
-    IO::st(sh, t, x);
+  for (int d = H; d >= 1; d >>= 1) {
+    XYZZ<F> v;
+    if (tt < d) v = xyzz_add<F>(IO::ld(tree, tt), IO::ld(tree, tt + d));
     __syncthreads();
-    if (t < d) x = xyzz_add<F>(x, IO::ld(sh, t + d));
+    if (tt < d) IO::st(tree, tt, v);
     __syncthreads();
   }
-#pragma unroll 1
-  for (int d = MSM_RB / 2; d >= 1; d >>= 1) {
-    IO::st(sh, t, y);
-    __syncthreads();
-    if (t < d) y = xyzz_add<F>(y, IO::ld(sh, t + d));
-    __syncthreads();
-  }
+  XYZZ<F> x;
   if (t == 0) {
+    x = IO::ld(sh, 0);
+    y = IO::ld(shy, 0);
     const int lq = 31 - __builtin_clz((unsigned)Q);
     for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
     IO::st(out_a, blockIdx.x, xyzz_canon<F>(xyzz_add<F>(y, x)));  // [0, p) when it leaves the MSM
