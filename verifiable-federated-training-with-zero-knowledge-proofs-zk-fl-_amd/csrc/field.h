@@ -421,6 +421,37 @@ ZK_DEV Fq fq_mul_compact(const Fq& a, const Fq& b) {
   return r;
 }
 
+// a*b + c*d and sum_{k<4} x_k*y_k over Fq (one Montgomery reduction, one conditional
+// subtraction).  The C forms (fp_mul_sum2 / fp_mul_sum4) compile to one asm statement per
+// product, and the compiler pads every statement boundary with an s_nop (G2 accumulation: ~2,500
+// s_nop of ~12,000 instructions); ZK_ASM_MULSUM selects one whole-asm statement per sum
+// (tools/gen_fp_mul_asm.py) instead.  Measured on MI355X: G2 accumulation 0.961 (C) vs 0.981 ms
+// (asm) per proof, bench flat — the other waves issue during the nops, and the compiler's
+// interleaving of independent products in the C form is worth more (profiles/r02_s4_ab_asm_mul.log).
+ZK_DEV Fq fq_mulsum2(const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+#ifndef ZK_ASM_MULSUM
+  return fp_mul_sum2(a, b, c, d);
+#else
+  uint32_t u[8];
+  ZK_FP_MULSUM2_ASM(u, a.v, b.v, c.v, d.v, FqP::P, FqP::INV);
+  Fq r;
+  fp_reduce_once<FqP>(r.v, u);
+  return r;
+#endif
+}
+
+ZK_DEV Fq fq_mulsum4(const Fq* x, const Fq* y) {
+#ifndef ZK_ASM_MULSUM
+  return fp_mul_sum4(x, y);
+#else
+  uint32_t u[8];
+  ZK_FP_MULSUM4_ASM(u, x[0].v, y[0].v, x[1].v, y[1].v, x[2].v, y[2].v, x[3].v, y[3].v, FqP::P, FqP::INV);
+  Fq r;
+  fp_reduce_once<FqP>(r.v, u);
+  return r;
+#endif
+}
+
 struct FqOpsCompact : FqOps {
   static ZK_DEV T mul(const T& a, const T& b) { return fq_mul_compact(a, b); }
   static ZK_DEV T sqr(const T& a) { return fq_mul_compact(a, a); }
@@ -494,7 +525,7 @@ struct FqOpsLazy : FqOps {
   // inputs < 2p: a*b + c*d < 8p^2, the product-sum is < 2.52p and its one subtraction of p leaves
   // it < 2p
   static ZK_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
-    return fp_mul_sum2(a, b, neg(c), d);
+    return fp_mul_sum2(a, b, neg(c), d);  // (the one-statement form needs 4 more VGPRs: spills at 128)
   }
   static ZK_DEV T canon(const T& a) {
     T r;
@@ -552,7 +583,7 @@ struct Fq2PairOps {
   static ZK_DEV T mul(const T& a, const T& b) {
     const bool h = pair_half();
     const Fq pa = pair_swap(a), pb = pair_swap(b);
-    return fp_mul_sum2(a, fq_sel(h, pb, b), fq_sel(h, pa, fp_neg(pa)), fq_sel(h, b, pb));
+    return fq_mulsum2(a, fq_sel(h, pb, b), fq_sel(h, pa, fp_neg(pa)), fq_sel(h, b, pb));
   }
   // a*b - c*d over Fq2 as one four-product sum per lane:
   //   lane 0: a0 b0 + (-a1) b1 + (-c0) d0 + c1 d1,  lane 1: a1 b0 + a0 b1 + (-c1) d0 + (-c0) d1
@@ -562,14 +593,18 @@ struct Fq2PairOps {
     const Fq npc = fp_neg(pc);
     const Fq x[4] = {a, fq_sel(h, pa, fp_neg(pa)), fp_neg(c), fq_sel(h, npc, pc)};
     const Fq y[4] = {fq_sel(h, pb, b), fq_sel(h, b, pb), fq_sel(h, pd, d), fq_sel(h, d, pd)};
-    return fp_mul_sum4(x, y);
+    return fq_mulsum4(x, y);
   }
   static ZK_DEV T canon(const T& a) { return a; }
   // c0 = (a0 + a1)(a0 - a1) (lane 0), c1 = 2 a0 a1 (lane 1)
   static ZK_DEV T sqr(const T& a) {
     const bool h = pair_half();
     const Fq pa = pair_swap(a);
+#ifndef ZK_ASM_MULSUM
     const Fq t = fp_mul(fq_sel(h, a, fp_add(a, pa)), fq_sel(h, pa, fp_sub(a, pa)));
+#else
+    const Fq t = fq_mul_compact(fq_sel(h, a, fp_add(a, pa)), fq_sel(h, pa, fp_sub(a, pa)));
+#endif
     return h ? fp_dbl(t) : t;
   }
 };

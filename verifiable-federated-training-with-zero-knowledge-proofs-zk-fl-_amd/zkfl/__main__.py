@@ -6,6 +6,10 @@
         name) + DIR/<name>_js/generate_witness.cjs, so the harness's
         `node <name>_js/generate_witness.cjs <name>_js/<name>.wasm in.json out.wtns` runs unchanged
     python -m zkfl info <circuit> [params..]                 snarkjs r1cs info (tests/test_verified_gradient.mjs:351-356)
+    python -m zkfl r1cs-info <file.r1cs>                     snarkjs r1cs info on a circom-compiled .r1cs
+    python -m zkfl setup-r1cs <file.r1cs> [-o DIR]           snarkjs groth16 setup (+ contribute, export vk) on a
+                                                             circom .r1cs (zkfl/r1cs_file.py); prove its circom
+                                                             .wtns with `prove`
     python -m zkfl setup <circuit> [params..] [-o DIR]       snarkjs groth16 setup + zkey contribute + zkey export
         -> DIR/<name>_final.zkey, DIR/verification_key.json  verificationkey (tests/full_system_simulation.mjs:713-735)
                                                              DEVELOPMENT ceremony: fresh random toxic waste, discarded
@@ -28,7 +32,7 @@ import os
 import secrets
 import sys
 
-from . import circuits, groth16, native, wprog, zkey
+from . import circuits, groth16, native, r1cs_file, wprog, zkey
 
 
 def _circuit(args):
@@ -64,9 +68,7 @@ def cmd_compile(args):
     print(f"written: {name}.r1cs, {name}.zkwp in {args.out}")
 
 
-def cmd_info(args):
-    b, _ = _circuit(args)
-    info = groth16.r1cs_info(b)
+def _print_info(info):
     print(f"[INFO]  snarkJS: Curve: {info['curve']}")
     print(f"[INFO]  snarkJS: # of Wires: {info['wires']}")
     print(f"[INFO]  snarkJS: # of Constraints: {info['constraints']}")
@@ -76,18 +78,44 @@ def cmd_info(args):
     print(f"[INFO]  snarkJS: # of Outputs: {info['outputs']}")
 
 
-def cmd_setup(args):
-    b, name = _circuit(args)
-    os.makedirs(args.out, exist_ok=True)
+def cmd_info(args):
+    b, _ = _circuit(args)
+    _print_info(groth16.r1cs_info(b))
+
+
+def _read_r1cs(path):
+    with open(path, "rb") as f:
+        return r1cs_file.read_r1cs(f.read())
+
+
+def cmd_r1cs_info(args):
+    rc = _read_r1cs(args.r1cs)
+    info = groth16.r1cs_info(rc)
+    info["labels"] = rc.n_labels
+    _print_info(info)
+
+
+def _setup(b, name, out):
+    os.makedirs(out, exist_ok=True)
     rnd = lambda: secrets.randbelow(zkey.R - 1) + 1  # noqa: E731
     with _ctx() as ctx:
         zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=rnd(), alpha=rnd(), beta=rnd(), gamma=rnd(), delta=rnd()))
         vk = groth16.export_verification_key(zk, ctx=ctx)
-    with open(os.path.join(args.out, name + "_final.zkey"), "wb") as f:
+    with open(os.path.join(out, name + "_final.zkey"), "wb") as f:
         f.write(zk)
-    with open(os.path.join(args.out, "verification_key.json"), "w") as f:
+    with open(os.path.join(out, "verification_key.json"), "w") as f:
         json.dump(vk, f, indent=1)
-    print(f"written: {name}_final.zkey ({len(zk)} bytes), verification_key.json in {args.out}")
+    print(f"written: {name}_final.zkey ({len(zk)} bytes), verification_key.json in {out}")
+
+
+def cmd_setup_r1cs(args):
+    name = args.name or os.path.splitext(os.path.basename(args.r1cs))[0]
+    _setup(_read_r1cs(args.r1cs), name, args.out)
+
+
+def cmd_setup(args):
+    b, name = _circuit(args)
+    _setup(b, name, args.out)
 
 
 def cmd_export_vk(args):
@@ -144,6 +172,12 @@ def main(argv=None):
                     help="also write <name>_js/<name>.wasm + generate_witness.cjs (circom's output layout)")
     circuit_args(sub.add_parser("info"))
     circuit_args(sub.add_parser("setup"), out=True)
+    sp = sub.add_parser("r1cs-info")
+    sp.add_argument("r1cs")
+    sp = sub.add_parser("setup-r1cs")
+    sp.add_argument("r1cs")
+    sp.add_argument("--name", default=None, help="output base name (default: the .r1cs file's)")
+    sp.add_argument("-o", "--out", default=".")
     sp = sub.add_parser("export-vk")
     sp.add_argument("zkey")
     sp.add_argument("vkey")
@@ -158,7 +192,8 @@ def main(argv=None):
     for a in ("vkey", "public", "proof"):
         sp.add_argument(a)
     args = ap.parse_args(argv)
-    fn = {"compile": cmd_compile, "info": cmd_info, "setup": cmd_setup, "export-vk": cmd_export_vk,
+    fn = {"compile": cmd_compile, "info": cmd_info, "setup": cmd_setup,
+          "r1cs-info": cmd_r1cs_info, "setup-r1cs": cmd_setup_r1cs, "export-vk": cmd_export_vk,
           "wtns": cmd_wtns, "prove": cmd_prove, "verify": cmd_verify}[args.cmd]
     try:
         return fn(args) or 0
