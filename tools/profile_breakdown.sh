@@ -7,7 +7,7 @@ TAG=${1:-bd}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o run -- python3 "$R/bench.py" --steps 32 --warmup 4 --no-cpu-baseline > "$OUT/bench.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o run -- python3 "$R/bench.py" --steps 32 --warmup 4 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 > "$OUT/bench.log" 2>&1
 python3 "$R/tools/rocpd_summary.py" kernels "$OUT/ks/run_results.db" "$OUT/kernel_stats.csv"
 python3 "$R/tools/rocpd_summary.py" breakdown "$OUT/ks/run_results.db" "$OUT/breakdown.csv" 6
 python3 "$R/tools/rocpd_summary.py" timeline "$OUT/ks/run_results.db" "$OUT/timeline.txt"
