@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Throughput probe for knock-out experiments (GPU box): the bench's timed region on M without
+any verification, so a deliberately broken library variant (a stage compiled out with
+-DZK_KNOCKOUT=mask, tools/build_ab.sh) can be timed.  1 / throughput differences between a
+variant and the full build give a stage's marginal cost per proof in the concurrent regime.
+Never a benchmark of record: the proofs of a knocked-out build are wrong.
+
+    ZKFL_LIB=build_ab/ko1/libzkfl.so python3 tools/ko_probe.py [--steps 48 --warmup 8 --slots 20]
+"""
+import argparse
+import os
+import sys
+import time
+
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZKFL_HW_QUEUES", "28")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--slots", type=int, default=20)
+    args = ap.parse_args()
+    from zkfl import circuits, clients, native, wprog, zkey
+    b = circuits.build("sgd_verified", 128, 4, 7, 1000)
+    objs = [clients.Client(c + 1, 128, 4, 7, clients.JsLcg(12345 + c)).training_input(128, 1000, 100000000)[0]
+            for c in range(4)]
+    ctx = native.Context(0)
+    zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
+    key = native.ProvingKey(ctx, zk)
+    key.set_slots(args.slots)
+    wp = native.WitnessProgram(ctx, wprog.compile_program(b))
+    res = wp.compute_resident(key, [wprog.input_bytes(b, o) for o in objs])
+    key.prove_batch([res[i % 4] for i in range(args.warmup * args.slots)])
+    ctx.synchronize()
+    n = args.steps * args.slots
+    t0 = time.perf_counter()
+    key.prove_batch([res[i % 4] for i in range(n)])
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{os.environ.get('ZKFL_LIB', 'in-tree')}: {n / dt:.2f} proofs/s ({dt / n * 1e3:.3f} ms per proof)")
+
+
+if __name__ == "__main__":
+    main()

@@ -442,37 +442,50 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
 // LDS suffix scan and two trees (depth ~18).  Level 0 reads the buckets as both a and s (g = 1,
 // Q = 8: 64 blocks); level 1 (Q = 1) combines the 64 block results into the MSM result.  Serial
 // folding first keeps the waves few: the reduction's cost is its waves' register-time.
-static_assert(MSM_NB == MSM_RB * MSM_RB * 8, "two reduction levels cover the buckets");
-template <class F, int MINW, class S = typename MsmIO<F>::S>
+// Q0: buckets folded serially per lane at level 0 (per curve: the reduction's waves hold their
+// registers for the whole serial fold, but fewer, longer lanes do less scan/tree work per bucket)
+#ifndef MSM_G1_WSUM_Q
+#define MSM_G1_WSUM_Q 16
+#endif
+#ifndef MSM_G2_WSUM_Q
+#define MSM_G2_WSUM_Q 16
+#endif
+template <class S>
+constexpr int msm_wsum_q0() {
+  return sizeof(typename S::T) == 32 ? MSM_G1_WSUM_Q : MSM_G2_WSUM_Q;
+}
+static_assert(MSM_NB % (MSM_RB * MSM_G1_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G1_WSUM_Q) <= MSM_RB &&
+                  MSM_NB % (MSM_RB * MSM_G2_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G2_WSUM_Q) <= MSM_RB,
+              "two reduction levels cover the buckets");
+template <class F, int MINW, bool L0, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
-k_msm_wsum(const MsmTailArgs<S> ta, int level) {
+k_msm_wsum(const MsmTailArgs<S> ta) {
+  // One kernel per level (template L0): level 0 keeps only the running sums R, W live through its
+  // fold, level 1 has no fold at all, so neither carries the other's registers.
   const int yb = blockIdx.y;
-  const bool l0 = level == 0;
-  const XYZZ<S>* __restrict__ in_a = l0 ? ta.buckets[yb] : ta.red_a[yb];
-  const XYZZ<S>* __restrict__ in_s = l0 ? ta.buckets[yb] : ta.red_s[yb];
-  const int N = l0 ? MSM_NB : MSM_RB, log2g = l0 ? 0 : 9, Q = l0 ? 8 : 1;
-  XYZZ<S>* __restrict__ out_a = l0 ? ta.red_a[yb] : ta.out[yb];
-  XYZZ<S>* __restrict__ out_s = l0 ? ta.red_s[yb] : ta.red_s[yb] + MSM_RB;
+  const XYZZ<S>* __restrict__ in_a = L0 ? ta.buckets[yb] : ta.red_a[yb];
+  const XYZZ<S>* __restrict__ in_s = L0 ? ta.buckets[yb] : ta.red_s[yb];
+  constexpr int Q0 = msm_wsum_q0<S>(), B0 = MSM_NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
+  constexpr int N = L0 ? MSM_NB : B0, Q = L0 ? Q0 : 1;
+  constexpr int log2g = L0 ? 0 : __builtin_ctz((unsigned)(Q0 * MSM_RB));
+  XYZZ<S>* __restrict__ out_a = L0 ? ta.red_a[yb] : ta.out[yb];
+  XYZZ<S>* __restrict__ out_s = L0 ? ta.red_s[yb] : ta.red_s[yb] + MSM_RB;
   using IO = MsmIO<F>;
   __shared__ XYZZ<S> sh[MSM_RB], shy[MSM_RB];
   const int t = threadIdx.x / IO::LANES;
-  const bool same = in_a == in_s;
-  // serial fold of items [(blk*RB + t)*Q, +Q)
-  const int i0 = (blockIdx.x * MSM_RB + t) * Q;
-  XYZZ<F> R = xyzz_inf<F>(), W = xyzz_inf<F>(), y = xyzz_inf<F>();
+  const int i0 = (blockIdx.x * MSM_RB + t) * Q;  // this lane's items [i0, i0 + Q)
+  XYZZ<F> R = xyzz_inf<F>(), y = xyzz_inf<F>();
+  if constexpr (L0) {  // serial fold over Q buckets (a = s: the buckets themselves, g = 1)
+    XYZZ<F> W = xyzz_inf<F>();
 #pragma unroll 1
-  for (int k = Q - 1; k >= 0; k--) {
-    if (i0 + k < N) {
-      R = xyzz_add<F>(R, IO::ld(in_s, i0 + k));
-      if (!same) y = xyzz_add<F>(y, IO::ld(in_a, i0 + k));
+    for (int k = Q - 1; k >= 0; k--) {
+      if (i0 + k < N) R = xyzz_add<F>(R, IO::ld(in_s, i0 + k));
+      if (k >= 1) W = xyzz_add<F>(W, R);
     }
-    if (k >= 1) W = xyzz_add<F>(W, R);
-  }
-  if (same) y = R;
-  if (Q > 1) {  // (Q = 1: W is infinity)
-#pragma unroll 1
-    for (int k = 0; k < log2g; k++) W = xyzz_dbl<F>(W);
-    y = xyzz_add<F>(y, W);  // this lane's item: group of Q*g buckets
+    y = xyzz_add<F>(R, W);  // this lane's item: a group of Q buckets
+  } else if (i0 < N) {  // one block result per lane
+    R = IO::ld(in_s, i0);
+    y = IO::ld(in_a, i0);
   }
 #pragma unroll 1
   for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
@@ -502,7 +515,7 @@ k_msm_wsum(const MsmTailArgs<S> ta, int level) {
   if (t == 0) {
     x = IO::ld(sh, 0);
     y = IO::ld(shy, 0);
-    const int lq = 31 - __builtin_clz((unsigned)Q);
+    constexpr int lq = __builtin_ctz((unsigned)Q);
     for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
     IO::st(out_a, blockIdx.x, xyzz_canon<F>(xyzz_add<F>(y, x)));  // [0, p) when it leaves the MSM
     IO::st(out_s, blockIdx.x, R);
@@ -664,8 +677,9 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
     N = 2 * lanes;
     cur ^= 1;
   }
-  for (int level = 0; level < 2; level++)
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW>), dim3(level == 0 ? MSM_RB : 1, n), dim3(MSM_RB * LN), 0, st, ta, level);
+  hipLaunchKernelGGL((k_msm_wsum<FC, TW, true>), dim3(MSM_NB / (MSM_RB * msm_wsum_q0<F>()), n), dim3(MSM_RB * LN), 0,
+                     st, ta);
+  hipLaunchKernelGGL((k_msm_wsum<FC, TW, false>), dim3(1, n), dim3(MSM_RB * LN), 0, st, ta);
   return hipGetLastError();
 }
 

@@ -11,8 +11,14 @@ namespace zkfl {
 constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
-constexpr int MSM_L = 16;                  // sorted entries per accumulation lane (fixed-size chunks)
-constexpr int MSM_SG = 8;                  // partial sums per lane in each stitching level
+#ifndef MSM_G1_L
+#define MSM_G1_L 16
+#endif
+#ifndef MSM_STITCH_SG
+#define MSM_STITCH_SG 8
+#endif
+constexpr int MSM_L = MSM_G1_L;            // sorted entries per accumulation lane (fixed-size chunks)
+constexpr int MSM_SG = MSM_STITCH_SG;      // partial sums per lane in each stitching level
 constexpr int MSM_RB = 64;                 // items per block (one wave) in the weighted bucket reduction
 constexpr uint32_t MSM_ITEM_DUMMY = 0x80000000u;  // stitch item flag: padding (its value is infinity)
 constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
