@@ -6,6 +6,7 @@ variant and the full build give a stage's marginal cost per proof in the concurr
 Never a benchmark of record: the proofs of a knocked-out build are wrong.
 
     ZKFL_LIB=build_ab/ko1/libzkfl.so python3 tools/ko_probe.py [--steps 48 --warmup 8 --slots 20]
+    --e2e: time the input.json -> proof path (zkfl_groth16_full_prove_json_batch) instead
 """
 import argparse
 import os
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--slots", type=int, default=20)
+    ap.add_argument("--e2e", action="store_true")
     args = ap.parse_args()
     from zkfl import circuits, clients, native, wprog, zkey
     b = circuits.build("sgd_verified", 128, 4, 7, 1000)
@@ -32,12 +34,19 @@ def main():
     key = native.ProvingKey(ctx, zk)
     key.set_slots(args.slots)
     wp = native.WitnessProgram(ctx, wprog.compile_program(b))
-    res = wp.compute_resident(key, [wprog.input_bytes(b, o) for o in objs])
-    key.prove_batch([res[i % 4] for i in range(args.warmup * args.slots)])
-    ctx.synchronize()
     n = args.steps * args.slots
-    t0 = time.perf_counter()
-    key.prove_batch([res[i % 4] for i in range(n)])
+    if args.e2e:
+        import json
+        texts = [json.dumps(o) for o in objs]
+        key.full_prove_json_batch(wp, [texts[i % 4] for i in range(args.warmup * args.slots)])
+        t0 = time.perf_counter()
+        key.full_prove_json_batch(wp, [texts[i % 4] for i in range(n)])
+    else:
+        res = wp.compute_resident(key, [wprog.input_bytes(b, o) for o in objs])
+        key.prove_batch([res[i % 4] for i in range(args.warmup * args.slots)])
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        key.prove_batch([res[i % 4] for i in range(n)])
     ctx.synchronize()
     dt = time.perf_counter() - t0
     print(f"{os.environ.get('ZKFL_LIB', 'in-tree')}: {n / dt:.2f} proofs/s ({dt / n * 1e3:.3f} ms per proof)")
