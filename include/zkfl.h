@@ -159,10 +159,11 @@ int zkfl_witness_compute_resident(zkfl_ctx* ctx, const zkfl_wprog* prog, const z
 
 /* Full prove, pipelined (snarkjs `groth16.fullProve(input, wasm, zkey)` for a batch; the
  * reference's per-client loop `generate_witness.cjs` + `groth16 prove`,
- * tests/full_system_simulation.mjs:758-776 and :1298-1343).  Each proof slot computes its witness
- * on its own stream straight into HBM and proves it on the same stream, so witness generation
- * of one client overlaps the MSMs of the others; nothing returns to the host but the proof and
- * the public signals.  inputs: n x n_inputs x 32 B std (zkfl_wprog_parse_inputs per input.json);
+ * tests/full_system_simulation.mjs:758-776 and :1298-1343).  The witnesses are computed a group
+ * of `slots` clients at a time (one batched run of the witness engine on the key's witness
+ * stream, straight into HBM), one group ahead of the proof slots that consume them, so witness
+ * generation overlaps the MSMs of the previous group; nothing returns to the host but the proofs
+ * and the public signals.  inputs: n x n_inputs x 32 B std (zkfl_wprog_parse_inputs per input.json);
  * rs: n x 64 B or NULL (CSPRNG); proofs_out: n x 256 B; pubs_out: n x nPublic x 32 B or NULL.
  * A witness whose asserts fail gives ZKFL_E_CONSTRAINT naming the first such index (its proof
  * bytes are zeroed, the others are valid); an input >= r gives ZKFL_E_ARG before any work. */
@@ -180,7 +181,7 @@ int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog*
  * host worker threads parse the texts against the program's signal table ahead of the slot
  * scheduler (at most 64 parsed vectors held), so parsing overlaps the proofs in flight; then the
  * zkfl_groth16_full_prove_batch pipeline.  Errors: a text that does not parse or does not fill
- * the program's inputs gives ZKFL_E_ARG naming its index (proofs before it are complete);
+ * the program's inputs gives ZKFL_E_ARG naming its index (proofs of earlier slot groups complete);
  * otherwise as zkfl_groth16_full_prove_batch. */
 int zkfl_groth16_full_prove_json_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
                                        const char* const* input_jsons, const uint8_t* rs, uint8_t* proofs_out,

@@ -422,6 +422,7 @@ struct zkfl_key {
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
   int max_slots = 3;
+  struct WitPipe* wpipe = nullptr;  // batched witnesses of the single-key full-prove entry points
 };
 
 struct zkfl_witness {
@@ -507,8 +508,77 @@ int get_slot(zkfl_key* k, size_t idx, ProofSlot** out) {
   return ZKFL_OK;
 }
 
+}  // namespace
+
+// Witnesses of the single-key full-prove entry points, computed G (= the key's slots) jobs at a
+// time by ONE batched launch sequence of the witness engine on the key's witness stream, ahead of
+// the slots that prove them: group g is computed into buffer set g % 3 while the slots prove
+// group g - 1 (when group g + 1 is enqueued, the slots have drained group g - 2, so its set is
+// free).  Per-slot witnesses cost ~25 small launches per proof on the slot's stream, each a
+// permutation-latency chain; batched, a group's 15 levels cost as much as one witness's.
+struct WitPipe {
+  struct Set {
+    Fr* W = nullptr;          // [G][nw] Montgomery scratch
+    Fr* d = nullptr;          // [G][nw] std-form witnesses = the proofs' scalars
+    uint32_t* in = nullptr;   // [G][n_in x 8]
+    uint32_t* fail = nullptr; // [G]
+    Fr** outs = nullptr;      // [G] device pointers into d
+    uint8_t* pin_in = nullptr;
+    hipEvent_t ev = nullptr;  // the group's witnesses are complete
+  };
+  size_t G = 0, nw = 0, n_in = 0;
+  hipStream_t st = nullptr;
+  Set set[3];
+};
+
+namespace {
+
+void wpipe_release(WitPipe* p) {
+  if (!p) return;
+  if (p->st) (void)hipStreamSynchronize(p->st);
+  for (auto& b : p->set) {
+    for (void* q : {(void*)b.W, (void*)b.d, (void*)b.in, (void*)b.fail, (void*)b.outs})
+      if (q) (void)hipFree(q);
+    if (b.pin_in) (void)hipHostFree(b.pin_in);
+    if (b.ev) (void)hipEventDestroy(b.ev);
+  }
+  if (p->st) (void)hipStreamDestroy(p->st);
+  delete p;
+}
+
+// The key's pipe for groups of G witnesses of nw wires and n_in inputs (kept between calls).
+hipError_t wpipe_get(zkfl_key* k, size_t G, size_t nw, size_t n_in, WitPipe** out) {
+  WitPipe* p = k->wpipe;
+  if (p && p->G == G && p->nw == nw && p->n_in == n_in) {
+    *out = p;
+    return hipSuccess;
+  }
+  wpipe_release(p);
+  k->wpipe = p = new WitPipe();
+  p->G = G;
+  p->nw = nw;
+  p->n_in = n_in;
+  ZK_CHECK(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+  for (auto& b : p->set) {
+    ZK_CHECK(hipMalloc(&b.W, G * nw * 32));
+    ZK_CHECK(hipMalloc(&b.d, G * nw * 32));
+    ZK_CHECK(hipMalloc(&b.in, G * n_in * 32 + 16));
+    ZK_CHECK(hipMalloc(&b.fail, G * 4));
+    ZK_CHECK(hipMalloc(&b.outs, G * sizeof(Fr*)));
+    ZK_CHECK(hipHostMalloc(&b.pin_in, G * n_in * 32 + 16));
+    ZK_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+    std::vector<Fr*> ptrs(G);
+    for (size_t j = 0; j < G; j++) ptrs[j] = b.d + j * nw;
+    ZK_CHECK(hipMemcpy(b.outs, ptrs.data(), G * sizeof(Fr*), hipMemcpyHostToDevice));
+  }
+  *out = p;
+  return hipSuccess;
+}
+
 void key_release(zkfl_key* k) {
   if (!k) return;
+  wpipe_release(k->wpipe);
+  k->wpipe = nullptr;
   for (ProofSlot* s : k->slots) slot_release(s);
   k->slots.clear();
   msm_bases_free_g1(k->bA);
@@ -683,6 +753,7 @@ int wait_full_slot(const zkfl_key* k, ProofSlot* s, uint32_t* failed_assert) {
 struct Job {
   zkfl_key* key = nullptr;
   const Fr* w = nullptr;
+  hipEvent_t w_ready = nullptr;  // the witness w is complete once this event is (batched pipe)
   const WProg* prog = nullptr;
   const uint8_t* input = nullptr;
   size_t n_in = 0;
@@ -735,7 +806,11 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     if (J.prog) {
       rc = enqueue_full_proof(ctx, J.key, J.prog, s, J.input, J.n_in, rsl);
     } else {
-      rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
+      if (J.w_ready) {
+        hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
+        if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
+      }
+      if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
       s->full = false;
     }
     if (rc) break;
@@ -1239,22 +1314,93 @@ static int full_prove_check(const zkfl_ctx* ctx, const zkfl_key* key, const zkfl
   return ZKFL_OK;
 }
 
+// Single-key full prove through the key's witness pipe: groups of G witnesses ahead of the slots
+// (WitPipe), the proofs wait on their group's event.  get_input(i, &ptr) yields job i's input
+// vector (n_in x 32 B std form, < r), in increasing i.
+extern "C++" {
+template <class GetInput>
+int full_prove_piped(zkfl_ctx* ctx, zkfl_key* key, const WProg* prog, size_t n, size_t n_in, GetInput get_input,
+                     const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
+  if (n == 0) return ZKFL_OK;
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  const size_t G = (size_t)key->max_slots, nw = key->nVars, npub = key->nPub;
+  WitPipe* P = nullptr;
+  HIP_TRY(wpipe_get(key, G, nw, n_in, &P), "witness pipe allocation");
+  const size_t rec = 4 + npub * 32;  // per job: fail flag | public signals (pinned, D2H by the pipe)
+  uint8_t* pin_out = nullptr;
+  HIP_TRY(hipHostMalloc(&pin_out, n * rec + 16), "pinned witness outputs");
+  const size_t groups = (n + G - 1) / G;
+  auto enqueue_group = [&](size_t g) -> int {
+    WitPipe::Set& b = P->set[g % 3];
+    const size_t i0 = g * G, m = std::min(G, n - i0);
+    HIP_TRY(hipEventSynchronize(b.ev), "witness set reuse");  // its group of 3 groups ago
+    for (size_t j = 0; j < m; j++) {
+      const uint8_t* in = nullptr;
+      int r = get_input(i0 + j, &in);
+      if (r) return r;
+      memcpy(b.pin_in + j * n_in * 32, in, n_in * 32);
+    }
+    if (n_in) HIP_TRY(hipMemcpyAsync(b.in, b.pin_in, m * n_in * 32, hipMemcpyHostToDevice, P->st), "upload inputs");
+    HIP_TRY(wprog_enqueue(prog, m, b.in, b.W, b.outs, b.fail, P->st), "witness group");
+    for (size_t j = 0; j < m; j++) {
+      uint8_t* o = pin_out + (i0 + j) * rec;
+      HIP_TRY(hipMemcpyAsync(o, b.fail + j, 4, hipMemcpyDeviceToHost, P->st), "witness status");
+      if (npub) HIP_TRY(hipMemcpyAsync(o + 4, b.d + j * nw + 1, npub * 32, hipMemcpyDeviceToHost, P->st), "publics");
+    }
+    HIP_TRY(hipEventRecord(b.ev, P->st), "event");
+    return ZKFL_OK;
+  };
+  int rc = enqueue_group(0);
+  if (rc == ZKFL_OK && groups > 1) rc = enqueue_group(1);
+  if (rc == ZKFL_OK)
+    rc = run_jobs(ctx, n, [&](size_t i, Job& J) {
+      const size_t g = i / G, j = i % G;
+      // slots hold group g - 1 now and have drained group g - 2, whose set group g + 1 takes
+      if (j == 0 && g >= 1 && g + 1 < groups) {
+        int r = enqueue_group(g + 1);
+        if (r) return r;
+      }
+      J.key = key;
+      J.w = P->set[g % 3].d + j * nw;
+      J.w_ready = P->set[g % 3].ev;
+      J.rs = rs ? rs + 64 * i : nullptr;
+      J.proof_out = proofs_out + 256 * i;
+      return ZKFL_OK;
+    });
+  const hipError_t e = hipStreamSynchronize(P->st);
+  if (rc == ZKFL_OK && e != hipSuccess) rc = hip_fail(e, "witness pipe");
+  size_t bad = SIZE_MAX;
+  uint32_t bad_assert = 0;
+  for (size_t i = 0; rc == ZKFL_OK && i < n; i++) {
+    uint32_t f;
+    memcpy(&f, pin_out + i * rec, 4);
+    if (f != 0xFFFFFFFFu) {  // unsatisfied witness: its proof bytes are zeroed
+      memset(proofs_out + 256 * i, 0, 256);
+      if (bad == SIZE_MAX) {
+        bad = i;
+        bad_assert = f;
+      }
+    }
+    if (pubs_out && npub) memcpy(pubs_out + i * npub * 32, pin_out + i * rec + 4, npub * 32);
+  }
+  (void)hipHostFree(pin_out);
+  if (rc == ZKFL_OK && bad != SIZE_MAX)
+    rc = fail(ZKFL_E_CONSTRAINT, "witness " + std::to_string(bad) + ": assert constraint #" +
+                                     std::to_string(bad_assert) + " failed (inputs do not satisfy the circuit)");
+  return rc;
+}
+}  // extern "C++"
+
 int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, size_t n,
                                   const uint8_t* inputs, const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
   if (!ctx || (n && !proofs_out)) return fail(ZKFL_E_ARG, "full_prove: null argument");
   size_t n_in = 0;
   int rc = full_prove_check(ctx, key, prog, n, inputs, &n_in);
   if (rc) return rc;
-  return run_jobs(ctx, n, [&](size_t i, Job& J) {
-    J.key = key;
-    J.prog = prog->p;
-    J.input = inputs + i * n_in * 32;
-    J.n_in = n_in;
-    J.rs = rs ? rs + 64 * i : nullptr;
-    J.proof_out = proofs_out + 256 * i;
-    J.pub_out = pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr;
+  return full_prove_piped(ctx, key, prog->p, n, n_in, [&](size_t i, const uint8_t** in) {
+    *in = inputs + i * n_in * 32;
     return ZKFL_OK;
-  });
+  }, rs, proofs_out, pubs_out);
 }
 
 int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, const char* input_json,
@@ -1352,19 +1498,9 @@ int zkfl_groth16_full_prove_json_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_
   int rc = full_prove_check(ctx, key, prog, 0, nullptr, &n_in);
   if (rc || n == 0) return rc;
   JsonParsePool pool(prog->p, input_jsons, n, n_in);
-  return run_jobs(ctx, n, [&](size_t i, Job& J) {
-    const uint8_t* in = nullptr;
-    int r = pool.get(i, &in);  // parsed values are < r by construction
-    if (r) return r;
-    J.key = key;
-    J.prog = prog->p;
-    J.input = in;
-    J.n_in = n_in;
-    J.rs = rs ? rs + 64 * i : nullptr;
-    J.proof_out = proofs_out + 256 * i;
-    J.pub_out = pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr;
-    return ZKFL_OK;
-  });
+  // parsed values are < r by construction
+  return full_prove_piped(ctx, key, prog->p, n, n_in, [&](size_t i, const uint8_t** in) { return pool.get(i, in); },
+                          rs, proofs_out, pubs_out);
 }
 
 int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,
