@@ -118,6 +118,86 @@ __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, i
     for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
 }
 
+// Same stages, two at a time: each thread takes the 4 elements of a radix-4 butterfly
+// (i0, i0 + q, i0 + 2q, i0 + 3q) through two radix-2 stages in registers, so a tile needs half the
+// LDS round trips and barriers and each thread has two independent products in flight per stage.
+// The products are the radix-2 ones (in a prime field the radix-4 rotation by the 4th root of
+// unity is a full product too), so the result is bit-identical to k_ntt_lds.
+template <bool DIF>
+__global__ void __launch_bounds__(256) k_ntt_lds4(Fr* __restrict__ a, size_t n, int logt, const Fr* __restrict__ tw,
+                                                  int nvec, size_t vstride, const Fr* __restrict__ scale) {
+  __shared__ Fr tile[NTT_LDS_N];
+  const uint32_t T = 1u << logt;
+  const size_t tiles_per_vec = n >> logt;
+  const size_t tile_id = blockIdx.x;
+  const size_t v = tile_id / tiles_per_vec;
+  if (v >= (size_t)nvec) return;
+  Fr* x = a + v * vstride + (tile_id - v * tiles_per_vec) * T;
+  for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) tile[i] = x[i];
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  int s = 0;
+  for (; s + 1 < logt; s += 2) {
+    if (t < (T >> 2)) {
+      if (DIF) {  // spans h1 = T >> (s + 1), h2 = h1 / 2
+        const uint32_t h2 = T >> (s + 2), h1 = h2 << 1;
+        const uint32_t j = t & (h2 - 1), i0 = ((t - j) << 2) + j;
+        const size_t st1 = n / (2 * (size_t)h1), st2 = 2 * st1;
+        const Fr xa = tile[i0], xb = tile[i0 + h2], xc = tile[i0 + h1], xd = tile[i0 + h1 + h2];
+        const Fr a1 = fp_add(xa, xc), c1 = fp_mul(fp_sub(xa, xc), tw[j * st1]);
+        const Fr b1 = fp_add(xb, xd), d1 = fp_mul(fp_sub(xb, xd), tw[(j + h2) * st1]);
+        const Fr w2 = tw[j * st2];
+        tile[i0] = fp_add(a1, b1);
+        tile[i0 + h2] = fp_mul(fp_sub(a1, b1), w2);
+        tile[i0 + h1] = fp_add(c1, d1);
+        tile[i0 + h1 + h2] = fp_mul(fp_sub(c1, d1), w2);
+      } else {  // spans h1 = 2^s, h2 = 2 h1
+        const uint32_t h1 = 1u << s, h2 = h1 << 1;
+        const uint32_t j = t & (h1 - 1), i0 = ((t - j) << 2) + j;
+        const size_t st1 = n / (2 * (size_t)h1), st2 = st1 / 2;
+        const Fr w1 = tw[j * st1];
+        const Fr xa = tile[i0], xb = fp_mul(tile[i0 + h1], w1), xc = tile[i0 + h2], xd = fp_mul(tile[i0 + h2 + h1], w1);
+        const Fr a1 = fp_add(xa, xb), b1 = fp_sub(xa, xb), c1 = fp_add(xc, xd), d1 = fp_sub(xc, xd);
+        const Fr c2 = fp_mul(c1, tw[j * st2]), d2 = fp_mul(d1, tw[(j + h1) * st2]);
+        tile[i0] = fp_add(a1, c2);
+        tile[i0 + h2] = fp_sub(a1, c2);
+        tile[i0 + h1] = fp_add(b1, d2);
+        tile[i0 + h2 + h1] = fp_sub(b1, d2);
+      }
+    }
+    __syncthreads();
+  }
+  if (s < logt) {  // odd tile exponent: the last radix-2 stage
+    const uint32_t half = DIF ? (T >> (s + 1)) : (1u << s);
+    const size_t twstride = n / (2 * (size_t)half);
+    for (uint32_t q = t; q < (T >> 1); q += blockDim.x) {
+      const uint32_t j = q & (half - 1), i0 = ((q - j) << 1) + j, i1 = i0 + half;
+      const Fr u = tile[i0], w = tile[i1], tws = tw[j * twstride];
+      if (DIF) {
+        tile[i0] = fp_add(u, w);
+        tile[i1] = fp_mul(fp_sub(u, w), tws);
+      } else {
+        const Fr wt = fp_mul(w, tws);
+        tile[i0] = fp_add(u, wt);
+        tile[i1] = fp_sub(u, wt);
+      }
+    }
+    __syncthreads();
+  }
+  const size_t base = (tile_id - v * tiles_per_vec) * T;
+  if (scale)  // fused coset scale (inverse pass): x[p] *= inc^bitrev(p) / n
+    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = fp_mul(tile[i], scale[base + i]);
+  else
+    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
+}
+
+// Measured on MI355X (M, 3 x 2^18): NTT stage 0.243/0.245 ms per proof radix-2 vs 0.250/0.250
+// radix-4, bench flat (profiles/r02_s4_ab_ntt_radix4.log): the pass is bound by its products, not
+// by the LDS round trips or barriers.  Radix-2 stays the default.
+#ifndef NTT_RADIX4
+#define NTT_RADIX4 0
+#endif
+
 // The top k stages (spans n/2 .. n/2^k) of a DIF (or the last k of a DIT) transform only combine
 // elements that share their low (logn - k) index bits: a "column" of 2^k elements with stride
 // 2^(logn-k).  One workgroup takes NTT_COL_TILE / 2^k consecutive columns (rows of consecutive
@@ -243,7 +323,10 @@ static hipError_t ntt_dif(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size
     const unsigned groups = (unsigned)((((size_t)1 << (pl.logn - kcol)) / ((size_t)NTT_COL_TILE >> kcol)) * nvec);
     hipLaunchKernelGGL(k_ntt_cols<true>, dim3(groups), dim3(256), 0, st, d, pl.logn, kcol, tw, nvec, vstride);
   }
-  if (logt > 0)
+  if (logt > 0 && NTT_RADIX4)
+    hipLaunchKernelGGL(k_ntt_lds4<true>, dim3((unsigned)((n >> logt) * nvec)), dim3(256), 0, st, d, n, logt, tw,
+                       nvec, vstride, scale);
+  else if (logt > 0)
     hipLaunchKernelGGL(k_ntt_lds<true>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
                        nvec, vstride, scale);
   else if (scale)
@@ -258,7 +341,10 @@ static hipError_t ntt_dit(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size
   const int top = pl.logn - logt;
   const int kcol = top <= NTT_COL_TILE_LOG ? top : 0;
   const size_t nb = (n >> 1) * nvec;
-  if (logt > 0)
+  if (logt > 0 && NTT_RADIX4)
+    hipLaunchKernelGGL(k_ntt_lds4<false>, dim3((unsigned)((n >> logt) * nvec)), dim3(256), 0, st, d, n, logt, tw,
+                       nvec, vstride, (const Fr*)nullptr);
+  else if (logt > 0)
     hipLaunchKernelGGL(k_ntt_lds<false>, dim3((unsigned)((n >> logt) * nvec)), dim3(512), 0, st, d, n, logt, tw,
                        nvec, vstride, (const Fr*)nullptr);
   if (kcol > 0) {
