@@ -113,9 +113,10 @@ def verify_all(ctx, zk, proofs, pubs_of):
 
 def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist):
     """input.json text -> proofs through zkfl_groth16_full_prove_json_batch: host worker threads
-    parse the texts (the C parser) while earlier proofs run, each slot computes its client's
-    witness on its own stream straight into HBM and proves it there; `steps` x `slots` proofs per
-    rank, max-over-ranks time.  The parse of every text is inside the timed region."""
+    parse the texts (the C parser) while earlier proofs run, the witness engine computes a
+    slot-group of witnesses at a time straight into HBM, one group ahead of the slots that prove
+    them; `steps` x `slots` proofs per rank, max-over-ranks time.  The parse of every text is
+    inside the timed region."""
     n = steps * slots
     texts = [json_inputs[i % len(json_inputs)] for i in range(n)]
     key.full_prove_json_batch(wp, texts[:slots])   # warm slot buffers
@@ -127,8 +128,8 @@ def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist):
     assert len(out) == n
     world = dist.get_world_size() if dist is not None else 1
     return {"value": round(world * n / dt, 3), "unit": "proofs/s", "proofs": world * n,
-            "path": "input.json texts -> C parse (host worker threads, overlapped) -> GPU witness on the slot "
-                    "stream -> GPU proof (zkfl_groth16_full_prove_json_batch)"}
+            "path": "input.json texts -> C parse (host worker threads, overlapped) -> GPU witnesses a slot-group "
+                    "at a time, one group ahead -> GPU proofs (zkfl_groth16_full_prove_json_batch)"}
 
 
 def roofline_pass(key, ctx, ws, slots, n=6):
@@ -239,7 +240,7 @@ def c5_leg(ctx, rank, world, rounds, slots, dist):
     return {"value": round(rounds * 16 / elapsed, 3), "unit": "proofs/s", "proofs": rounds * 16, "verified": ok,
             "rounds": rounds, "ms_per_round": round(elapsed / rounds * 1e3, 3), "scaling": "strong",
             "workload": "8 clients x {sgd_verified(8,4,3,1000) training, SecureMaskedUpdate(4,7) secagg} per "
-                        "round, proof k -> GPU k mod G, input.json -> C parse -> GPU witness -> proof "
+                        "round, proof k -> GPU k mod G, input.json -> C parse -> GPU witness groups per key -> proof "
                         "(zkfl_groth16_full_prove_multi, both keys resident)",
             "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
 
@@ -356,7 +357,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slots", type=int, default=20, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
-    ap.add_argument("--e2e-steps", type=int, default=8, help="steps of the input.json -> proof leg (0: skip)")
+    ap.add_argument("--e2e-steps", type=int, default=16, help="steps of the input.json -> proof leg (0: skip)")
     ap.add_argument("--c5-rounds", type=int, default=8, help="federated rounds of the config-5 leg (0: skip)")
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     args = ap.parse_args()

@@ -394,17 +394,6 @@ struct ProofSlot {
   bool busy = false;
   size_t job = 0;                 // index of the in-flight proof in its batch
   uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
-  uint8_t* out_pub = nullptr;     // full-prove: where its public signals go (nullable)
-  // full-prove pipeline (zkfl_groth16_full_prove_batch): the witness engine runs on the slot's
-  // stream straight into wit_d, ahead of the proof that consumes it
-  bool full = false;           // the in-flight proof came from full-prove (check wit fail at wait)
-  size_t wit_n_in = 0, wit_n_wires = 0;
-  Fr* wit_W = nullptr;         // [n_wires] Montgomery scratch of the witness engine
-  Fr* wit_d = nullptr;         // [n_wires] std-form witness = the proof's scalars
-  uint32_t* wit_in = nullptr;  // [n_inputs x 8]
-  uint32_t* wit_fail = nullptr;
-  Fr** wit_outs = nullptr;     // [1] = wit_d
-  uint8_t* wit_pinned = nullptr;  // fail flag (16) | public signals (nPub x 32) | inputs (n_in x 32)
 };
 
 struct zkfl_key {
@@ -446,12 +435,10 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->extra, s->abc,    s->abc_head, s->abc_tail, s->h,        s->res,     s->resB2,
-                  s->d_rs,  s->d_proof, s->wit_W,    s->wit_d,    s->wit_in,   s->wit_fail, s->wit_outs};
+  void* ptrs[] = {s->extra, s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
-  if (s->wit_pinned) (void)hipHostFree(s->wit_pinned);
   for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2})
@@ -689,77 +676,14 @@ int wait_slot(ProofSlot* s) {
   return ZKFL_OK;
 }
 
-// Witness buffers of a slot for the full-prove pipeline (allocated on first use, kept).
-hipError_t slot_witness_buffers(const zkfl_key* k, ProofSlot* s, size_t n_in) {
-  if (s->wit_d && s->wit_n_in == n_in && s->wit_n_wires == k->nVars) return hipSuccess;
-  for (void* p : {(void*)s->wit_W, (void*)s->wit_d, (void*)s->wit_in, (void*)s->wit_fail, (void*)s->wit_outs})
-    if (p) (void)hipFree(p);
-  if (s->wit_pinned) (void)hipHostFree(s->wit_pinned);
-  s->wit_W = s->wit_d = nullptr;
-  s->wit_in = s->wit_fail = nullptr;
-  s->wit_outs = nullptr;
-  s->wit_pinned = nullptr;
-  s->wit_n_in = s->wit_n_wires = 0;
-  const size_t nw = k->nVars;
-  ZK_CHECK(hipMalloc(&s->wit_W, nw * 32));
-  ZK_CHECK(hipMalloc(&s->wit_d, nw * 32));
-  ZK_CHECK(hipMalloc(&s->wit_in, n_in * 32 + 16));
-  ZK_CHECK(hipMalloc(&s->wit_fail, 16));
-  ZK_CHECK(hipMalloc(&s->wit_outs, sizeof(Fr*)));
-  ZK_CHECK(hipHostMalloc(&s->wit_pinned, 16 + (size_t)k->nPub * 32 + n_in * 32));
-  ZK_CHECK(hipMemcpy(s->wit_outs, &s->wit_d, sizeof(Fr*), hipMemcpyHostToDevice));
-  s->wit_n_in = n_in;
-  s->wit_n_wires = nw;
-  return hipSuccess;
-}
-
-// input vector -> witness (slot stream) -> public signals + fail flag D2H -> proof (same stream)
-int enqueue_full_proof(zkfl_ctx* ctx, zkfl_key* k, const WProg* prog, ProofSlot* s, const uint8_t* input,
-                       size_t n_in, const uint32_t rs_host[16]) {
-  HIP_TRY(slot_witness_buffers(k, s, n_in), "full-prove witness buffers");
-  hipStream_t st = s->st_main;
-  uint8_t* pin_fail = s->wit_pinned;
-  uint8_t* pin_pub = s->wit_pinned + 16;
-  uint8_t* pin_in = pin_pub + (size_t)k->nPub * 32;
-  memcpy(pin_in, input, n_in * 32);
-  int pw = ctx->prof.begin("witness", st);
-  if (n_in) HIP_TRY(hipMemcpyAsync(s->wit_in, pin_in, n_in * 32, hipMemcpyHostToDevice, st), "upload inputs");
-  HIP_TRY(wprog_enqueue(prog, 1, s->wit_in, s->wit_W, s->wit_outs, s->wit_fail, st), "witness");
-  ctx->prof.end(pw, st, 1.0);
-  HIP_TRY(hipMemcpyAsync(pin_fail, s->wit_fail, 4, hipMemcpyDeviceToHost, st), "witness status");
-  if (k->nPub)
-    HIP_TRY(hipMemcpyAsync(pin_pub, s->wit_d + 1, (size_t)k->nPub * 32, hipMemcpyDeviceToHost, st), "public signals");
-  int rc = enqueue_proof(ctx, k, s, s->wit_d, rs_host, 0);
-  s->full = true;
-  return rc;
-}
-
-// Wait for a full-prove slot: proof and public signals out; *failed_assert = the witness's first
-// failed assert (0xFFFFFFFF: none), in which case the proof bytes are zeroed.
-int wait_full_slot(const zkfl_key* k, ProofSlot* s, uint32_t* failed_assert) {
-  int rc = wait_slot(s);
-  s->full = false;
-  if (rc) return rc;
-  uint32_t f;
-  memcpy(&f, s->wit_pinned, 4);
-  *failed_assert = f;
-  if (f != 0xFFFFFFFFu && s->out_proof) memset(s->out_proof, 0, 256);
-  if (s->out_pub && k->nPub) memcpy(s->out_pub, s->wit_pinned + 16, (size_t)k->nPub * 32);
-  return ZKFL_OK;
-}
-
-// One proof of a batch.  Either a device-resident witness (w) or a witness-program input vector
-// (prog + input: the full-prove pipeline).  Jobs of one batch may use different keys.
+// One proof of a batch: a device-resident witness, complete once w_ready is (nullptr: already).
+// Jobs of one batch may use different keys.
 struct Job {
   zkfl_key* key = nullptr;
   const Fr* w = nullptr;
-  hipEvent_t w_ready = nullptr;  // the witness w is complete once this event is (batched pipe)
-  const WProg* prog = nullptr;
-  const uint8_t* input = nullptr;
-  size_t n_in = 0;
+  hipEvent_t w_ready = nullptr;  // the witness group of the full-prove pipe (full_prove_piped)
   const uint8_t* rs = nullptr;  // 64 B or nullptr (CSPRNG)
   uint8_t* proof_out = nullptr;
-  uint8_t* pub_out = nullptr;
 };
 
 // The batch scheduler behind every prove entry point: job i goes to the next slot of its key
@@ -771,18 +695,6 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   std::vector<std::pair<zkfl_key*, size_t>> cursor;  // per key: proofs issued in this batch
   int rc = ZKFL_OK;
-  size_t bad_index = SIZE_MAX;
-  uint32_t bad_assert = 0;
-  auto drain = [&](zkfl_key* k, ProofSlot* s) {
-    if (!s->full) return wait_slot(s);
-    uint32_t f = 0xFFFFFFFFu;
-    int r2 = wait_full_slot(k, s, &f);
-    if (r2 == ZKFL_OK && f != 0xFFFFFFFFu && s->job < bad_index) {
-      bad_index = s->job;
-      bad_assert = f;
-    }
-    return r2;
-  };
   for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
     Job J;
     rc = job(i, J);
@@ -797,34 +709,25 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     rc = get_slot(J.key, cursor[c].second++, &s);
     if (rc) break;
     if (s->busy) {
-      rc = drain(J.key, s);
+      rc = wait_slot(s);
       if (rc) break;
     }
     s->job = i;
     s->out_proof = J.proof_out;
-    s->out_pub = J.pub_out;
-    if (J.prog) {
-      rc = enqueue_full_proof(ctx, J.key, J.prog, s, J.input, J.n_in, rsl);
-    } else {
-      if (J.w_ready) {
-        hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
-        if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
-      }
-      if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
-      s->full = false;
+    if (J.w_ready) {
+      hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
+      if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
     }
+    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
     if (rc) break;
     s->busy = true;
   }
   for (auto& kc : cursor)
     for (ProofSlot* s : kc.first->slots)
       if (s->busy) {
-        int r2 = drain(kc.first, s);
+        int r2 = wait_slot(s);
         if (rc == ZKFL_OK) rc = r2;
       }
-  if (rc == ZKFL_OK && bad_index != SIZE_MAX)
-    rc = fail(ZKFL_E_CONSTRAINT, "witness " + std::to_string(bad_index) + ": assert constraint #" +
-                                     std::to_string(bad_assert) + " failed (inputs do not satisfy the circuit)");
   return rc;
 }
 
@@ -1314,66 +1217,102 @@ static int full_prove_check(const zkfl_ctx* ctx, const zkfl_key* key, const zkfl
   return ZKFL_OK;
 }
 
-// Single-key full prove through the key's witness pipe: groups of G witnesses ahead of the slots
-// (WitPipe), the proofs wait on their group's event.  get_input(i, &ptr) yields job i's input
-// vector (n_in x 32 B std form, < r), in increasing i.
+// Full prove through the keys' witness pipes: for each key, groups of G = its slots witnesses one
+// group ahead of its slots (WitPipe); a proof waits on its group's event.  Job i uses key_of(i),
+// program prog_of(i) (nVars / inputs of that key), get_input(i, &ptr) yields its input vector
+// (n_in x 32 B std form, < r; called in increasing i per key), pub_of(i) its public-signal
+// destination (nullable).
 extern "C++" {
-template <class GetInput>
-int full_prove_piped(zkfl_ctx* ctx, zkfl_key* key, const WProg* prog, size_t n, size_t n_in, GetInput get_input,
-                     const uint8_t* rs, uint8_t* proofs_out, uint8_t* pubs_out) {
+template <class KeyOf, class ProgOf, class GetInput, class PubOf>
+int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetInput get_input, const uint8_t* rs,
+                     uint8_t* proofs_out, PubOf pub_of) {
   if (n == 0) return ZKFL_OK;
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-  const size_t G = (size_t)key->max_slots, nw = key->nVars, npub = key->nPub;
-  WitPipe* P = nullptr;
-  HIP_TRY(wpipe_get(key, G, nw, n_in, &P), "witness pipe allocation");
-  const size_t rec = 4 + npub * 32;  // per job: fail flag | public signals (pinned, D2H by the pipe)
+  struct PerKey {
+    zkfl_key* key;
+    const WProg* prog;
+    size_t G = 0, n_in = 0, groups = 0;
+    WitPipe* pipe = nullptr;
+    std::vector<size_t> jobs;  // global indices, in order
+  };
+  std::vector<PerKey> ks;
+  std::vector<size_t> kidx(n), local(n), off(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    zkfl_key* k = key_of(i);
+    size_t c = 0;
+    while (c < ks.size() && ks[c].key != k) c++;
+    if (c == ks.size()) {
+      PerKey pk;
+      pk.key = k;
+      pk.prog = prog_of(i);
+      uint32_t nw = 0, nin = 0, np = 0;
+      wprog_info(pk.prog, &nw, &nin, &np);
+      pk.n_in = nin;
+      pk.G = (size_t)k->max_slots;
+      ks.push_back(pk);
+    }
+    kidx[i] = c;
+    local[i] = ks[c].jobs.size();
+    ks[c].jobs.push_back(i);
+    off[i + 1] = off[i] + 4 + (size_t)k->nPub * 32;  // pinned record: fail flag | public signals
+  }
+  for (auto& pk : ks) {
+    pk.groups = (pk.jobs.size() + pk.G - 1) / pk.G;
+    HIP_TRY(wpipe_get(pk.key, pk.G, pk.key->nVars, pk.n_in, &pk.pipe), "witness pipe allocation");
+  }
   uint8_t* pin_out = nullptr;
-  HIP_TRY(hipHostMalloc(&pin_out, n * rec + 16), "pinned witness outputs");
-  const size_t groups = (n + G - 1) / G;
-  auto enqueue_group = [&](size_t g) -> int {
+  HIP_TRY(hipHostMalloc(&pin_out, off[n] + 16), "pinned witness outputs");
+  auto enqueue_group = [&](PerKey& pk, size_t g) -> int {
+    WitPipe* P = pk.pipe;
     WitPipe::Set& b = P->set[g % 3];
-    const size_t i0 = g * G, m = std::min(G, n - i0);
+    const size_t l0 = g * pk.G, m = std::min(pk.G, pk.jobs.size() - l0), nw = pk.key->nVars;
+    const size_t npub = pk.key->nPub;
     HIP_TRY(hipEventSynchronize(b.ev), "witness set reuse");  // its group of 3 groups ago
     for (size_t j = 0; j < m; j++) {
       const uint8_t* in = nullptr;
-      int r = get_input(i0 + j, &in);
+      int r = get_input(pk.jobs[l0 + j], &in);
       if (r) return r;
-      memcpy(b.pin_in + j * n_in * 32, in, n_in * 32);
+      memcpy(b.pin_in + j * pk.n_in * 32, in, pk.n_in * 32);
     }
-    if (n_in) HIP_TRY(hipMemcpyAsync(b.in, b.pin_in, m * n_in * 32, hipMemcpyHostToDevice, P->st), "upload inputs");
-    HIP_TRY(wprog_enqueue(prog, m, b.in, b.W, b.outs, b.fail, P->st), "witness group");
+    if (pk.n_in)
+      HIP_TRY(hipMemcpyAsync(b.in, b.pin_in, m * pk.n_in * 32, hipMemcpyHostToDevice, P->st), "upload inputs");
+    HIP_TRY(wprog_enqueue(pk.prog, m, b.in, b.W, b.outs, b.fail, P->st), "witness group");
     for (size_t j = 0; j < m; j++) {
-      uint8_t* o = pin_out + (i0 + j) * rec;
+      uint8_t* o = pin_out + off[pk.jobs[l0 + j]];
       HIP_TRY(hipMemcpyAsync(o, b.fail + j, 4, hipMemcpyDeviceToHost, P->st), "witness status");
       if (npub) HIP_TRY(hipMemcpyAsync(o + 4, b.d + j * nw + 1, npub * 32, hipMemcpyDeviceToHost, P->st), "publics");
     }
     HIP_TRY(hipEventRecord(b.ev, P->st), "event");
     return ZKFL_OK;
   };
-  int rc = enqueue_group(0);
-  if (rc == ZKFL_OK && groups > 1) rc = enqueue_group(1);
+  int rc = ZKFL_OK;
+  for (auto& pk : ks)
+    for (size_t g = 0; g < 2 && g < pk.groups && rc == ZKFL_OK; g++) rc = enqueue_group(pk, g);
   if (rc == ZKFL_OK)
     rc = run_jobs(ctx, n, [&](size_t i, Job& J) {
-      const size_t g = i / G, j = i % G;
-      // slots hold group g - 1 now and have drained group g - 2, whose set group g + 1 takes
-      if (j == 0 && g >= 1 && g + 1 < groups) {
-        int r = enqueue_group(g + 1);
+      PerKey& pk = ks[kidx[i]];
+      const size_t g = local[i] / pk.G, j = local[i] % pk.G;
+      // the key's slots hold its group g - 1 now and have drained group g - 2, whose set g + 1 takes
+      if (j == 0 && g >= 1 && g + 1 < pk.groups) {
+        int r = enqueue_group(pk, g + 1);
         if (r) return r;
       }
-      J.key = key;
-      J.w = P->set[g % 3].d + j * nw;
-      J.w_ready = P->set[g % 3].ev;
+      J.key = pk.key;
+      J.w = pk.pipe->set[g % 3].d + j * pk.key->nVars;
+      J.w_ready = pk.pipe->set[g % 3].ev;
       J.rs = rs ? rs + 64 * i : nullptr;
       J.proof_out = proofs_out + 256 * i;
       return ZKFL_OK;
     });
-  const hipError_t e = hipStreamSynchronize(P->st);
-  if (rc == ZKFL_OK && e != hipSuccess) rc = hip_fail(e, "witness pipe");
+  for (auto& pk : ks) {
+    const hipError_t e = hipStreamSynchronize(pk.pipe->st);
+    if (rc == ZKFL_OK && e != hipSuccess) rc = hip_fail(e, "witness pipe");
+  }
   size_t bad = SIZE_MAX;
   uint32_t bad_assert = 0;
   for (size_t i = 0; rc == ZKFL_OK && i < n; i++) {
     uint32_t f;
-    memcpy(&f, pin_out + i * rec, 4);
+    memcpy(&f, pin_out + off[i], 4);
     if (f != 0xFFFFFFFFu) {  // unsatisfied witness: its proof bytes are zeroed
       memset(proofs_out + 256 * i, 0, 256);
       if (bad == SIZE_MAX) {
@@ -1381,7 +1320,8 @@ int full_prove_piped(zkfl_ctx* ctx, zkfl_key* key, const WProg* prog, size_t n, 
         bad_assert = f;
       }
     }
-    if (pubs_out && npub) memcpy(pubs_out + i * npub * 32, pin_out + i * rec + 4, npub * 32);
+    uint8_t* pub = pub_of(i);
+    if (pub) memcpy(pub, pin_out + off[i] + 4, off[i + 1] - off[i] - 4);
   }
   (void)hipHostFree(pin_out);
   if (rc == ZKFL_OK && bad != SIZE_MAX)
@@ -1397,10 +1337,13 @@ int zkfl_groth16_full_prove_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog
   size_t n_in = 0;
   int rc = full_prove_check(ctx, key, prog, n, inputs, &n_in);
   if (rc) return rc;
-  return full_prove_piped(ctx, key, prog->p, n, n_in, [&](size_t i, const uint8_t** in) {
-    *in = inputs + i * n_in * 32;
-    return ZKFL_OK;
-  }, rs, proofs_out, pubs_out);
+  return full_prove_piped(
+      ctx, n, [&](size_t) { return key; }, [&](size_t) { return (const WProg*)prog->p; },
+      [&](size_t i, const uint8_t** in) {
+        *in = inputs + i * n_in * 32;
+        return ZKFL_OK;
+      },
+      rs, proofs_out, [&](size_t i) { return pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr; });
 }
 
 int zkfl_groth16_full_prove_json(zkfl_ctx* ctx, zkfl_key* key, const zkfl_wprog* prog, const char* input_json,
@@ -1499,8 +1442,10 @@ int zkfl_groth16_full_prove_json_batch(zkfl_ctx* ctx, zkfl_key* key, const zkfl_
   if (rc || n == 0) return rc;
   JsonParsePool pool(prog->p, input_jsons, n, n_in);
   // parsed values are < r by construction
-  return full_prove_piped(ctx, key, prog->p, n, n_in, [&](size_t i, const uint8_t** in) { return pool.get(i, in); },
-                          rs, proofs_out, pubs_out);
+  return full_prove_piped(
+      ctx, n, [&](size_t) { return key; }, [&](size_t) { return (const WProg*)prog->p; },
+      [&](size_t i, const uint8_t** in) { return pool.get(i, in); }, rs, proofs_out,
+      [&](size_t i) { return pubs_out ? pubs_out + (size_t)key->nPub * 32 * i : nullptr; });
 }
 
 int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_wprog* const* progs,
@@ -1512,16 +1457,22 @@ int zkfl_groth16_full_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys
     int rc = full_prove_check(ctx, keys[i], progs[i], 1, inputs[i], &n_in[i]);
     if (rc) return fail(rc, "job " + std::to_string(i) + ": " + g_err);
   }
-  return run_jobs(ctx, n, [&](size_t i, Job& J) {
-    J.key = keys[i];
-    J.prog = progs[i]->p;
-    J.input = inputs[i];
-    J.n_in = n_in[i];
-    J.rs = rs ? rs + 64 * i : nullptr;
-    J.proof_out = proofs_out + 256 * i;
-    J.pub_out = pubs_out ? pubs_out[i] : nullptr;
-    return ZKFL_OK;
-  });
+  std::vector<std::pair<const zkfl_key*, const zkfl_wprog*>> kp;  // a key's jobs share its witness program
+  for (size_t i = 0; i < n; i++) {
+    size_t c = 0;
+    while (c < kp.size() && kp[c].first != keys[i]) c++;
+    if (c == kp.size()) kp.push_back({keys[i], progs[i]});
+    else if (kp[c].second != progs[i])
+      return fail(ZKFL_E_ARG, "full_prove_multi: job " + std::to_string(i) +
+                                  " uses its key with another witness program than an earlier job");
+  }
+  return full_prove_piped(
+      ctx, n, [&](size_t i) { return keys[i]; }, [&](size_t i) { return (const WProg*)progs[i]->p; },
+      [&](size_t i, const uint8_t** in) {
+        *in = inputs[i];
+        return ZKFL_OK;
+      },
+      rs, proofs_out, [&](size_t i) { return pubs_out ? pubs_out[i] : nullptr; });
 }
 
 int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, const uint8_t* rs,
@@ -1548,7 +1499,7 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   uint32_t zeros[16] = {0};
   if (rc == ZKFL_OK && s->busy) rc = wait_slot(s);
   if (rc == ZKFL_OK) {
-    s->out_proof = s->out_pub = nullptr;
+    s->out_proof = nullptr;
     rc = enqueue_proof(ctx, key, s, w->d, zeros, 1);
   }
   if (rc == ZKFL_OK) rc = wait_slot(s);
