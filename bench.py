@@ -60,7 +60,7 @@ FQMUL_PEAK_GPS = 1024 * 32 * 2.4 / (128 * 2.2 + 128 * 1.8)     # = 153.6 G Fq-mu
 KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOpsLazy (G1 compute type)
                  "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}     # Fq2PairOps
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "prove")
+PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "assemble", "prove")
 
 CIRCUITS = {
     "M": ("sgd_verified", (128, 4, 7, 1000)),

@@ -174,6 +174,23 @@ def test_config5_round_interleaved_multi_key(gpu_ctx):
     assert total == [sum(g[k] for _, _, g in rnd) % R for k in range(4)], "8-client masks do not cancel"
     assert ow.evaluate(bs, objs[1]) == zkey.read_wtns(wp_s.compute([jobs[1][2]])[0])
 
+    # the witness pipes at small slot counts: several groups per key, a ragged last group
+    key_t.set_slots(3)
+    key_s.set_slots(2)
+    assert gpu_ctx.full_prove_multi(jobs, b"".join(rs)) == out
+    wp_t2 = native.WitnessProgram(gpu_ctx, wprog.compile_program(bt))   # the same key, another program
+    with pytest.raises(native.ZkflError) as e:
+        gpu_ctx.full_prove_multi([jobs[0], (key_t, wp_t2, jobs[2][2])])
+    assert e.value.code == -1
+    wp_t2.close()
+    bad = dict(objs[4])                                # client 2's training input, made unsatisfiable
+    bad["remainder"] = list(bad["remainder"])
+    bad["remainder"][0] = str(int(bad["remainder"][0]) + 1)
+    with pytest.raises(native.ZkflError) as e:         # job 12 sits in key_t's third group
+        gpu_ctx.full_prove_multi(jobs[:12] + [(key_t, wp_t, wprog.input_bytes(bt, bad))] + jobs[13:])
+    assert e.value.code == -7 and "witness 12" in str(e.value)
+    assert gpu_ctx.full_prove_multi(jobs[:4], b"".join(rs[:4])) == out[:4]   # keys keep working
+
     # resident-witness form of the same round: zkfl_groth16_prove_multi
     res = [k.upload(wp.compute([inp])[0]) for k, wp, inp in jobs]
     key_t.set_slots(8)

@@ -233,36 +233,112 @@ __device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Quad-cooperative G1 point operations (k_assemble): four lanes evaluate one XYZZ doubling or
+// addition together.  The products of each dependency level are spread over the quad (lane q
+// computes product q) and broadcast by DPP quad_perm moves; every lane keeps the whole point, so all
+// control flow stays uniform inside a quad.  A chain of point operations then costs one
+// multiply latency per level (doubling 3, addition 4) instead of one per product (9 / 14).
+// ---------------------------------------------------------------------------
+// lane K of the caller's quad to all four lanes: DPP quad_perm [K,K,K,K] (a VALU move, no
+// LDS-path round trip as with ds_bpermute)
+template <int K>
+ZK_DEV Fq quad_bcast(const Fq& v) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], K * 0x55, 0xF, 0xF, false);
+  return r;
+}
+
+ZK_DEV Fq pick4(int q, const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+  // mask arithmetic: a select chain over references is turned into a select of addresses,
+  // which pins every operand to the stack
+  const uint32_t ma = 0u - (uint32_t)(q == 0), mb = 0u - (uint32_t)(q == 1), mc = 0u - (uint32_t)(q == 2),
+                 md = 0u - (uint32_t)(q == 3);
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (a.v[i] & ma) | (b.v[i] & mb) | (c.v[i] & mc) | (d.v[i] & md);
+  return r;
+}
+
+// dbl-2008-s-1 by levels: {U^2, X^2} -> {U V, X V, V ZZ, M^2} -> {M (S - X3), W Y, W ZZZ}
+ZK_DEV G1P quad_dbl(const G1P& p, int q) {
+  if (xyzz_is_inf<FqOps>(p)) return p;
+  const Fq U = fp_dbl(p.Y);
+  const Fq a1 = pick4(q & 1, U, p.X, U, p.X);
+  Fq t = fp_mul(a1, a1);
+  const Fq V = quad_bcast<0>(t), X2 = quad_bcast<1>(t);
+  const Fq M = fp_add(fp_dbl(X2), X2);
+  t = fp_mul(pick4(q, U, p.X, p.ZZ, M), pick4(q, V, V, V, M));
+  const Fq W = quad_bcast<0>(t), S = quad_bcast<1>(t), ZZ3 = quad_bcast<2>(t), M2 = quad_bcast<3>(t);
+  G1P r;
+  r.X = fp_sub(M2, fp_dbl(S));
+  t = fp_mul(pick4(q, M, W, W, W), pick4(q, fp_sub(S, r.X), p.Y, p.ZZZ, p.ZZZ));
+  r.Y = fp_sub(quad_bcast<0>(t), quad_bcast<1>(t));
+  r.ZZ = ZZ3;
+  r.ZZZ = quad_bcast<2>(t);
+  return r;
+}
+
+// add-2008-s by levels: {U1, U2, S1, S2} -> {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2} -> {P PP, U1 PP, ZZ PP}
+// -> {R (Q - X3), S1 PPP, ZZZ PPP}
+ZK_DEV G1P quad_add(const G1P& p, const G1P& o, int q) {
+  if (xyzz_is_inf<FqOps>(o)) return p;
+  if (xyzz_is_inf<FqOps>(p)) return o;
+  Fq t = fp_mul(pick4(q, p.X, o.X, p.Y, o.Y), pick4(q, o.ZZ, p.ZZ, o.ZZZ, p.ZZZ));
+  const Fq U1 = quad_bcast<0>(t), U2 = quad_bcast<1>(t), S1 = quad_bcast<2>(t), S2 = quad_bcast<3>(t);
+  const Fq P = fp_sub(U2, U1), R = fp_sub(S2, S1);
+  if (fp_is_zero(P)) {
+    if (fp_is_zero(R)) return quad_dbl(p, q);
+    return xyzz_inf<FqOps>();
+  }
+  t = fp_mul(pick4(q, P, R, p.ZZ, p.ZZZ), pick4(q, P, R, o.ZZ, o.ZZZ));
+  const Fq PP = quad_bcast<0>(t), R2 = quad_bcast<1>(t), Z12 = quad_bcast<2>(t),
+           ZZZ12 = quad_bcast<3>(t);
+  t = fp_mul(pick4(q, P, U1, Z12, P), PP);
+  const Fq PPP = quad_bcast<0>(t), Q = quad_bcast<1>(t);
+  G1P r;
+  r.ZZ = quad_bcast<2>(t);
+  r.X = fp_sub(fp_sub(R2, PPP), fp_dbl(Q));
+  const Fq QX = fp_sub(Q, r.X);
+  t = fp_mul(pick4(q, R, S1, ZZZ12, R), pick4(q, QX, PPP, PPP, QX));
+  r.Y = fp_sub(quad_bcast<0>(t), quad_bcast<1>(t));
+  r.ZZZ = quad_bcast<2>(t);
+  return r;
+}
+
 // Proof assembly, one block of three waves (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
-//   wave 0, lanes 0..3: k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)), the GLV
-//     halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over a per-lane table
-//     of 1P..8P in LDS; then lane 0: pi_c = C' + H + sum -> proof[48..63]
+//   wave 0, quads 0..3 (lanes 0..15): k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)),
+//     the GLV halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over a per-quad
+//     table of 1P..8P in LDS, each point operation evaluated by the quad (quad_dbl / quad_add);
+//     quad 4: C' + H meanwhile; then quads 0, 1 sum the parts and quad 0 adds C' + H and writes
+//     pi_c (one inversion) -> proof[48..63]
 //   wave 1, lane 0: pi_a affine -> proof[0..15];  wave 2, lane 0: pi_b affine -> proof[16..47]
-// The three field inversions and the four scalar multiplications run side by side; the
-// critical path is 132 doublings + 33 additions + one inversion.
+// The critical path is 132 quad doublings + 33 quad additions + 2 additions + one inversion.
 __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                   const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
   __shared__ G1P tab[4][8];
-  __shared__ G1P part[4];
+  __shared__ G1P part[6];  // the four products, C' + H, then the sum of parts 2 + 3
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave == 0 && lane < 4) {
-    G1P P = res[lane >> 1];
-    if (lane & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
+  const int g = lane >> 2, q = lane & 3;
+  if (wave == 0 && g < 4) {
+    G1P P = res[g >> 1];
+    if (g & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
       Fq beta;
 #pragma unroll
       for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
       P.X = fp_mul(P.X, fp_to_mont(beta));
     }
-    const GlvScalar k = ks[lane];
+    const GlvScalar k = ks[g];
     if (k.neg) P = xyzz_neg<FqOps>(P);
-    tab[lane][0] = P;
-    G1P Q = xyzz_dbl<FqOps>(P);
-    tab[lane][1] = Q;
+    if (q == 0) tab[g][0] = P;
+    G1P Q = quad_dbl(P, q);
+    if (q == 0) tab[g][1] = Q;
 #pragma unroll 1
     for (int j = 2; j < 8; j++) {
-      Q = xyzz_add<FqOps>(Q, P);
-      tab[lane][j] = Q;
+      Q = quad_add(Q, P, q);
+      if (q == 0) tab[g][j] = Q;
     }
     // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
     // d_8i .. d_8i+7, word 4 holds d_32 (the final carry)
@@ -278,27 +354,39 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
 #pragma unroll 1
     for (int w = 32; w >= 0; w--) {
       if (w < 32)
-        for (int j = 0; j < 4; j++) acc = xyzz_dbl<FqOps>(acc);
+        for (int j = 0; j < 4; j++) acc = quad_dbl(acc, q);
       const int wi = w >> 3;
       const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
       const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
       if (nib) {
         const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
-        const G1P t = tab[lane][(d < 0 ? -d : d) - 1];
-        acc = xyzz_add<FqOps>(acc, d < 0 ? xyzz_neg<FqOps>(t) : t);
+        G1P t = tab[g][(d < 0 ? -d : d) - 1];
+        const Fq ny = fp_neg(t.Y);
+#pragma unroll
+        for (int i = 0; i < 8; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
+        acc = quad_add(acc, t, q);
       }
     }
-    part[lane] = acc;
+    if (q == 0) part[g] = acc;
+  } else if (wave == 0 && g == 4) {  // C' + H, off the critical path
+    const G1P c = quad_add(res[2], res[3], q);
+    if (q == 0) part[4] = c;
   } else if (wave == 1 && lane == 0) {
     store_affine_std<FqOps>(xyzz_to_affine<FqOps>(res[0]), proof);
   } else if (wave == 2 && lane == 0) {
     store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    G1P T = xyzz_add<FqOps>(xyzz_add<FqOps>(part[0], part[1]), xyzz_add<FqOps>(part[2], part[3]));
-    G1P C = xyzz_add<FqOps>(xyzz_add<FqOps>(res[2], res[3]), T);
-    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
+  if (wave == 0 && g == 1) {
+    const G1P t = quad_add(part[2], part[3], q);
+    if (q == 0) part[5] = t;
+  }
+  G1P t01 = xyzz_inf<FqOps>();
+  if (wave == 0 && g == 0) t01 = quad_add(part[0], part[1], q);
+  __syncthreads();
+  if (wave == 0 && g == 0) {
+    const G1P C = quad_add(quad_add(t01, part[5], q), part[4], q);
+    if (q == 0) store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
   }
 }
 
@@ -659,8 +747,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (!plain) {
+    const int pa = prof->begin("assemble", st);
     hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
                        reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+    prof->end(pa, st, 1.0);
     HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   }
   prof->end(pp, st, 1.0);
