@@ -250,14 +250,12 @@ ZK_DEV Fq quad_bcast(const Fq& v) {
   return r;
 }
 
-ZK_DEV Fq pick4(int q, const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
-  // mask arithmetic: a select chain over references is turned into a select of addresses,
-  // which pins every operand to the stack
-  const uint32_t ma = 0u - (uint32_t)(q == 0), mb = 0u - (uint32_t)(q == 1), mc = 0u - (uint32_t)(q == 2),
-                 md = 0u - (uint32_t)(q == 3);
+ZK_DEV Fq pick4(int q, Fq a, Fq b, Fq c, Fq d) {
+  // operands by value: over references the select chain becomes a select of addresses, which
+  // pins every operand to the stack
   Fq r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (a.v[i] & ma) | (b.v[i] & mb) | (c.v[i] & mc) | (d.v[i] & md);
+  for (int i = 0; i < 8; i++) r.v[i] = (q & 2) ? ((q & 1) ? d.v[i] : c.v[i]) : ((q & 1) ? b.v[i] : a.v[i]);
   return r;
 }
 
