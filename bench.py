@@ -51,13 +51,16 @@ IMPL_BYTES_PER_ENTRY = {"msm_accumulate_g1": 2 + 4 + 64, "msm_accumulate_g2": 2 
 # Fq multiplications per entry: XYZZ mixed addition madd-2008-s = 8M + 2S over Fq (G1), over Fq2
 # (G2: 3 Fq products per Fq2 product)
 FQMUL_PER_ENTRY = {"msm_accumulate_g1": 10, "msm_accumulate_g2": 30}
-# Integer-VALU ceiling from ISA issue rates, not from this library's own multiply: a 256-bit
-# product-scanning Montgomery multiply is 128 v_mad_u64_u32 (8x8 limb products for a*b and for
-# m*p) + 128 carry adds; issue costs relative to a 2-cycle wave64 v_add_u32 are 2.2x / 1.8x
-# (tools/isa_rate.hip, MI355X).  1024 SIMDs x 32 lanes/cycle x 2.4 GHz / (128 x 2.2 + 128 x 1.8).
-FQMUL_PEAK_GPS = 1024 * 32 * 2.4 / (128 * 2.2 + 128 * 1.8)     # = 153.6 G Fq-mul/s
+# Integer-VALU ceiling from ISA issue rates, not from this library's own timing: the G1 kernels
+# multiply in nine 29-bit limbs (csrc/field29.h), a Montgomery product is 81 + 81 v_mad_u64_u32
+# (a*b and m*p limb products, 64-bit column accumulators, no carry adds); issue cost relative to a
+# 2-cycle wave64 v_add_u32 is 2.2x (tools/isa_rate.hip, MI355X).  1024 SIMDs x 32 lanes/cycle x
+# 2.4 GHz / (162 x 2.2) = 220.7 G Fq-mul/s.  (32-bit limbs: 128 mad + 128 carry adds, 2.2x / 1.8x:
+# 153.6 G/s -- the G2 kernels' ceiling.)
+FQMUL_PEAK_GPS = 1024 * 32 * 2.4 / (162 * 2.2)
+FQMUL_PEAK_GPS_32 = 1024 * 32 * 2.4 / (128 * 2.2 + 128 * 1.8)
 # rocprofv3 kernel names of the instrumented kernels (profiles/pmc_traffic.json keys)
-KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOpsLazy (G1 compute type)
+KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOps29 (G1 compute type)
                  "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}     # Fq2PairOps
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "assemble", "prove")
@@ -187,7 +190,8 @@ def roofline(prof, key):
             "launches": launches, "entries_per_launch": round(entries),
             "valu": {"achieved": round(fq, 2), "peak": round(FQMUL_PEAK_GPS, 1), "unit": "G Fq-mul/s",
                      "frac": round(fq / FQMUL_PEAK_GPS, 4),
-                     "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (128 mad x 2.2 + 128 addc x 1.8)"}}
+                     "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (162 mad x 2.2), 29-bit limbs",
+                     "peak_32bit_limbs": round(FQMUL_PEAK_GPS_32, 1)}}
 
 
 def c5_leg(ctx, rank, world, rounds, slots, dist):

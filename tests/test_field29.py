@@ -1,0 +1,196 @@
+"""29-bit-limb G1 arithmetic (csrc/field29.h) against Python big integers, on the CPU.
+
+The formulas are __host__ __device__: tools/f29_check.cpp drives them from stdin.  Checked:
+Montgomery products (R = 2^261) and product sums at the extreme operand kinds the bound analysis
+allows (lazy limbs), and the XYZZ madd / add / dbl on real BN254 points with coordinates pushed to
+the top of their documented ranges (X, Y < 6p, ZZ, ZZZ < 2p), including the P == 0 special cases
+(doubling, cancellation to infinity) -- results equal the affine sums and stay inside the ranges.
+"""
+import os
+import random
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd")
+HIPCC = "/opt/rocm/bin/hipcc"
+P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+R = pow(2, 261, P)
+RINV = pow(R, -1, P)
+MASK = (1 << 29) - 1
+
+
+@pytest.fixture(scope="module")
+def f29(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = str(tmp_path_factory.mktemp("f29") / "f29_check")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17", "-I" + os.path.join(PKG, "csrc"), "-o", out,
+                    os.path.join(ROOT, "tools", "f29_check.cpp")], check=True, capture_output=True)
+
+    def run(lines):
+        r = subprocess.run([out], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True)
+        return [[limbs_val(t) for t in ln.split()] for ln in r.stdout.strip().split("\n")]
+    return run
+
+
+def limbs(v, lazy=None):
+    """Normalized 9 x 29-bit limbs of v (or the given raw limb list)."""
+    if lazy is not None:
+        return ",".join(str(x) for x in lazy)
+    assert 0 <= v < 1 << 261
+    return ",".join(str((v >> (29 * i)) & MASK if i < 8 else v >> 232) for i in range(9))
+
+
+def limbs_val(t):
+    ls = [int(x) for x in t.split(",")]
+    assert all(x <= MASK for x in ls[:8]), "not normalized"
+    return sum(x << (29 * i) for i, x in enumerate(ls))
+
+
+def lazy_limbs(rng, top):
+    """Random limb vector with limbs 0..7 up to `top` (not normalized) and its value."""
+    ls = [rng.randrange(top) for _ in range(8)] + [rng.randrange(1 << 22)]
+    return ls, sum(x << (29 * i) for i, x in enumerate(ls))
+
+
+def test_mul_and_mulsum_at_lazy_extremes(f29):
+    rng = random.Random(29)
+    cases, want = [], []
+    for k in range(400):
+        a, va = lazy_limbs(rng, 2 << 29)          # U = 2Y kind
+        b, vb = lazy_limbs(rng, 2 << 29)
+        if k % 4 == 0:  # all-max limbs
+            a = [(2 << 29) - 1] * 8 + [1 << 22]
+            va = sum(x << (29 * i) for i, x in enumerate(a))
+            b, vb = a, va
+        cases.append(f"mul {limbs(0, a)} {limbs(0, b)}")
+        want.append(("mul", va, vb))
+        n, vn = lazy_limbs(rng, 1 << 29)           # normalized
+        q, vq = lazy_limbs(rng, 3 << 29)           # QX kind
+        c, vc = lazy_limbs(rng, 2 << 29)           # nY kind
+        d, vd = lazy_limbs(rng, 1 << 29)
+        if k % 4 == 1:
+            n = d = [MASK] * 8 + [1 << 22]
+            q = [(3 << 29) - 1] * 8 + [1 << 22]
+            c = [(2 << 29) - 1] * 8 + [1 << 22]
+            vn, vq, vc, vd = (sum(x << (29 * i) for i, x in enumerate(t)) for t in (n, q, c, d))
+        cases.append(f"mulsum2 {limbs(0, n)} {limbs(0, q)} {limbs(0, c)} {limbs(0, d)}")
+        want.append(("mulsum2", vn * vq + vc * vd, None))
+    got = f29(cases)
+    for (kind, x, y), (r,) in zip(want, got):
+        prod = x * y if kind == "mul" else x
+        assert r % P == prod * RINV % P
+        assert r < P + prod // (1 << 261) + 1  # Montgomery bound: no final subtraction
+
+
+def test_below256(f29):
+    rng = random.Random(5)
+    vals = [rng.randrange(6 * P) for _ in range(300)] + [(1 << 256) - 1, 1 << 256, 6 * P - 1, 0, 2 * P]
+    got = f29([f"below256 {limbs(v)}" for v in vals])
+    for v, (r,) in zip(vals, got):
+        assert r % P == v % P and r < 1 << 256
+
+
+# --- BN254 G1 reference (affine, real coordinates) ---
+def g1_add(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    if a[0] == b[0]:
+        if (a[1] + b[1]) % P == 0:
+            return None
+        lam = 3 * a[0] * a[0] * pow(2 * a[1], -1, P) % P
+    else:
+        lam = (b[1] - a[1]) * pow(b[0] - a[0], -1, P) % P
+    x = (lam * lam - a[0] - b[0]) % P
+    return (x, (lam * (a[0] - x) - a[1]) % P)
+
+
+def g1_mul(k, a):
+    r = None
+    while k:
+        if k & 1:
+            r = g1_add(r, a)
+        a = g1_add(a, a)
+        k >>= 1
+    return r
+
+
+def to_xyzz(pt, rng, top):
+    """pt in XYZZ, Montgomery domain, coordinates lifted by random multiples of p (top: max)."""
+    if pt is None:
+        zz = rng.choice([0, P])
+        return [R + rng.randrange(5) * P, R + rng.randrange(5) * P, zz, zz]
+    z = rng.randrange(1, P)
+    zz, zzz = z * z % P, z * z * z % P
+    X, Y = pt[0] * zz % P, pt[1] * zzz % P
+    m = lambda v: v * R % P
+    lift = lambda v, k: v + (k if top else rng.randrange(k + 1)) * P
+    return [lift(m(X), 5), lift(m(Y), 5), lift(m(zz), 1), lift(m(zzz), 1)]
+
+
+def from_xyzz(c):
+    X, Y, ZZ, ZZZ = (v * RINV % P for v in c)
+    assert c[0] < 6 * P and c[1] < 6 * P and c[2] < 2 * P and c[3] < 2 * P, "range"
+    if ZZ == 0:
+        return None
+    assert pow(ZZ, 3, P) == pow(ZZZ, 2, P)
+    return (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
+
+
+def pt_str(c):
+    return " ".join(limbs(v) for v in c)
+
+
+def test_point_formulas(f29):
+    rng = random.Random(261)
+    G = (1, 2)
+    pts = [g1_mul(rng.randrange(1, P), G) for _ in range(24)]
+    cases, want = [], []
+    for i in range(240):
+        a, b = rng.choice(pts), rng.choice(pts)
+        kind = i % 6
+        if kind == 1:
+            b = a                                   # P == 0, R == 0: doubling
+        elif kind == 2:
+            b = (a[0], (P - a[1]) % P)              # P == 0, R != 0: infinity
+        elif kind == 3 and i % 12 == 3:
+            a = None                                # accumulator at infinity
+        top = i % 2 == 0
+        pa = to_xyzz(a, rng, top)
+        # madd: base canonical (the kernel's negation p - y keeps y in (0, p])
+        bx, by = b[0] * R % P, b[1] * R % P
+        cases.append(f"madd {pt_str(pa)} {limbs(bx)} {limbs(by)}")
+        want.append(g1_add(a, b))
+        pb = to_xyzz(b, rng, not top)
+        cases.append(f"add {pt_str(pa)} {pt_str(pb)}")
+        want.append(g1_add(a, b))
+        cases.append(f"dbl {pt_str(pa)}")
+        want.append(g1_add(a, a))
+    got = f29(cases)
+    for w, g in zip(want, got):
+        assert from_xyzz(g) == w
+
+
+def test_madd_chain_stays_in_range(f29):
+    """Long accumulation chains feed outputs back as inputs (the bucket accumulator)."""
+    rng = random.Random(7)
+    G = (1, 2)
+    bases = [g1_mul(rng.randrange(1, P), G) for _ in range(16)]
+    acc_pts = [None] * 8
+    acc = [to_xyzz(None, rng, False) for _ in range(8)]
+    for step in range(40):
+        lines, exp = [], []
+        for j in range(8):
+            b = rng.choice(bases)
+            lines.append(f"madd {pt_str(acc[j])} {limbs(b[0] * R % P)} {limbs(b[1] * R % P)}")
+            exp.append(g1_add(acc_pts[j], b))
+        got = f29(lines)
+        for j in range(8):
+            acc[j] = got[j]
+            acc_pts[j] = exp[j]
+            assert from_xyzz(acc[j]) == exp[j]

@@ -29,6 +29,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
+#include "field29.h"
 #include "msm_api.h"
 
 namespace zkfl {
@@ -38,8 +39,11 @@ namespace zkfl {
 // (Fq2PairOps): the accumulation 168 VGPRs (3 waves/SIMD), the tails 179-241 (2 waves/SIMD), no
 // spills; one lane per G2 point needed > 256 registers, so a single wave owned the whole SIMD
 // for the kernel's duration (measured 186 -> 208 proofs/s moving G2 to lane pairs).
+// G1 in 29-bit limbs (field29.h) needs ~140 VGPRs in the accumulation: 3 waves/SIMD without
+// spills measured 352.8 proofs/s against 342.9 at 4 waves with 17 spilled VGPRs (32-bit limbs,
+// 4 waves: 331.3).
 #ifndef MSM_G1_WAVES
-#define MSM_G1_WAVES 4
+#define MSM_G1_WAVES 3
 #endif
 #ifndef MSM_G2_WAVES
 #define MSM_G2_WAVES 3
@@ -145,20 +149,68 @@ template <>
 struct MsmIO<FqOpsCompact> : MsmIOSameLayout<FqOpsCompact> {};
 template <>
 struct MsmIO<FqOpsLazy> : MsmIOSameLayout<FqOpsLazy> {};
+// G1 in 29-bit limbs (field29.h): the same 8 x 32-bit storage, converted on every load / store
+// (stored values < 2^256, in the 2^261 Montgomery domain)
+template <>
+struct MsmIO<FqOps29> {
+  using S = FqOps;
+  static constexpr int LANES = 1;
+  static ZK_DEV Affine<FqOps29> ld_aff(const Affine<S>* p, size_t i) {
+    const Affine<S> a = p[i];
+    return {f29_pack(a.x.v), f29_pack(a.y.v)};
+  }
+  static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
+    return reinterpret_cast<const uint4*>(p + i) + q;
+  }
+  static ZK_DEV Affine<FqOps29> from_pieces(const uint4 (&u)[4]) {
+    Affine<S> a;
+    memcpy(&a, u, sizeof(a));
+    return {f29_pack(a.x.v), f29_pack(a.y.v)};
+  }
+  static ZK_DEV XYZZ<FqOps29> ld(const XYZZ<S>* p, size_t i) {
+    const XYZZ<S> a = p[i];
+    return {f29_pack(a.X.v), f29_pack(a.Y.v), f29_pack(a.ZZ.v), f29_pack(a.ZZZ.v)};
+  }
+  static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<FqOps29>& v) {
+    XYZZ<S> a;
+    f29_unpack(a.X.v, f29_below256(v.X));
+    f29_unpack(a.Y.v, f29_below256(v.Y));
+    f29_unpack(a.ZZ.v, v.ZZ);
+    f29_unpack(a.ZZZ.v, v.ZZZ);
+    p[i] = a;
+  }
+};
 // Compute type the MSM kernels use for a stored curve (G1: redundant [0, 2p) arithmetic with
 // the compact multiply; MSM_G1_NO_LAZY: canonical values, compact multiply).
 template <class F>
 struct MsmCompute {
   using type = F;
 };
+// MSM_G1_F29 (default): 29-bit limbs (field29.h); 0: 32-bit limbs in [0, 2p) (FqOpsLazy).
+#ifndef MSM_G1_F29
+#define MSM_G1_F29 1
+#endif
 template <>
 struct MsmCompute<FqOps> {
-#ifndef MSM_G1_NO_LAZY
+#if MSM_G1_F29
+  using type = FqOps29;
+#elif !defined(MSM_G1_NO_LAZY)
   using type = FqOpsLazy;
 #else
   using type = FqOpsCompact;
 #endif
 };
+
+// Bases into the compute type's Montgomery domain (FqOps29: x 2^261 = fp_mul(x 2^256, 2^261 mod p)).
+static __global__ void __launch_bounds__(256) k_msm_to_m29(Affine<FqOps>* __restrict__ b, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fq c;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
+  b[i].x = fp_mul(b[i].x, c);
+  b[i].y = fp_mul(b[i].y, c);
+}
 template <>
 struct MsmCompute<Fq2Ops> {
   using type = Fq2PairOps;
@@ -517,7 +569,9 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
     y = IO::ld(shy, 0);
     constexpr int lq = __builtin_ctz((unsigned)Q);
     for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
-    IO::st(out_a, blockIdx.x, xyzz_canon<F>(xyzz_add<F>(y, x)));  // [0, p) when it leaves the MSM
+    const XYZZ<F> a = xyzz_add<F>(y, x);
+    // canonical (and, for FqOps29, back in the 2^256 domain) only when it leaves the MSM
+    IO::st(out_a, blockIdx.x, L0 ? a : xyzz_canon<F>(a));
     IO::st(out_s, blockIdx.x, R);
   }
 }
@@ -551,6 +605,10 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
     ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
+  if constexpr (std::is_same<typename MsmCompute<F>::type, FqOps29>::value) {
+    if (b.n)
+      hipLaunchKernelGGL(k_msm_to_m29, dim3(zk_grid(b.n * MSM_W, 256)), dim3(256), 0, st, b.bases_w, b.n * MSM_W);
+  }
   return hipGetLastError();
 }
 
