@@ -194,3 +194,86 @@ def test_madd_chain_stays_in_range(f29):
             acc[j] = got[j]
             acc_pts[j] = exp[j]
             assert from_xyzz(acc[j]) == exp[j]
+
+
+# --- G2 (Fq2 on lane pairs; the host policy runs both lanes of a pair) ---
+def _fq2():
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import bn254
+    return bn254
+
+
+def to_xyzz2(bn, pt, rng, top):
+    F2 = bn.Fq2
+    if pt is None:
+        zz = rng.choice([0, P])
+        one = [R + rng.randrange(5) * P, rng.randrange(5) * P]
+        return one + one + [zz, zz, zz, zz]
+    z = F2(rng.randrange(1, P), rng.randrange(P))
+    zz = z * z
+    zzz = zz * z
+    X, Y = pt[0] * zz, pt[1] * zzz
+    out = []
+    for v, k in ((X, 5), (Y, 5), (zz, 1), (zzz, 1)):
+        for c in (v.c0, v.c1):
+            out.append(c * R % P + (k if top else rng.randrange(k + 1)) * P)
+    return out
+
+
+def from_xyzz2(bn, c):
+    F2 = bn.Fq2
+    assert all(v < 6 * P for v in c[:4]) and all(v < 2 * P for v in c[4:]), "range"
+    X, Y, ZZ, ZZZ = (F2(c[2 * i] * RINV, c[2 * i + 1] * RINV) for i in range(4))
+    if ZZ.is_zero():
+        return None
+    assert ZZ * ZZ * ZZ == ZZZ * ZZZ
+    return (X * ZZ.inv(), Y * ZZZ.inv())
+
+
+def test_g2_point_formulas(f29):
+    bn = _fq2()
+    rng = random.Random(2261)
+    pts = [bn.mul(bn.G2_GEN, rng.randrange(1, P)) for _ in range(12)]
+    cases, want = [], []
+    for i in range(150):
+        a, b = rng.choice(pts), rng.choice(pts)
+        kind = i % 6
+        if kind == 1:
+            b = a
+        elif kind == 2:
+            b = bn.neg(a)
+        elif kind == 3 and i % 12 == 3:
+            a = None
+        top = i % 2 == 0
+        pa = to_xyzz2(bn, a, rng, top)
+        base = [b[0].c0 * R % P, b[0].c1 * R % P, b[1].c0 * R % P, b[1].c1 * R % P]
+        cases.append("g2madd " + pt_str(pa) + " " + pt_str(base))
+        want.append(bn.add(a, b))
+        pb = to_xyzz2(bn, b, rng, not top)
+        cases.append("g2add " + pt_str(pa) + " " + pt_str(pb))
+        want.append(bn.add(a, b))
+        cases.append("g2dbl " + pt_str(pa))
+        want.append(bn.add(a, a))
+    got = f29(cases)
+    for w, g in zip(want, got):
+        assert from_xyzz2(bn, g) == w
+
+
+def test_g2_madd_chain_stays_in_range(f29):
+    bn = _fq2()
+    rng = random.Random(77)
+    bases = [bn.mul(bn.G2_GEN, rng.randrange(1, P)) for _ in range(8)]
+    acc_pts = [None] * 4
+    acc = [to_xyzz2(bn, None, rng, False) for _ in range(4)]
+    for step in range(30):
+        lines, exp = [], []
+        for j in range(4):
+            b = rng.choice(bases)
+            base = [b[0].c0 * R % P, b[0].c1 * R % P, b[1].c0 * R % P, b[1].c1 * R % P]
+            lines.append("g2madd " + pt_str(acc[j]) + " " + pt_str(base))
+            exp.append(bn.add(acc_pts[j], b))
+        got = f29(lines)
+        for j in range(4):
+            acc[j], acc_pts[j] = got[j], exp[j]
+            assert from_xyzz2(bn, acc[j]) == exp[j]

@@ -2,6 +2,7 @@
 // tests/test_field29.py: the formulas are __host__ __device__, so their bound analysis is
 // checked on the CPU against Python big integers.  One operation per stdin line:
 //   mul a b | mulsum2 a b c d | below256 a | dbl P | madd P x y | add P Q
+//   g2dbl P | g2madd P x y | g2add P Q   (Fq2 values as two elements: c0 c1)
 // field elements as 9 comma-separated decimal limbs, points as X Y ZZ ZZZ; the result is
 // printed the same way.
 // Build: hipcc --offload-arch=gfx950 -O1 -std=c++17 -I<pkg>/csrc -o f29_check f29_check.cpp
@@ -47,6 +48,64 @@ static void wrp(const XYZZ<FqOps29>& p) {
   wr(p.ZZZ);
 }
 
+// both lanes of a pair side by side (the device policy is Pair29Dev)
+struct PairHost {
+  struct V {
+    F29 l[2];
+  };
+  static V zero() { return {f29_zero(), f29_zero()}; }
+  static V one() { return {f29_const(P29::ONE), f29_zero()}; }
+  static V swap(const V& a) { return {a.l[1], a.l[0]}; }
+  static V sel(const V& v1, const V& v0) { return {v0.l[0], v1.l[1]}; }
+  static bool is_zero(const V& a) { return f29_is_zero(a.l[0]) && f29_is_zero(a.l[1]); }
+  static V add(const V& a, const V& b) { return {f29_add_lazy(a.l[0], b.l[0]), f29_add_lazy(a.l[1], b.l[1])}; }
+  static void norm(V& a) {
+    f29_norm(a.l[0]);
+    f29_norm(a.l[1]);
+  }
+  static V ksub(const uint32_t (&k)[9], const V& a, const V& b) {
+    return {f29_ksub(k, a.l[0], b.l[0]), f29_ksub(k, a.l[1], b.l[1])};
+  }
+  static V ksub3(const uint32_t (&k)[9], const V& a, const V& b, const V& c, const V& d) {
+    return {f29_ksub3(k, a.l[0], b.l[0], c.l[0], d.l[0]), f29_ksub3(k, a.l[1], b.l[1], c.l[1], d.l[1])};
+  }
+  static V mulsum2(const V& a, const V& b, const V& c, const V& d) {
+    return {f29_mulsum2(a.l[0], b.l[0], c.l[0], d.l[0]), f29_mulsum2(a.l[1], b.l[1], c.l[1], d.l[1])};
+  }
+  static V mulsum4(const V (&x)[4], const V (&y)[4]) {
+    V r;
+    for (int h = 0; h < 2; h++) {
+      const F29 xs[4] = {x[0].l[h], x[1].l[h], x[2].l[h], x[3].l[h]};
+      const F29 ys[4] = {y[0].l[h], y[1].l[h], y[2].l[h], y[3].l[h]};
+      r.l[h] = f29_mulsum4(xs, ys);
+    }
+    return r;
+  }
+};
+
+static PairHost::V rd2(std::istringstream& in) {
+  PairHost::V v;
+  v.l[0] = rd(in);
+  v.l[1] = rd(in);
+  return v;
+}
+
+static G2P29<PairHost> rdp2(std::istringstream& in) {
+  G2P29<PairHost> p;
+  p.X = rd2(in);
+  p.Y = rd2(in);
+  p.ZZ = rd2(in);
+  p.ZZZ = rd2(in);
+  return p;
+}
+
+static void wrp2(const G2P29<PairHost>& p) {
+  for (const PairHost::V* v : {&p.X, &p.Y, &p.ZZ, &p.ZZZ}) {
+    wr(v->l[0]);
+    wr(v->l[1]);
+  }
+}
+
 int main() {
   std::string line;
   while (std::getline(std::cin, line)) {
@@ -72,6 +131,15 @@ int main() {
     } else if (op == "add") {
       XYZZ<FqOps29> p = rdp(in), q = rdp(in);
       wrp(f29_add(p, q));
+    } else if (op == "g2dbl") {
+      wrp2(f2_dbl<PairHost>(rdp2(in)));
+    } else if (op == "g2madd") {
+      G2P29<PairHost> p = rdp2(in);
+      PairHost::V x = rd2(in), y = rd2(in);
+      wrp2(f2_madd<PairHost>(p, x, y));
+    } else if (op == "g2add") {
+      G2P29<PairHost> p = rdp2(in), q = rdp2(in);
+      wrp2(f2_add<PairHost>(p, q));
     } else {
       printf("?");
     }

@@ -52,6 +52,14 @@ struct P29 {
                                        0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
   static constexpr uint32_t K3_2[9] = {0x4976f7d5u, 0x430d2222u, 0x5557e9ebu, 0x487f6870u, 0x40918c66u,
                                        0x4891c240u, 0x41f4a3c1u, 0x4b14729au, 0x00912ce9u};
+  static constexpr uint32_t K3_1[9] = {0x2976f7d5u, 0x230d2223u, 0x3557e9ecu, 0x287f6871u, 0x20918c67u,
+                                       0x2891c241u, 0x21f4a3c2u, 0x2b14729bu, 0x00912ceau};
+  static constexpr uint32_t K4_1[9] = {0x21f3f51cu, 0x241182dau, 0x31ca8d3bu, 0x2b548b42u, 0x361765dfu,
+                                       0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u};
+  static constexpr uint32_t K9_1[9] = {0x3c64e77fu, 0x2927666bu, 0x2007bdc6u, 0x397e3957u, 0x21b4a537u,
+                                       0x39b546c5u, 0x25ddeb48u, 0x213d57d3u, 0x01b386c1u};
+  static constexpr uint32_t K13_1[9] = {0x3e58dc9bu, 0x2d38e946u, 0x31d24b02u, 0x24d2c49au, 0x37cc0b18u,
+                                        0x252249c7u, 0x2879704du, 0x3aadf0a3u, 0x027517fau};
   static constexpr uint32_t K4_3[9] = {0x61f3f51cu, 0x641182d8u, 0x71ca8d39u, 0x6b548b40u, 0x761765ddu,
                                        0x6b6d02ffu, 0x629b8501u, 0x797098cdu, 0x00c19136u};
   static constexpr uint32_t K5_1[9] = {0x3a70f263u, 0x2515e390u, 0x2e3d308au, 0x2e29ae13u, 0x2b9d3f57u,
@@ -184,6 +192,40 @@ ZK_HD F29 f29_mul(const F29& a, const F29& b) {
 #pragma unroll
     for (int i = k - 8; i < 9; i++) {
       acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)m[i] * P29::P[k - i];
+    }
+    r.v[k - 9] = (uint32_t)acc & P29::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return r;
+}
+
+// (sum_{j<4} x_j y_j) 2^-261 with one reduction (the G2 y-coordinate product pair)
+ZK_HD F29 f29_mulsum4(const F29 (&x)[4], const F29 (&y)[4]) {
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[i] * y[j].v[k - i];
+      acc += (uint64_t)m[i] * P29::P[k - i];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[k] * y[j].v[0];
+    m[k] = ((uint32_t)acc * P29::NINV) & P29::MASK;
+    acc += (uint64_t)m[k] * P29::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int i = k - 8; i < 9; i++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[i] * y[j].v[k - i];
       acc += (uint64_t)m[i] * P29::P[k - i];
     }
     r.v[k - 9] = (uint32_t)acc & P29::MASK;
@@ -346,6 +388,192 @@ ZK_HD XYZZ<FqOps29> f29_add(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
   return r;
 }
 
+// ---------------------------------------------------------------------------
+// G2: Fq2 on lane pairs (lane 2k + h holds component h of every value, as Fq2PairOps), each
+// component in 29-bit limbs.  The formulas are written against a lane policy L (the device one
+// exchanges partner components through DPP; the host one in tools/f29_check.cpp runs both lanes
+// of a pair side by side), so tests/test_field29.py checks the same code on the CPU.
+//   L::V  one lane's component;  swap: the partner's;  sel(v1, v0): v1 in lane 1, v0 in lane 0;
+//   is_zero: both components == 0 mod p (each normalized, < 2p).
+// An Fq2 product is one sum of two Fq products per lane with one reduction:
+//   lane 0: a0 b0 + (K - a1) b1,  lane 1: a1 b0 + a0 b1     (f2_mul; a normalized, K > a)
+// so a product of a < A p and b < B p is < p + (A + K) B p / 169 per component; the column bound
+// needs a normalized and b normalized or lazy with limbs < 2^30.  Bounds per formula below, in
+// units of p, for each component; invariant between operations as for G1: X, Y < 6p,
+// ZZ, ZZZ < 2p, normalized.
+// ---------------------------------------------------------------------------
+template <class L>
+struct G2P29 {
+  typename L::V X, Y, ZZ, ZZZ;
+};
+
+template <class L>
+ZK_HD typename L::V f2_mul(const typename L::V& a, const typename L::V& b, const uint32_t (&k)[9]) {
+  using V = typename L::V;
+  const V pa = L::swap(a), pb = L::swap(b);
+  const V zero = L::zero();
+  return L::mulsum2(a, L::sel(pb, b), L::sel(pa, L::ksub(k, zero, pa)), L::sel(b, pb));
+}
+
+// A B - Y D over Fq2 (a normalized A < kA, Y < kY; B, D normalized): four products per lane
+//   lane 0: A0 B0 + (kA - A1) B1 + (kY - Y0) D0 + Y1 D1
+//   lane 1: A1 B0 + A0 B1 + (kY - Y1) D0 + (kY - Y0) D1
+template <class L>
+ZK_HD typename L::V f2_mulsub(const typename L::V& A, const typename L::V& B, const uint32_t (&kA)[9],
+                              const typename L::V& Y, const typename L::V& D, const uint32_t (&kY)[9]) {
+  using V = typename L::V;
+  const V pA = L::swap(A), pB = L::swap(B), pY = L::swap(Y), pD = L::swap(D);
+  const V zero = L::zero();
+  const V x[4] = {A, L::sel(pA, L::ksub(kA, zero, pA)), L::ksub(kY, zero, Y), L::sel(L::ksub(kY, zero, pY), pY)};
+  const V y[4] = {L::sel(pB, B), L::sel(B, pB), L::sel(pD, D), L::sel(D, pD)};
+  return L::mulsum4(x, y);
+}
+
+template <class L>
+ZK_HD G2P29<L> f2_inf() {
+  return {L::one(), L::one(), L::zero(), L::zero()};
+}
+
+// dbl-2008-s-1.  U = 2Y < 12p (normalized); V = U^2 < p + (12 + 13) 12/169 p = 2.78p;
+// W = V U < 1.48p; S = V X < 1.24p; X^2 < 1.46p; M = 3 X^2 < 4.38p (normalized);
+// M^2 < 1.24p; X3 = M^2 + 3p - 2S < 4.24p; SX = S + 5p - X3 < 6.24p (normalized);
+// Y3 = M SX - Y W < p + ((4.38 + 5) 6.24 + (7 + 6) 1.48)/169 p < 1.47p; ZZ3, ZZZ3 < 1.07p.
+template <class L>
+ZK_HD G2P29<L> f2_dbl(const G2P29<L>& p) {
+  using V = typename L::V;
+  if (L::is_zero(p.ZZ)) return p;
+  V U = L::add(p.Y, p.Y);
+  L::norm(U);
+  const V Vv = f2_mul<L>(U, U, P29::K13_1);
+  const V W = f2_mul<L>(Vv, U, P29::K4_1);
+  const V S = f2_mul<L>(Vv, p.X, P29::K4_1);
+  const V X2 = f2_mul<L>(p.X, p.X, P29::K7_1);
+  V M = L::add(L::add(X2, X2), X2);
+  L::norm(M);
+  G2P29<L> r;
+  r.X = L::ksub3(P29::K3_2, f2_mul<L>(M, M, P29::K5_1), S, S, L::zero());
+  L::norm(r.X);
+  V SX = L::ksub(P29::K5_1, S, r.X);
+  L::norm(SX);
+  r.Y = f2_mulsub<L>(M, SX, P29::K5_1, p.Y, W, P29::K7_1);
+  r.ZZ = f2_mul<L>(Vv, p.ZZ, P29::K4_1);
+  r.ZZZ = f2_mul<L>(W, p.ZZZ, P29::K2_1);
+  return r;
+}
+
+// madd-2008-s.  x, y <= p (canonical base, y possibly negated); U2, S2 < 1.04p;
+// P = U2 + 7p - X1, R < 8.04p (normalized); PP, R^2 < p + (8.04 + 9) 8.04/169 p = 1.81p;
+// PPP = PP P < 1.18p; Q = PP X1 < 1.14p; X3 = R^2 + 4p - PPP - 2Q < 5.81p;
+// QX = Q + 6p - X3 < 7.14p (normalized); Y3 = R QX - Y1 PPP
+// < p + ((8.04 + 9) 7.14 + (7 + 6) 1.18)/169 p < 1.81p; ZZ3, ZZZ3 < 1.06p.
+template <class L>
+ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typename L::V& ay) {
+  using V = typename L::V;
+  if (L::is_zero(ax) && L::is_zero(ay)) return p;
+  if (L::is_zero(p.ZZ)) return {ax, ay, L::one(), L::one()};
+  const V U2 = f2_mul<L>(ax, p.ZZ, P29::K2_1);
+  const V S2 = f2_mul<L>(ay, p.ZZZ, P29::K2_1);
+  V P = L::ksub(P29::K7_1, U2, p.X);
+  V R = L::ksub(P29::K7_1, S2, p.Y);
+  L::norm(P);
+  L::norm(R);
+  const V PP = f2_mul<L>(P, P, P29::K9_1);
+  if (L::is_zero(PP)) {
+    if (L::is_zero(f2_mul<L>(R, R, P29::K9_1))) return f2_dbl<L>({ax, ay, L::one(), L::one()});
+    return f2_inf<L>();
+  }
+  const V PPP = f2_mul<L>(PP, P, P29::K2_1);
+  const V Q = f2_mul<L>(PP, p.X, P29::K2_1);
+  const V RR = f2_mul<L>(R, R, P29::K9_1);
+  G2P29<L> r;
+  r.X = L::ksub3(P29::K4_3, RR, PPP, Q, Q);
+  L::norm(r.X);
+  V QX = L::ksub(P29::K6_1, Q, r.X);
+  L::norm(QX);
+  r.Y = f2_mulsub<L>(R, QX, P29::K9_1, p.Y, PPP, P29::K7_1);
+  r.ZZ = f2_mul<L>(p.ZZ, PP, P29::K3_1);
+  r.ZZZ = f2_mul<L>(p.ZZZ, PPP, P29::K3_1);
+  return r;
+}
+
+// add-2008-s.  U1, U2, S1, S2 = (ZZ or ZZZ) (X or Y) < p + (2 + 3) 6/169 p = 1.18p;
+// P = U2 + 2p - U1, R < 3.18p (normalized); PP, R^2 < 1.14p; PPP < 1.07p; Q < 1.04p;
+// X3 = R^2 + 4p - PPP - 2Q < 5.14p; QX < 7.04p (normalized);
+// Y3 = R QX - S1 PPP < p + ((3.18 + 4) 7.04 + (2 + 1.18) 1.07)/169 p < 1.32p;
+// ZZ1 ZZ2 < 1.06p, ZZ3 = (ZZ1 ZZ2) PP < 1.04p (ZZZ likewise).
+template <class L>
+ZK_HD G2P29<L> f2_add(const G2P29<L>& p, const G2P29<L>& q) {
+  using V = typename L::V;
+  if (L::is_zero(q.ZZ)) return p;
+  if (L::is_zero(p.ZZ)) return q;
+  const V U1 = f2_mul<L>(q.ZZ, p.X, P29::K3_1);
+  const V U2 = f2_mul<L>(p.ZZ, q.X, P29::K3_1);
+  const V S1 = f2_mul<L>(q.ZZZ, p.Y, P29::K3_1);
+  const V S2 = f2_mul<L>(p.ZZZ, q.Y, P29::K3_1);
+  V P = L::ksub(P29::K2_1, U2, U1);
+  V R = L::ksub(P29::K2_1, S2, S1);
+  L::norm(P);
+  L::norm(R);
+  const V PP = f2_mul<L>(P, P, P29::K4_1);
+  if (L::is_zero(PP)) {
+    if (L::is_zero(f2_mul<L>(R, R, P29::K4_1))) return f2_dbl<L>(p);
+    return f2_inf<L>();
+  }
+  const V PPP = f2_mul<L>(PP, P, P29::K2_1);
+  const V Q = f2_mul<L>(PP, U1, P29::K2_1);
+  const V RR = f2_mul<L>(R, R, P29::K4_1);
+  G2P29<L> r;
+  r.X = L::ksub3(P29::K4_3, RR, PPP, Q, Q);
+  L::norm(r.X);
+  V QX = L::ksub(P29::K6_1, Q, r.X);
+  L::norm(QX);
+  r.Y = f2_mulsub<L>(R, QX, P29::K4_1, S1, PPP, P29::K2_1);
+  r.ZZ = f2_mul<L>(f2_mul<L>(p.ZZ, q.ZZ, P29::K3_1), PP, P29::K2_1);
+  r.ZZZ = f2_mul<L>(f2_mul<L>(p.ZZZ, q.ZZZ, P29::K3_1), PPP, P29::K2_1);
+  return r;
+}
+
+// Device lane policy for the G2 formulas: this lane's component, the partner's through DPP
+struct Pair29Dev {
+  using V = F29;
+  static ZK_DEV V zero() { return f29_zero(); }
+  static ZK_DEV V one() { return pair_half() ? f29_zero() : f29_const(P29::ONE); }
+  static ZK_DEV V swap(const V& a) {
+    V r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = pair_swap_u32(a.v[i]);
+    return r;
+  }
+  static ZK_DEV V sel(const V& v1, const V& v0) {
+    const bool h = pair_half() != 0;
+    V r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = h ? v1.v[i] : v0.v[i];
+    return r;
+  }
+  static ZK_DEV bool is_zero(const V& a) {
+    const uint32_t z = f29_is_zero(a) ? 1u : 0u;
+    return (z & pair_swap_u32(z)) != 0;
+  }
+  static ZK_DEV V add(const V& a, const V& b) { return f29_add_lazy(a, b); }
+  static ZK_DEV void norm(V& a) { f29_norm(a); }
+  static ZK_DEV V ksub(const uint32_t (&k)[9], const V& a, const V& b) { return f29_ksub(k, a, b); }
+  static ZK_DEV V ksub3(const uint32_t (&k)[9], const V& a, const V& b, const V& c, const V& d) {
+    return f29_ksub3(k, a, b, c, d);
+  }
+  static ZK_DEV V mulsum2(const V& a, const V& b, const V& c, const V& d) { return f29_mulsum2(a, b, c, d); }
+  static ZK_DEV V mulsum4(const V (&x)[4], const V (&y)[4]) { return f29_mulsum4(x, y); }
+};
+
+// Compute type of the G2 MSM kernels: Fq2 on lane pairs, 29-bit limbs (storage Affine/XYZZ<Fq2Ops>)
+struct Fq2Pair29 {
+  using T = F29;  // this lane's component
+  static ZK_DEV T zero() { return f29_zero(); }
+  static ZK_DEV T one() { return Pair29Dev::one(); }
+  static ZK_DEV bool is_zero(const T& a) { return Pair29Dev::is_zero(a); }
+  static ZK_DEV T canon(const T& a) { return FqOps29::canon(a); }
+};
+
 // the generic point templates (curve.h) for this representation
 template <>
 ZK_DEV Affine<FqOps29> aff_neg<FqOps29>(const Affine<FqOps29>& a) {
@@ -362,6 +590,26 @@ ZK_DEV XYZZ<FqOps29> xyzz_add<FqOps29>(const XYZZ<FqOps29>& p, const XYZZ<FqOps2
 template <>
 ZK_DEV XYZZ<FqOps29> xyzz_dbl<FqOps29>(const XYZZ<FqOps29>& p) {
   return f29_dbl(p);
+}
+
+template <>
+ZK_DEV Affine<Fq2Pair29> aff_neg<Fq2Pair29>(const Affine<Fq2Pair29>& a) {
+  return {a.x, FqOps29::neg(a.y)};  // both components: p - y
+}
+template <>
+ZK_DEV XYZZ<Fq2Pair29> xyzz_madd<Fq2Pair29>(const XYZZ<Fq2Pair29>& p, const Affine<Fq2Pair29>& a) {
+  const G2P29<Pair29Dev> r = f2_madd<Pair29Dev>({p.X, p.Y, p.ZZ, p.ZZZ}, a.x, a.y);
+  return {r.X, r.Y, r.ZZ, r.ZZZ};
+}
+template <>
+ZK_DEV XYZZ<Fq2Pair29> xyzz_add<Fq2Pair29>(const XYZZ<Fq2Pair29>& p, const XYZZ<Fq2Pair29>& q) {
+  const G2P29<Pair29Dev> r = f2_add<Pair29Dev>({p.X, p.Y, p.ZZ, p.ZZZ}, {q.X, q.Y, q.ZZ, q.ZZZ});
+  return {r.X, r.Y, r.ZZ, r.ZZZ};
+}
+template <>
+ZK_DEV XYZZ<Fq2Pair29> xyzz_dbl<Fq2Pair29>(const XYZZ<Fq2Pair29>& p) {
+  const G2P29<Pair29Dev> r = f2_dbl<Pair29Dev>({p.X, p.Y, p.ZZ, p.ZZZ});
+  return {r.X, r.Y, r.ZZ, r.ZZZ};
 }
 
 }  // namespace zkfl

@@ -45,8 +45,10 @@ namespace zkfl {
 #ifndef MSM_G1_WAVES
 #define MSM_G1_WAVES 3
 #endif
+// G2 in 29-bit limbs: 168 VGPRs + 14 spilled at 3 waves/SIMD, 180 without spills at 2 -- equal
+// throughput (399.5 vs 400.9 proofs/s, profiles/r02_s5_ab_limb29_g2.log); 2 keeps scratch out.
 #ifndef MSM_G2_WAVES
-#define MSM_G2_WAVES 3
+#define MSM_G2_WAVES 2
 #endif
 // 1: the next entry's base is loaded while the current one is added (one affine point of
 // registers); 0: loaded after it, latency hidden by the other waves only.  Without it G1 at 4
@@ -186,6 +188,38 @@ template <class F>
 struct MsmCompute {
   using type = F;
 };
+template <>
+struct MsmIO<Fq2Pair29> {
+  using S = Fq2Ops;
+  static constexpr int LANES = 2;
+  static ZK_DEV Affine<Fq2Pair29> ld_aff(const Affine<S>* p, size_t i) {
+    const Fq* q = reinterpret_cast<const Fq*>(p + i);
+    const uint32_t h = pair_half();
+    return {f29_pack(q[h].v), f29_pack(q[2 + h].v)};
+  }
+  static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
+    return reinterpret_cast<const uint4*>(p + i) + 2 * pair_half() + (q & 1) + (q >> 1) * 4;
+  }
+  static ZK_DEV Affine<Fq2Pair29> from_pieces(const uint4 (&u)[4]) {
+    Fq x, y;
+    memcpy(&x, &u[0], 32);
+    memcpy(&y, &u[2], 32);
+    return {f29_pack(x.v), f29_pack(y.v)};
+  }
+  static ZK_DEV XYZZ<Fq2Pair29> ld(const XYZZ<S>* p, size_t i) {
+    const Fq* q = reinterpret_cast<const Fq*>(p + i);
+    const uint32_t h = pair_half();
+    return {f29_pack(q[h].v), f29_pack(q[2 + h].v), f29_pack(q[4 + h].v), f29_pack(q[6 + h].v)};
+  }
+  static ZK_DEV void st(XYZZ<S>* p, size_t i, const XYZZ<Fq2Pair29>& v) {
+    Fq* q = reinterpret_cast<Fq*>(p + i);
+    const uint32_t h = pair_half();
+    f29_unpack(q[h].v, f29_below256(v.X));
+    f29_unpack(q[2 + h].v, f29_below256(v.Y));
+    f29_unpack(q[4 + h].v, v.ZZ);
+    f29_unpack(q[6 + h].v, v.ZZZ);
+  }
+};
 // MSM_G1_F29 (default): 29-bit limbs (field29.h); 0: 32-bit limbs in [0, 2p) (FqOpsLazy).
 #ifndef MSM_G1_F29
 #define MSM_G1_F29 1
@@ -201,19 +235,27 @@ struct MsmCompute<FqOps> {
 #endif
 };
 
-// Bases into the compute type's Montgomery domain (FqOps29: x 2^261 = fp_mul(x 2^256, 2^261 mod p)).
-static __global__ void __launch_bounds__(256) k_msm_to_m29(Affine<FqOps>* __restrict__ b, size_t n) {
+// Base coordinates (n Fq values) into the 29-bit compute types' Montgomery domain:
+// x 2^261 = fp_mul(x 2^256, 2^261 mod p)
+static __global__ void __launch_bounds__(256) k_msm_to_m29(Fq* __restrict__ a, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Fq c;
 #pragma unroll
   for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
-  b[i].x = fp_mul(b[i].x, c);
-  b[i].y = fp_mul(b[i].y, c);
+  a[i] = fp_mul(a[i], c);
 }
+// MSM_G2_F29 (default): lane pairs in 29-bit limbs (Fq2Pair29); 0: 32-bit limbs (Fq2PairOps).
+#ifndef MSM_G2_F29
+#define MSM_G2_F29 1
+#endif
 template <>
 struct MsmCompute<Fq2Ops> {
+#if MSM_G2_F29
+  using type = Fq2Pair29;
+#else
   using type = Fq2PairOps;
+#endif
 };
 
 // ---------------------------------------------------------------------------
@@ -605,9 +647,11 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
     ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
-  if constexpr (std::is_same<typename MsmCompute<F>::type, FqOps29>::value) {
-    if (b.n)
-      hipLaunchKernelGGL(k_msm_to_m29, dim3(zk_grid(b.n * MSM_W, 256)), dim3(256), 0, st, b.bases_w, b.n * MSM_W);
+  using FC = typename MsmCompute<F>::type;
+  if constexpr (std::is_same<FC, FqOps29>::value || std::is_same<FC, Fq2Pair29>::value) {
+    const size_t nfq = b.n * MSM_W * (sizeof(Affine<F>) / sizeof(Fq));
+    if (nfq)
+      hipLaunchKernelGGL(k_msm_to_m29, dim3(zk_grid(nfq, 256)), dim3(256), 0, st, reinterpret_cast<Fq*>(b.bases_w), nfq);
   }
   return hipGetLastError();
 }
