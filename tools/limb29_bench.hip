@@ -84,6 +84,47 @@ __device__ __forceinline__ F29 mul29(const F29& a, const F29& b) {
   return r;
 }
 
+// NACC independent column accumulators (products dealt round-robin), kept apart by empty asm
+// barriers so the compiler cannot re-associate them into one dependency chain
+template <int NACC>
+__device__ __forceinline__ F29 mul29_split(const F29& a, const F29& b) {
+  uint32_t m[9];
+  F29 r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t acc[NACC];
+#pragma unroll
+    for (int j = 0; j < NACC; j++) acc[j] = 0;
+    acc[0] = carry;
+    int t = 0;
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      acc[t % NACC] += (uint64_t)a.v[i] * b.v[k - i];
+      t++;
+      if (i < k) {  // m_i p_(k-i); m_k is not known yet
+        acc[t % NACC] += (uint64_t)m[i] * P29[k - i];
+        t++;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NACC; j++) asm volatile("" : "+v"(acc[j]));
+    uint64_t s = acc[0];
+#pragma unroll
+    for (int j = 1; j < NACC; j++) s += acc[j];
+    if (k < 9) {
+      m[k] = ((uint32_t)s * NINV29) & M29;
+      s += (uint64_t)m[k] * P29[0];
+    } else {
+      r.v[k - 9] = (uint32_t)s & M29;
+    }
+    carry = s >> 29;
+  }
+  r.v[8] = (uint32_t)carry;
+  return r;
+}
+
 template <int V, class T>
 __device__ __forceinline__ T vmul(const T& x, const T& y);
 template <>
@@ -92,6 +133,10 @@ template <>
 __device__ __forceinline__ F29 vmul<1, F29>(const F29& x, const F29& y) { return mul29<false>(x, y); }
 template <>
 __device__ __forceinline__ F29 vmul<2, F29>(const F29& x, const F29& y) { return mul29<true>(x, y); }
+template <>
+__device__ __forceinline__ F29 vmul<3, F29>(const F29& x, const F29& y) { return mul29_split<2>(x, y); }
+template <>
+__device__ __forceinline__ F29 vmul<4, F29>(const F29& x, const F29& y) { return mul29_split<3>(x, y); }
 
 template <int V, class T>
 __global__ void __launch_bounds__(256) kbench(T* data, int iters) {
@@ -143,14 +188,14 @@ __global__ void kcheck(const Fq* a, const Fq* b, const Fq* c, int n, int* bad) {
       for (int j = 0; j < 9; j++) x.v[j] = a29.v[j] + c29.v[j];
       want = fp_mul(fp_mul(fp_add(a[i], c[i]), b[i]), c251);
     }
-    for (int v = 1; v <= 2; v++) {
-      F29 r = v == 1 ? mul29<false>(x, b29) : mul29<true>(x, b29);
+    for (int v = 1; v <= 4; v++) {
+      F29 r = v == 1 ? mul29<false>(x, b29) : v == 2 ? mul29<true>(x, b29) : v == 3 ? mul29_split<2>(x, b29) : mul29_split<3>(x, b29);
       Fq u = unpack29(r);
       Fq red;
       fp_reduce_once<FqP>(red.v, u.v);
       bool lim = true;
       for (int j = 0; j < 9; j++) lim &= r.v[j] <= (j < 8 ? M29 : 0xFFFFFFu);
-      if (!fp_eq(red, want) || !lim) atomicAdd(bad + mode * 2 + (v - 1), 1);
+      if (!fp_eq(red, want) || !lim) atomicAdd(bad + mode * 4 + (v - 1), 1);
     }
   }
 }
@@ -167,13 +212,14 @@ int main() {
         st ^= st << 13; st ^= st >> 7; st ^= st << 17;
         h[i].v[j] = (uint32_t)st & (j == 7 ? 0x1fffffffu : 0xffffffffu);  // < 2^253 < p
       }
-    Fq* dd; int* bad; int hb[6] = {0, 0, 0, 0, 0, 0};
+    Fq* dd; int* bad; int hb[12] = {0};
     hipMalloc(&dd, 3 * m * sizeof(Fq)); hipMalloc(&bad, sizeof(hb));
     hipMemcpy(dd, h, 3 * m * sizeof(Fq), hipMemcpyHostToDevice); hipMemset(bad, 0, sizeof(hb));
     hipLaunchKernelGGL(kcheck, dim3(m / 256), dim3(256), 0, 0, dd, dd + m, dd + 2 * m, m, bad);
     hipMemcpy(hb, bad, sizeof(hb), hipMemcpyDeviceToHost);
-    printf("mismatches (a<p, a<2p, lazy limbs) x (1 acc, 2 acc): %d %d | %d %d | %d %d (of %d)\n", hb[0], hb[1], hb[2],
-           hb[3], hb[4], hb[5], m);
+    printf("mismatches (a<p, a<2p, lazy limbs) x (1 acc, ab|mp acc, split2, split3):");
+    for (int k = 0; k < 12; k++) printf(" %d", hb[k]);
+    printf(" (of %d)\n", m);
     free(h);
   }
   Fq* d32;
@@ -185,14 +231,17 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  const char* names[3] = {"8x32 whole-asm (FqOpsLazy::mul)", "9x29, one accumulator", "9x29, two accumulators"};
-  for (int v = 0; v < 3; v++) {
+  const char* names[5] = {"8x32 whole-asm (FqOpsLazy::mul)", "9x29, one accumulator", "9x29, ab | mp accumulators",
+                          "9x29, 2 split accumulators", "9x29, 3 split accumulators"};
+  for (int v = 0; v < 5; v++) {
     float ms = 0, lat = 0;
     for (int rep = 0; rep < 2; rep++) {
       hipEventRecord(a);
       if (v == 0) hipLaunchKernelGGL((kbench<0, Fq>), dim3(blocks), dim3(threads), 0, 0, d32, iters);
       if (v == 1) hipLaunchKernelGGL((kbench<1, F29>), dim3(blocks), dim3(threads), 0, 0, d29, iters);
       if (v == 2) hipLaunchKernelGGL((kbench<2, F29>), dim3(blocks), dim3(threads), 0, 0, d29, iters);
+      if (v == 3) hipLaunchKernelGGL((kbench<3, F29>), dim3(blocks), dim3(threads), 0, 0, d29, iters);
+      if (v == 4) hipLaunchKernelGGL((kbench<4, F29>), dim3(blocks), dim3(threads), 0, 0, d29, iters);
       hipEventRecord(b);
       hipEventSynchronize(b);
       hipEventElapsedTime(&ms, a, b);
@@ -201,6 +250,8 @@ int main() {
     if (v == 0) hipLaunchKernelGGL((klat<0, Fq>), dim3(1), dim3(1), 0, 0, d32, 10000);
     if (v == 1) hipLaunchKernelGGL((klat<1, F29>), dim3(1), dim3(1), 0, 0, d29, 10000);
     if (v == 2) hipLaunchKernelGGL((klat<2, F29>), dim3(1), dim3(1), 0, 0, d29, 10000);
+    if (v == 3) hipLaunchKernelGGL((klat<3, F29>), dim3(1), dim3(1), 0, 0, d29, 10000);
+    if (v == 4) hipLaunchKernelGGL((klat<4, F29>), dim3(1), dim3(1), 0, 0, d29, 10000);
     hipEventRecord(b);
     hipEventSynchronize(b);
     hipEventElapsedTime(&lat, a, b);

@@ -170,104 +170,67 @@ ZK_HD F29 f29_below256(const F29& a) {
   return r;
 }
 
-// Montgomery product a b 2^-261 (product scanning, one 64-bit column accumulator)
-ZK_HD F29 f29_mul(const F29& a, const F29& b) {
+// Product-scanning Montgomery engine over NP operand pairs: (sum_j x_j y_j) 2^-261, one
+// reduction.  Each column's products are dealt to two 64-bit accumulators in turn, kept apart by
+// an empty asm barrier so the compiler cannot re-associate them into one chain: a lone column
+// chain of dependent v_mad_u64_u32 made one product ~3,700 cycles of latency, two chains ~1,400
+// (tools/limb29_bench.hip: 1537 -> 578 ns single-lane; 172 -> 166 G/s at full occupancy).
+#ifndef F29_SPLIT
+#define F29_SPLIT 1
+#endif
+ZK_HD void f29_keep(uint64_t& a) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(a));
+#else
+  (void)a;
+#endif
+}
+
+template <int NP>
+ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
   uint32_t m[9];
   F29 r;
-  uint64_t acc = 0;
+  uint64_t carry = 0;
 #pragma unroll
-  for (int k = 0; k < 9; k++) {
+  for (int k = 0; k < 17; k++) {
+    uint64_t acc[2] = {carry, 0};
+    int t = 0;
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
 #pragma unroll
-    for (int i = 0; i < k; i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
+    for (int i = lo; i <= hi; i++) {
+#pragma unroll
+      for (int j = 0; j < NP; j++) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)x[j].v[i] * y[j].v[k - i];
+      if (i < k) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)m[i] * P29::P[k - i];  // m_k is not known yet
     }
-    acc += (uint64_t)a.v[k] * b.v[0];
-    m[k] = ((uint32_t)acc * P29::NINV) & P29::MASK;
-    acc += (uint64_t)m[k] * P29::P[0];
-    acc >>= 29;
-  }
-#pragma unroll
-  for (int k = 9; k < 17; k++) {
-#pragma unroll
-    for (int i = k - 8; i < 9; i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
+    f29_keep(acc[0]);
+    f29_keep(acc[1]);
+    uint64_t c = acc[0] + acc[1];
+    if (k < 9) {
+      m[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
+      c += (uint64_t)m[k] * P29::P[0];
+    } else {
+      r.v[k - 9] = (uint32_t)c & P29::MASK;
     }
-    r.v[k - 9] = (uint32_t)acc & P29::MASK;
-    acc >>= 29;
+    carry = c >> 29;
   }
-  r.v[8] = (uint32_t)acc;
+  r.v[8] = (uint32_t)carry;
   return r;
 }
 
-// (sum_{j<4} x_j y_j) 2^-261 with one reduction (the G2 y-coordinate product pair)
-ZK_HD F29 f29_mulsum4(const F29 (&x)[4], const F29 (&y)[4]) {
-  uint32_t m[9];
-  F29 r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-#pragma unroll
-    for (int i = 0; i < k; i++) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[i] * y[j].v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[k] * y[j].v[0];
-    m[k] = ((uint32_t)acc * P29::NINV) & P29::MASK;
-    acc += (uint64_t)m[k] * P29::P[0];
-    acc >>= 29;
-  }
-#pragma unroll
-  for (int k = 9; k < 17; k++) {
-#pragma unroll
-    for (int i = k - 8; i < 9; i++) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc += (uint64_t)x[j].v[i] * y[j].v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
-    }
-    r.v[k - 9] = (uint32_t)acc & P29::MASK;
-    acc >>= 29;
-  }
-  r.v[8] = (uint32_t)acc;
-  return r;
+// Montgomery product a b 2^-261
+ZK_HD F29 f29_mul(const F29& a, const F29& b) {
+  const F29 x[1] = {a}, y[1] = {b};
+  return f29_mont<1>(x, y);
 }
 
 // (a b + c d) 2^-261 with one reduction
 ZK_HD F29 f29_mulsum2(const F29& a, const F29& b, const F29& c, const F29& d) {
-  uint32_t m[9];
-  F29 r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-#pragma unroll
-    for (int i = 0; i < k; i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acc += (uint64_t)c.v[i] * d.v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
-    }
-    acc += (uint64_t)a.v[k] * b.v[0];
-    acc += (uint64_t)c.v[k] * d.v[0];
-    m[k] = ((uint32_t)acc * P29::NINV) & P29::MASK;
-    acc += (uint64_t)m[k] * P29::P[0];
-    acc >>= 29;
-  }
-#pragma unroll
-  for (int k = 9; k < 17; k++) {
-#pragma unroll
-    for (int i = k - 8; i < 9; i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acc += (uint64_t)c.v[i] * d.v[k - i];
-      acc += (uint64_t)m[i] * P29::P[k - i];
-    }
-    r.v[k - 9] = (uint32_t)acc & P29::MASK;
-    acc >>= 29;
-  }
-  r.v[8] = (uint32_t)acc;
-  return r;
+  const F29 x[2] = {a, c}, y[2] = {b, d};
+  return f29_mont<2>(x, y);
 }
+
+// (sum_{j<4} x_j y_j) 2^-261 with one reduction (the G2 y-coordinate product pair)
+ZK_HD F29 f29_mulsum4(const F29 (&x)[4], const F29 (&y)[4]) { return f29_mont<4>(x, y); }
 
 // Compute type of the G1 MSM kernels over this representation (storage: Affine/XYZZ<FqOps>).
 struct FqOps29 {
