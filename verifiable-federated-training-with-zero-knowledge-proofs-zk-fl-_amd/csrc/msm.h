@@ -745,14 +745,16 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
   if (need > pl.sort_tmp_bytes || chunks > t.max_chunks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
                      b.extra_start, b.n, pl.keys_in, pl.vals_in, t.nnz);
-  ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
-                                     st));
+  if (!(ZK_KNOCKOUT & 2))
+    ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
+                                       st));
   const int pidx = prof ? prof->begin(tag, st) : -1;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
-  hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, pl.keys_out,
-                     pl.vals_out, b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
+  if (!((ZK_KNOCKOUT & 64) && LN == 1))
+    hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, pl.keys_out,
+                       pl.vals_out, b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
   return hipGetLastError();
 }
@@ -772,13 +774,14 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   for (int i = 0; i < n; i++) N = std::max(N, t[i]->item_cap[0]);
   N = std::max<size_t>(N, 2);
   int cur = 0;
-  for (int level = 1;; level++) {
+  for (int level = 1; !(ZK_KNOCKOUT & 8); level++) {
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
     hipLaunchKernelGGL((k_msm_stitch<FC, SW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
     if (N <= (size_t)MSM_SG) break;
     N = 2 * lanes;
     cur ^= 1;
   }
+  if (ZK_KNOCKOUT & 16) return hipGetLastError();
   hipLaunchKernelGGL((k_msm_wsum<FC, TW, true>), dim3(MSM_NB / (MSM_RB * msm_wsum_q0<F>()), n), dim3(MSM_RB * LN), 0,
                      st, ta);
   hipLaunchKernelGGL((k_msm_wsum<FC, TW, false>), dim3(1, n), dim3(MSM_RB * LN), 0, st, ta);

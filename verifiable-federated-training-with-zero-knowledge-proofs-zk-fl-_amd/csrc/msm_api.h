@@ -11,6 +11,12 @@ namespace zkfl {
 constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
+// Knock-out builds for marginal-cost measurements (tools/ko_probe.py; proofs are WRONG, timing
+// only): 1 assembly, 2 radix sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
+// 64 the G1 accumulation kernel.  0 in every real build.
+#ifndef ZK_KNOCKOUT
+#define ZK_KNOCKOUT 0
+#endif
 #ifndef MSM_G1_L
 #define MSM_G1_L 16
 #endif

@@ -118,6 +118,49 @@ __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, i
     for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
 }
 
+// The inverse transform's LDS pass, the coset scale and the forward transform's LDS pass on
+// the same tile in one kernel (the tiles coincide: both passes take T consecutive elements), so
+// the tile makes one HBM round trip instead of two.  Bit-identical to k_ntt_lds<true> with
+// `scale` followed by k_ntt_lds<false>.
+__global__ void __launch_bounds__(512) k_ntt_lds_pair(Fr* __restrict__ a, size_t n, int logt,
+                                                      const Fr* __restrict__ tw_inv, const Fr* __restrict__ tw_fwd,
+                                                      int nvec, size_t vstride, const Fr* __restrict__ scale) {
+  __shared__ Fr tile[NTT_LDS_N];
+  const size_t T = (size_t)1 << logt;
+  const size_t tiles_per_vec = n >> logt;
+  const size_t tile_id = blockIdx.x;
+  const size_t v = tile_id / tiles_per_vec;
+  if (v >= (size_t)nvec) return;
+  const size_t base = (tile_id - v * tiles_per_vec) * T;
+  Fr* x = a + v * vstride + base;
+  for (size_t i = threadIdx.x; i < T; i += blockDim.x) tile[i] = x[i];
+  __syncthreads();
+  const size_t nbf = T >> 1;
+  for (int s = 0; s < logt; s++) {  // DIF, spans T/2 .. 1
+    const size_t half = T >> (s + 1), twstride = n / (half << 1);
+    for (size_t t = threadIdx.x; t < nbf; t += blockDim.x) {
+      const size_t j = t & (half - 1), i0 = ((t - j) << 1) + j, i1 = i0 + half;
+      const Fr u = tile[i0], w = tile[i1];
+      tile[i0] = fp_add(u, w);
+      tile[i1] = fp_mul(fp_sub(u, w), tw_inv[j * twstride]);
+    }
+    __syncthreads();
+  }
+  for (size_t i = threadIdx.x; i < T; i += blockDim.x) tile[i] = fp_mul(tile[i], scale[base + i]);
+  __syncthreads();
+  for (int s = 0; s < logt; s++) {  // DIT, spans 1 .. T/2
+    const size_t half = (size_t)1 << s, twstride = n / (half << 1);
+    for (size_t t = threadIdx.x; t < nbf; t += blockDim.x) {
+      const size_t j = t & (half - 1), i0 = ((t - j) << 1) + j, i1 = i0 + half;
+      const Fr u = tile[i0], w = fp_mul(tile[i1], tw_fwd[j * twstride]);
+      tile[i0] = fp_add(u, w);
+      tile[i1] = fp_sub(u, w);
+    }
+    __syncthreads();
+  }
+  for (size_t i = threadIdx.x; i < T; i += blockDim.x) x[i] = tile[i];
+}
+
 // Same stages, two at a time: each thread takes the 4 elements of a radix-4 butterfly
 // (i0, i0 + q, i0 + 2q, i0 + 3q) through two radix-2 stages in registers, so a tile needs half the
 // LDS round trips and barriers and each thread has two independent products in flight per stage.
@@ -361,9 +404,23 @@ static hipError_t ntt_dit(const NttPlan& pl, Fr* d, const Fr* tw, int nvec, size
 
 // In place: nvec vectors (stride vstride) of evaluations on the domain -> evaluations on
 // the odd coset (snarkjs ifft + batchApplyKey + fft).
+#ifndef NTT_LDS_PAIR
+#define NTT_LDS_PAIR 1
+#endif
 hipError_t ntt_coset_shift(const NttPlan& pl, Fr* d, int nvec, size_t vstride, hipStream_t st) {
-  ZK_CHECK(ntt_dif(pl, d, pl.tw_inv, nvec, vstride, pl.coset, st));
-  return ntt_dit(pl, d, pl.tw_fwd, nvec, vstride, st);
+  const int logt = pl.logn < NTT_LDS_LOG ? pl.logn : NTT_LDS_LOG;
+  const int top = pl.logn - logt;
+  if (!NTT_LDS_PAIR || NTT_RADIX4 || logt == 0 || top == 0 || top > NTT_COL_TILE_LOG) {
+    ZK_CHECK(ntt_dif(pl, d, pl.tw_inv, nvec, vstride, pl.coset, st));
+    return ntt_dit(pl, d, pl.tw_fwd, nvec, vstride, st);
+  }
+  // column pass (inverse, top stages) -> fused LDS pair -> column pass (forward, top stages)
+  const unsigned groups = (unsigned)((((size_t)1 << (pl.logn - top)) / ((size_t)NTT_COL_TILE >> top)) * nvec);
+  hipLaunchKernelGGL(k_ntt_cols<true>, dim3(groups), dim3(256), 0, st, d, pl.logn, top, pl.tw_inv, nvec, vstride);
+  hipLaunchKernelGGL(k_ntt_lds_pair, dim3((unsigned)((pl.n >> logt) * nvec)), dim3(512), 0, st, d, pl.n, logt,
+                     pl.tw_inv, pl.tw_fwd, nvec, vstride, pl.coset);
+  hipLaunchKernelGGL(k_ntt_cols<false>, dim3(groups), dim3(256), 0, st, d, pl.logn, top, pl.tw_fwd, nvec, vstride);
+  return hipGetLastError();
 }
 
 // Plain transforms (natural order in and out) for parity tests: inverse includes 1/n.

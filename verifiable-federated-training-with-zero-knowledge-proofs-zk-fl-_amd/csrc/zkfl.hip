@@ -711,7 +711,8 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   // G2 stream
   HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
-  HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
+  if (!(ZK_KNOCKOUT & 32))
+    HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
   HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
@@ -734,7 +735,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
                      s->abc_tail, s->abc);
   prof->end(pi, st, (double)k->K);
   pi = prof->begin("ntt", st);
-  HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
+  if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
   prof->end(pi, st, 3.0 * (double)n);
   hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
   HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
@@ -744,7 +745,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(msm_tails_g1(tails, outs, 4, st), "msm tails");
   }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
-  if (!plain) {
+  if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
     hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
                        reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
