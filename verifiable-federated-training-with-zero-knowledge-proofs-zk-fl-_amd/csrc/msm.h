@@ -728,35 +728,54 @@ hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
   return hipGetLastError();
 }
 
-// digits (+ nnz) -> radix sort by bucket -> accumulate (level 0: fixed chunks, closed runs
-// straight into the buckets, open runs as items).  The tail must have been reset
+// digits (+ nnz) -> radix sort by bucket into pl.keys_out / pl.vals_out.  *nnz must be zero.
+template <class F>
+hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
+                    const uint32_t* d_extra, hipStream_t st) {
+  if (b.n > pl.cap) return hipErrorInvalidValue;
+  if (b.n == 0) return hipSuccess;
+  const size_t m = b.n * MSM_W;
+  size_t need = 0;
+  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
+  if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
+                     b.extra_start, b.n, pl.keys_in, pl.vals_in, nnz);
+  if (!(ZK_KNOCKOUT & 2))
+    ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
+                                       st));
+  return hipGetLastError();
+}
+
+// Accumulation (level 0: fixed chunks, closed runs straight into the buckets, open runs as items)
+// over sorted (bucket, entry) pairs and t.nnz.  The pairs may come from another MSM with the same
+// scalars and base index map (B1's sort serves B2: msm_sort once, accumulate on both curves).
+template <class F>
+hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, MsmTail<F>& t,
+                                 hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
+  if (b.n == 0) return hipSuccess;
+  const size_t m = b.n * MSM_W;
+  const size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  if (chunks > t.max_chunks) return hipErrorInvalidValue;
+  const int pidx = prof ? prof->begin(tag, st) : -1;
+  using FC = typename MsmCompute<F>::type;
+  constexpr int LN = MsmIO<FC>::LANES;
+  constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
+  if (!((ZK_KNOCKOUT & 64) && LN == 1))
+    hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, keys, vals,
+                       b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
+  if (prof) prof->end(pidx, st, 0.0, t.nnz);
+  return hipGetLastError();
+}
+
+// digits (+ nnz) -> radix sort by bucket -> accumulate.  The tail must have been reset
 // (msm_tails_reset).  An MSM with no bases leaves nnz = 0 and empty buckets: its tail yields
 // infinity.
 template <class F>
 hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
                           const uint32_t* d_extra, hipStream_t st, Profiler* prof = nullptr,
                           const char* tag = nullptr) {
-  if (b.n > pl.cap) return hipErrorInvalidValue;
-  if (b.n == 0) return hipSuccess;
-  const size_t m = b.n * MSM_W;
-  const size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
-  size_t need = 0;
-  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
-  if (need > pl.sort_tmp_bytes || chunks > t.max_chunks) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
-                     b.extra_start, b.n, pl.keys_in, pl.vals_in, t.nnz);
-  if (!(ZK_KNOCKOUT & 2))
-    ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
-                                       st));
-  const int pidx = prof ? prof->begin(tag, st) : -1;
-  using FC = typename MsmCompute<F>::type;
-  constexpr int LN = MsmIO<FC>::LANES;
-  constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
-  if (!((ZK_KNOCKOUT & 64) && LN == 1))
-    hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, pl.keys_out,
-                       pl.vals_out, b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
-  if (prof) prof->end(pidx, st, 0.0, t.nnz);
-  return hipGetLastError();
+  ZK_CHECK(msm_sort(b, pl, t.nnz, d_scalars, d_extra, st));
+  return msm_accumulate_sorted(b, pl.keys_out, pl.vals_out, t, st, prof, tag);
 }
 
 // Tails of n accumulated MSMs in one batch: stitching levels until one lane holds every
@@ -815,6 +834,14 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
   hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc, \
                                   const uint32_t* ex, hipStream_t st, Profiler* prof, const char* tag) { \
     return msm_accumulate(b, s, t, sc, ex, st, prof, tag);                                               \
+  }                                                                                                      \
+  hipError_t msm_sort_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc,      \
+                            const uint32_t* ex, hipStream_t st) {                                        \
+    return msm_sort(b, s, nnz, sc, ex, st);                                                              \
+  }                                                                                                      \
+  hipError_t msm_accumulate_sorted_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals,  \
+                                         MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag) { \
+    return msm_accumulate_sorted(b, keys, vals, t, st, prof, tag);                                       \
   }                                                                                                      \
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {         \
     return msm_tails(t, outs, n, st);                                                                    \

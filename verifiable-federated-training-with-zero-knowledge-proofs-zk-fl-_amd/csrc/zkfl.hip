@@ -482,6 +482,9 @@ struct ProofSlot {
   uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
 };
 
+#ifndef ZK_NO_SHARE_B
+#define ZK_NO_SHARE_B 0  // 1: B2 sorts its own digits (A/B builds)
+#endif
 struct zkfl_key {
   zkfl_ctx* ctx = nullptr;
   uint32_t nVars = 0, nPub = 0, n = 0;
@@ -494,6 +497,7 @@ struct zkfl_key {
   uint32_t cshift = 0;       // packed terms: col | dict index << cshift in cols[]; 0 = wide
   MsmBases<FqOps> bA, bB1, bC, bH;
   MsmBases<Fq2Ops> bB2;
+  bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
   int max_slots = 3;
@@ -709,16 +713,34 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
-  // G2 stream
-  HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
-  if (!(ZK_KNOCKOUT & 32))
-    HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
-  HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
-  // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
+  // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
+  // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
+  const bool share = k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32);
+  if (!share) {  // G2 stream
+    HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
+    if (!(ZK_KNOCKOUT & 32))
+      HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
+    HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
+  }
+  // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   HIP_TRY(msm_tails_reset_g1(tails, 4, st), "msm reset");
   HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
-  HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
+  if (share) {
+    MsmTail<Fq2Ops>* t2 = &s->g2t;
+    G2P* o2 = s->resB2;
+    HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
+    HIP_TRY(msm_sort_g1(k->bB1, s->g1s, s->g1t[1].nnz, W, E, st), "msm B1 sort");
+    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s.keys_out, s->g1s.vals_out, s->g1t[1], st, prof,
+                                     "msm_accumulate_g1"), "msm B1");
+    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s.keys_out, s->g1s.vals_out, s->g2t, st, prof,
+                                     "msm_accumulate_g2"), "msm B2");
+    HIP_TRY(msm_tails_g2(&t2, &o2, 1, st), "msm B2 tail");
+    HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
+  } else {
+    HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
+  }
   HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
   int pi = prof->begin("abc", st);
   if (k->K) {
@@ -1150,8 +1172,10 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       uint32_t sidx;
     };
     // Build the compacted (host) base image + index map, upload, expand.
+    std::vector<uint32_t> sidx_b1, sidx_b2;
     auto build = [&](auto& mb, size_t psz, const uint8_t* sec, size_t cnt, uint32_t scalar_off,
-                     std::initializer_list<Aug> aug, bool identity) -> hipError_t {
+                     std::initializer_list<Aug> aug, bool identity,
+                     std::vector<uint32_t>* keep = nullptr) -> hipError_t {
       std::vector<uint8_t> img;
       std::vector<uint32_t> sidx;
       img.reserve((cnt + aug.size()) * psz);
@@ -1166,6 +1190,7 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
         img.insert(img.end(), a.pt, a.pt + psz);
         sidx.push_back(a.sidx);
       }
+      if (keep) *keep = sidx;
       hipError_t e = bases_alloc_any(mb, sidx.size());
       if (e != hipSuccess || sidx.empty()) return e;
       void* d_img = nullptr;
@@ -1178,8 +1203,13 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       return e;
     };
     hipError_t e = build(k->bA, 64, z.secA, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
-    if (e == hipSuccess) e = build(k->bB1, 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false);
-    if (e == hipSuccess) e = build(k->bB2, 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false);
+    if (e == hipSuccess)
+      e = build(k->bB1, 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false, &sidx_b1);
+    if (e == hipSuccess)
+      e = build(k->bB2, 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false, &sidx_b2);
+    // B_i(tau) G1 and B_i(tau) G2 vanish together in an honest zkey; the sort is shared only when
+    // the two index maps really are equal
+    k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
     if (e == hipSuccess) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
     if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, true);
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
