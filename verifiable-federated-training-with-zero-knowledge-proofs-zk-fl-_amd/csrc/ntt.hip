@@ -4,7 +4,10 @@
 
 namespace zkfl {
 
-constexpr int NTT_LDS_LOG = 10;
+#ifndef NTT_LDS_LOG_BITS
+#define NTT_LDS_LOG_BITS 10
+#endif
+constexpr int NTT_LDS_LOG = NTT_LDS_LOG_BITS;
 constexpr int NTT_LDS_N = 1 << NTT_LDS_LOG;
 
 // tw[i] = root^i (Montgomery) for i < n/2
