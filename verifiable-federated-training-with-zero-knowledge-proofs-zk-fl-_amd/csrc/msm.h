@@ -342,6 +342,163 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(nnz, cnt);
 }
 
+// ---------------------------------------------------------------------------
+// Bucket sort of the digits (the default; MSM_SORT_ROCPRIM=1 keeps the rocPRIM radix sort).
+// Keys are 15-bit bucket numbers, so two counting passes put every non-zero digit in bucket
+// order with no look-back and no memsets:
+//   count   per block of bases: digits -> LDS histogram of the high 7 key bits -> cnt[bin][block]
+//   scan    one workgroup: cnt (bin-major) -> exclusive offsets, bin starts, nnz
+//   scatter per block: digits again (the scalars are 2 B per entry, the pairs 6) -> each pair
+//           to its high bin at an LDS-atomic cursor
+//   bins    one workgroup per high bin: LDS histogram of the low 8 bits, then each pair to its
+//           bucket at an LDS-atomic cursor
+// Zero digits are dropped (the accumulation reads only the first nnz pairs).  The order inside
+// a bucket is arbitrary: a bucket's sum does not depend on it, and the proof is affine.
+// ---------------------------------------------------------------------------
+constexpr int MSM_SORT_T = 256;           // threads per block in count / scatter
+constexpr int MSM_SORT_HB = MSM_NB >> 8;  // high bins (7 bits)
+constexpr int MSM_SORT_MAXBLK = 256;      // count/scatter blocks (the scan holds cnt in LDS)
+constexpr int MSM_SORT_BT = 1024;         // threads per high-bin workgroup
+static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
+
+// Signed digits of base i's scalar: fn(key, val) for every non-zero digit (as k_msm_digits).
+template <class Fn>
+ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra,
+                           const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t i, Fn&& fn) {
+  const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
+  const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
+  const uint4* sp = reinterpret_cast<const uint4*>(src);
+  const uint4 a = sp[0], b = sp[1];
+  const uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < MSM_W; j++) {
+    const uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+    int32_t d = (int32_t)(raw + carry);
+    carry = d > MSM_NB ? 1u : 0u;
+    if (carry) d -= (1 << MSM_C);
+    if (d != 0) {
+      const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      fn(mag - 1, (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u));
+    }
+  }
+}
+
+static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint32_t* __restrict__ scalars,
+                                                                   const uint32_t* __restrict__ extra,
+                                                                   const uint32_t* __restrict__ sidx,
+                                                                   uint32_t extra_start, size_t n, size_t per_blk,
+                                                                   uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[MSM_SORT_HB];
+  if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
+    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> 8], 1u); });
+  __syncthreads();
+  if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// cnt[HB * nblk] (bin-major) -> exclusive offsets in place; bin_start[HB + 1]; *nnz.
+static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* __restrict__ cnt, uint32_t nblk,
+                                                                   uint32_t* __restrict__ bin_start,
+                                                                   uint32_t* __restrict__ nnz) {
+  __shared__ uint32_t c[MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_BT];  // +1 word per 32: no bank conflicts
+  __shared__ uint32_t part[MSM_SORT_BT];
+  const uint32_t total = MSM_SORT_HB * nblk, t = threadIdx.x;
+  for (uint32_t k = t; k < total; k += MSM_SORT_BT) c[k + (k >> 5)] = cnt[k];
+  __syncthreads();
+  uint32_t s = 0;
+  for (uint32_t q = 0; q < 32; q++) {
+    const uint32_t k = t * 32 + q;
+    if (k < total) s += c[k + (k >> 5)];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < MSM_SORT_BT; off <<= 1) {
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (uint32_t q = 0; q < 32; q++) {
+    const uint32_t k = t * 32 + q;
+    if (k < total) {
+      const uint32_t v = c[k + (k >> 5)];
+      c[k + (k >> 5)] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = t; k < total; k += MSM_SORT_BT) {
+    const uint32_t v = c[k + (k >> 5)];
+    cnt[k] = v;
+    if (k % nblk == 0) bin_start[k / nblk] = v;
+  }
+  if (t == MSM_SORT_BT - 1) {
+    bin_start[MSM_SORT_HB] = part[t];
+    *nnz = part[t];
+  }
+}
+
+static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
+    const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra, const uint32_t* __restrict__ sidx,
+    uint32_t extra_start, size_t n, size_t per_blk, const uint32_t* __restrict__ cnt, uint16_t* __restrict__ keys,
+    uint32_t* __restrict__ vals) {
+  __shared__ uint32_t cur[MSM_SORT_HB];
+  if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
+    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t val) {
+      const uint32_t p = atomicAdd(&cur[key >> 8], 1u);
+      keys[p] = (uint16_t)key;
+      vals[p] = val;
+    });
+}
+
+// One workgroup per high bin: [bin_start[b], bin_start[b+1]) of (tk, tv) -> buckets in (ko, vo).
+static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
+                                                                   const uint16_t* __restrict__ tk,
+                                                                   const uint32_t* __restrict__ tv,
+                                                                   uint16_t* __restrict__ ko,
+                                                                   uint32_t* __restrict__ vo) {
+  __shared__ uint32_t c[256];
+  const uint32_t b0 = bin_start[blockIdx.x], b1 = bin_start[blockIdx.x + 1], t = threadIdx.x;
+  if (b0 == b1) return;
+  if (t < 256) c[t] = 0;
+  __syncthreads();
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) atomicAdd(&c[tk[p] & 255u], 1u);
+  __syncthreads();
+  // exclusive scan of the 256 counters by the first 4 waves (wave scan + wave totals)
+  uint32_t v = 0, x = 0;
+  if (t < 256) {
+    v = c[t];
+    x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if ((t & 63) >= (uint32_t)o) x += y;
+    }
+  }
+  __shared__ uint32_t wt[4];
+  if (t < 256 && (t & 63) == 63) wt[t >> 6] = x;
+  __syncthreads();
+  if (t < 256) {
+    uint32_t base = b0;
+    for (uint32_t w = 0; w < (t >> 6); w++) base += wt[w];
+    c[t] = base + x - v;
+  }
+  __syncthreads();
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
+    const uint16_t key = tk[p];
+    const uint32_t q = atomicAdd(&c[key & 255u], 1u);
+    ko[q] = key;
+    vo[q] = tv[p];
+  }
+}
+
 // Where a bucket run found by one lane goes (shared by the accumulation and stitching levels).
 // A run [a, b] of bucket k inside a lane's range [q0, q1) is open on the left if it starts the
 // range and the previous range ends in the same bucket, open on the right likewise.  A closed
@@ -664,8 +821,12 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
   ZK_CHECK(hipMalloc(&s.keys_out, m * sizeof(uint16_t)));
   ZK_CHECK(hipMalloc(&s.vals_in, m * sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&s.vals_out, m * sizeof(uint32_t)));
+#if MSM_SORT_ROCPRIM
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, s.sort_tmp_bytes, s.keys_in, s.keys_out, s.vals_in, s.vals_out, m, 0,
                                      16, st));
+#else
+  s.sort_tmp_bytes = (MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_HB + 1) * sizeof(uint32_t);
+#endif
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
   return hipSuccess;
 }
@@ -728,12 +889,33 @@ hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
   return hipGetLastError();
 }
 
-// digits (+ nnz) -> radix sort by bucket into pl.keys_out / pl.vals_out.  *nnz must be zero.
+// digits (+ nnz) -> sort by bucket into pl.keys_out / pl.vals_out (the first *nnz pairs).  With the
+// rocPRIM sort *nnz must be zero on entry; the bucket sort writes it.
 template <class F>
 hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
                     const uint32_t* d_extra, hipStream_t st) {
   if (b.n > pl.cap) return hipErrorInvalidValue;
   if (b.n == 0) return hipSuccess;
+#if !MSM_SORT_ROCPRIM
+  // count / scan / scatter / bins (see k_msm_bin_count); keys_in/vals_in hold the high-bin order
+  const size_t per_blk = (b.n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
+                             ? (size_t)MSM_SORT_T
+                             : ((b.n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
+  const uint32_t nblk = (uint32_t)((b.n + per_blk - 1) / per_blk);
+  if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
+  uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
+  uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
+  hipLaunchKernelGGL(k_msm_bin_count, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx, b.extra_start,
+                     b.n, per_blk, cnt);
+  hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
+  if (!(ZK_KNOCKOUT & 2)) {
+    hipLaunchKernelGGL(k_msm_bin_scatter, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
+                       b.extra_start, b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
+    hipLaunchKernelGGL(k_msm_bin_sort, dim3(MSM_SORT_HB), dim3(MSM_SORT_BT), 0, st, bin_start, pl.keys_in, pl.vals_in,
+                       pl.keys_out, pl.vals_out);
+  }
+  return hipGetLastError();
+#else
   const size_t m = b.n * MSM_W;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
@@ -744,6 +926,7 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
     ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
                                        st));
   return hipGetLastError();
+#endif
 }
 
 // Accumulation (level 0: fixed chunks, closed runs straight into the buckets, open runs as items)

@@ -17,6 +17,10 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef ZK_KNOCKOUT
 #define ZK_KNOCKOUT 0
 #endif
+// 1: digits sorted by rocPRIM's radix sort (A/B builds); 0: the two-pass bucket sort in msm.h
+#ifndef MSM_SORT_ROCPRIM
+#define MSM_SORT_ROCPRIM 0
+#endif
 #ifndef MSM_G1_L
 #define MSM_G1_L 16
 #endif
