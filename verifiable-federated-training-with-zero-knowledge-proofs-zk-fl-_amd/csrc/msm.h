@@ -346,18 +346,21 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
 // Bucket sort of the digits (the default; MSM_SORT_ROCPRIM=1 keeps the rocPRIM radix sort).
 // Keys are 15-bit bucket numbers, so two counting passes put every non-zero digit in bucket
 // order with no look-back and no memsets:
-//   count   per block of bases: digits -> LDS histogram of the high 7 key bits -> cnt[bin][block]
+//   count   per block of bases: digits -> LDS histogram of the high key bits -> cnt[bin][block]
 //   scan    one workgroup: cnt (bin-major) -> exclusive offsets, bin starts, nnz
 //   scatter per block: digits again (the scalars are 2 B per entry, the pairs 6) -> each pair
 //           to its high bin at an LDS-atomic cursor
-//   bins    one workgroup per high bin: LDS histogram of the low 8 bits, then each pair to its
+//   bins    one workgroup per high bin: LDS histogram of the low bits, then each pair to its
 //           bucket at an LDS-atomic cursor
 // Zero digits are dropped (the accumulation reads only the first nnz pairs).  The order inside
 // a bucket is arbitrary: a bucket's sum does not depend on it, and the proof is affine.
 // ---------------------------------------------------------------------------
 constexpr int MSM_SORT_T = 256;           // threads per block in count / scatter
-constexpr int MSM_SORT_HB = MSM_NB >> 8;  // high bins (7 bits)
-constexpr int MSM_SORT_MAXBLK = 256;      // count/scatter blocks (the scan holds cnt in LDS)
+constexpr int MSM_SORT_LB = MSM_SORT_LOW_BITS;       // key bits sorted inside a high bin
+constexpr int MSM_SORT_NL = 1 << MSM_SORT_LB;        // low counters per high-bin workgroup
+constexpr int MSM_SORT_HB = MSM_NB >> MSM_SORT_LB;   // high bins
+constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
+static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 256 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
 constexpr int MSM_SORT_BT = 1024;         // threads per high-bin workgroup
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
@@ -394,7 +397,7 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint3
   __syncthreads();
   const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> 8], 1u); });
+    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> MSM_SORT_LB], 1u); });
   __syncthreads();
   if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
@@ -452,7 +455,7 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
   const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
     msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t val) {
-      const uint32_t p = atomicAdd(&cur[key >> 8], 1u);
+      const uint32_t p = atomicAdd(&cur[key >> MSM_SORT_LB], 1u);
       keys[p] = (uint16_t)key;
       vals[p] = val;
     });
@@ -464,16 +467,16 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
                                                                    const uint32_t* __restrict__ tv,
                                                                    uint16_t* __restrict__ ko,
                                                                    uint32_t* __restrict__ vo) {
-  __shared__ uint32_t c[256];
+  __shared__ uint32_t c[MSM_SORT_NL];
   const uint32_t b0 = bin_start[blockIdx.x], b1 = bin_start[blockIdx.x + 1], t = threadIdx.x;
   if (b0 == b1) return;
-  if (t < 256) c[t] = 0;
+  if (t < MSM_SORT_NL) c[t] = 0;
   __syncthreads();
-  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) atomicAdd(&c[tk[p] & 255u], 1u);
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) atomicAdd(&c[tk[p] & (MSM_SORT_NL - 1)], 1u);
   __syncthreads();
-  // exclusive scan of the 256 counters by the first 4 waves (wave scan + wave totals)
+  // exclusive scan of the low counters by the first waves (wave scan + wave totals)
   uint32_t v = 0, x = 0;
-  if (t < 256) {
+  if (t < MSM_SORT_NL) {
     v = c[t];
     x = v;
 #pragma unroll
@@ -483,9 +486,9 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
     }
   }
   __shared__ uint32_t wt[4];
-  if (t < 256 && (t & 63) == 63) wt[t >> 6] = x;
+  if (t < MSM_SORT_NL && (t & 63) == 63) wt[t >> 6] = x;
   __syncthreads();
-  if (t < 256) {
+  if (t < MSM_SORT_NL) {
     uint32_t base = b0;
     for (uint32_t w = 0; w < (t >> 6); w++) base += wt[w];
     c[t] = base + x - v;
@@ -493,7 +496,7 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
   __syncthreads();
   for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
     const uint16_t key = tk[p];
-    const uint32_t q = atomicAdd(&c[key & 255u], 1u);
+    const uint32_t q = atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
     ko[q] = key;
     vo[q] = tv[p];
   }

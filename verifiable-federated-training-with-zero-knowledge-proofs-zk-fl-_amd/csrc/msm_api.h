@@ -21,6 +21,10 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef MSM_SORT_ROCPRIM
 #define MSM_SORT_ROCPRIM 0
 #endif
+// key bits sorted inside one high bin of the bucket sort (8: 128 high bins, 7: 256)
+#ifndef MSM_SORT_LOW_BITS
+#define MSM_SORT_LOW_BITS 8
+#endif
 #ifndef MSM_G1_L
 #define MSM_G1_L 16
 #endif
