@@ -472,7 +472,22 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
   if (b0 == b1) return;
   if (t < MSM_SORT_NL) c[t] = 0;
   __syncthreads();
+#if MSM_SORT_STAGE
+  // a bin that fits is read from memory once: its pairs wait in LDS for the placing loop
+  __shared__ uint16_t sk[MSM_SORT_STAGE];
+  __shared__ uint32_t sv[MSM_SORT_STAGE];
+  const bool staged = b1 - b0 <= MSM_SORT_STAGE;
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
+    const uint16_t key = tk[p];
+    if (staged) {
+      sk[p - b0] = key;
+      sv[p - b0] = tv[p];
+    }
+    atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
+  }
+#else
   for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) atomicAdd(&c[tk[p] & (MSM_SORT_NL - 1)], 1u);
+#endif
   __syncthreads();
   // exclusive scan of the low counters by the first waves (wave scan + wave totals)
   uint32_t v = 0, x = 0;
@@ -495,10 +510,16 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
   }
   __syncthreads();
   for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
+#if MSM_SORT_STAGE
+    const uint16_t key = staged ? sk[p - b0] : tk[p];
+    const uint32_t val = staged ? sv[p - b0] : tv[p];
+#else
     const uint16_t key = tk[p];
+    const uint32_t val = tv[p];
+#endif
     const uint32_t q = atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
     ko[q] = key;
-    vo[q] = tv[p];
+    vo[q] = val;
   }
 }
 

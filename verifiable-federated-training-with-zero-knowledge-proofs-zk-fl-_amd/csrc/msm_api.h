@@ -25,6 +25,10 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef MSM_SORT_LOW_BITS
 #define MSM_SORT_LOW_BITS 8
 #endif
+// pairs of one high bin staged in LDS by the bucket sort's bins pass (0: the bin is read twice)
+#ifndef MSM_SORT_STAGE
+#define MSM_SORT_STAGE 0
+#endif
 #ifndef MSM_G1_L
 #define MSM_G1_L 16
 #endif
