@@ -121,7 +121,7 @@ def test_msm_g1_matches_oracle_pippenger(gpu_ctx):
     assert _g1_std(gpu_ctx.msm_g1(bases, _scal(ss))) == bn.msm(pts, ss)
 
 
-@pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max"])
+@pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max", "binedge"])
 def test_msm_g1_edge_cases(gpu_ctx, case):
     rnd = random.Random(hash(case) & 0xFFFF)
     n = 3000
@@ -143,6 +143,9 @@ def test_msm_g1_edge_cases(gpu_ctx, case):
         ss = [ss[i // 2] for i in range(n)]
     elif case == "max":
         ss = [R - 1] * n
+    elif case == "binedge":       # bucket sort (csrc/msm.h k_msm_bin_*): digits on high-bin edges
+        edge = [1, 2, 255, 256, 257, 512, 32767, 32768, 32769, 65535]
+        ss = [sum(rnd.choice(edge) << (16 * j) for j in range(16)) % R for _ in range(n)]
     bases = bytearray(_bases_g1(gpu_ctx, ks))
     if case == "inf_base":
         for i in range(0, n, 3):

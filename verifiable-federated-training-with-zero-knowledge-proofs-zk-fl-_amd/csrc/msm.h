@@ -361,7 +361,9 @@ constexpr int MSM_SORT_NL = 1 << MSM_SORT_LB;        // low counters per high-bi
 constexpr int MSM_SORT_HB = MSM_NB >> MSM_SORT_LB;   // high bins
 constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
 static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 256 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
-constexpr int MSM_SORT_BT = 1024;         // threads per high-bin workgroup
+constexpr int MSM_SORT_BT = 1024;         // threads of the scan workgroup
+constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin workgroup
+static_assert(MSM_SORT_BINT >= MSM_SORT_NL && MSM_SORT_BINT <= 1024, "bins: one thread per low counter");
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
 // Signed digits of base i's scalar: fn(key, val) for every non-zero digit (as k_msm_digits).
@@ -462,7 +464,7 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
 }
 
 // One workgroup per high bin: [bin_start[b], bin_start[b+1]) of (tk, tv) -> buckets in (ko, vo).
-static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
+static __global__ void __launch_bounds__(MSM_SORT_BINT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
                                                                    const uint16_t* __restrict__ tk,
                                                                    const uint32_t* __restrict__ tv,
                                                                    uint16_t* __restrict__ ko,
@@ -477,7 +479,7 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
   __shared__ uint16_t sk[MSM_SORT_STAGE];
   __shared__ uint32_t sv[MSM_SORT_STAGE];
   const bool staged = b1 - b0 <= MSM_SORT_STAGE;
-  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BINT) {
     const uint16_t key = tk[p];
     if (staged) {
       sk[p - b0] = key;
@@ -486,7 +488,7 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
     atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
   }
 #else
-  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) atomicAdd(&c[tk[p] & (MSM_SORT_NL - 1)], 1u);
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BINT) atomicAdd(&c[tk[p] & (MSM_SORT_NL - 1)], 1u);
 #endif
   __syncthreads();
   // exclusive scan of the low counters by the first waves (wave scan + wave totals)
@@ -509,7 +511,7 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_sort(const uint3
     c[t] = base + x - v;
   }
   __syncthreads();
-  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BT) {
+  for (uint32_t p = b0 + t; p < b1; p += MSM_SORT_BINT) {
 #if MSM_SORT_STAGE
     const uint16_t key = staged ? sk[p - b0] : tk[p];
     const uint32_t val = staged ? sv[p - b0] : tv[p];
@@ -935,7 +937,7 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
   if (!(ZK_KNOCKOUT & 2)) {
     hipLaunchKernelGGL(k_msm_bin_scatter, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
                        b.extra_start, b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
-    hipLaunchKernelGGL(k_msm_bin_sort, dim3(MSM_SORT_HB), dim3(MSM_SORT_BT), 0, st, bin_start, pl.keys_in, pl.vals_in,
+    hipLaunchKernelGGL(k_msm_bin_sort, dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st, bin_start, pl.keys_in, pl.vals_in,
                        pl.keys_out, pl.vals_out);
   }
   return hipGetLastError();

@@ -29,6 +29,10 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef MSM_SORT_STAGE
 #define MSM_SORT_STAGE 0
 #endif
+// threads per high-bin workgroup of the bucket sort's bins pass
+#ifndef MSM_SORT_BIN_THREADS
+#define MSM_SORT_BIN_THREADS 1024
+#endif
 #ifndef MSM_G1_L
 #define MSM_G1_L 16
 #endif
