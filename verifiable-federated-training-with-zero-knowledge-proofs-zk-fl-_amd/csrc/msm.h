@@ -14,7 +14,8 @@
 //    no window combination.  288 GB of HBM makes the 16x base expansion (~2 GB for the
 //    2^18-constraint training circuit) free.
 //  * Signed digits in [-2^15, 2^15]; the sign is applied by negating y on the fly.
-//  * (bucket, entry) pairs are radix-sorted (rocPRIM, 16 key bits).  The sorted entries are cut
+//  * (bucket, entry) pairs are bucket-sorted (two counting passes over the 15-bit bucket
+//    number, k_msm_bin_*; zero digits dropped).  The sorted entries are cut
 //    into fixed chunks of L entries, one lane each, independent of bucket boundaries: every lane
 //    does exactly L additions.  A bucket run that starts and ends inside its chunk is final and
 //    written to its bucket; a run cut by a chunk edge becomes an "item" (<= 2 per chunk).
