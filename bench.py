@@ -68,6 +68,9 @@ PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "assemble", 
 CIRCUITS = {
     "M": ("sgd_verified", (128, 4, 7, 1000)),
     "C2": ("sgd_verified", (8, 4, 3, 1000)),
+    # circom's compile of the Report's N=128 training circuit has ~283 K constraints (Report.pdf p.6
+    # Table 5) -> domain 2^19; this build's tighter R1CS reaches that count at BATCH = 139
+    "M19": ("sgd_verified", (139, 4, 7, 1000)),
 }
 
 
@@ -114,12 +117,15 @@ def verify_all(ctx, zk, proofs, pubs_of):
     return sum(ok)
 
 
-def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist):
+def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist, zk, expect_pubs):
     """input.json text -> proofs through zkfl_groth16_full_prove_json_batch: host worker threads
     parse the texts (the C parser) while earlier proofs run, the witness engine computes a
     slot-group of witnesses at a time straight into HBM, one group ahead of the slots that prove
     them; `steps` x `slots` proofs per rank, max-over-ranks time.  The parse of every text is
-    inside the timed region."""
+    inside the timed region.  Afterwards every proof goes through the GPU batch verifier against
+    the public signals it returned, and those must equal the ones its input commits to
+    (expect_pubs[i % clients], from the host witness images): `steps` slot-groups reuse the
+    pipeline's three device witness sets, so a reuse race would show here."""
     n = steps * slots
     texts = [json_inputs[i % len(json_inputs)] for i in range(n)]
     key.full_prove_json_batch(wp, texts[:slots])   # warm slot buffers
@@ -129,8 +135,15 @@ def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist):
     _barrier(ctx, dist)
     dt = _max_over_ranks(time.perf_counter() - t0, dist)
     assert len(out) == n
+    for i, (_, pub) in enumerate(out):
+        got = b"".join(x.to_bytes(32, "little") for x in pub)
+        if got != expect_pubs[i % len(expect_pubs)]:
+            raise SystemExit(f"end-to-end proof {i}: public signals differ from its input's witness")
+    ok = _sum_over_ranks(verify_all(ctx, zk, [p for p, _ in out], lambda i: expect_pubs[i % len(expect_pubs)]), dist)
     world = dist.get_world_size() if dist is not None else 1
-    return {"value": round(world * n / dt, 3), "unit": "proofs/s", "proofs": world * n,
+    if ok != world * n:
+        raise SystemExit(f"end-to-end: {world * n - ok} proofs do not verify")
+    return {"value": round(world * n / dt, 3), "unit": "proofs/s", "proofs": world * n, "verified": ok,
             "path": "input.json texts -> C parse (host worker threads, overlapped) -> GPU witnesses a slot-group "
                     "at a time, one group ahead -> GPU proofs (zkfl_groth16_full_prove_json_batch)"}
 
@@ -151,19 +164,24 @@ def roofline_pass(key, ctx, ws, slots, n=6):
 
 
 def _pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/rocpd_summary.py)."""
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/rocpd_summary.py pmc),
+    used only when that summary was collected on a library built from the same sources as the one
+    loaded now (its build_id == zkfl_build_id()).  -> (bytes or None, provenance note)"""
+    from zkfl import native
     try:
         with open(PMC_TRAFFIC) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no PMC summary (profiles/pmc_traffic.json)"
+    if d.get("build_id") != native.build_id():
+        return None, f"PMC summary is of build {d.get('build_id')}, not the loaded {native.build_id()}"
     for name, v in d.get("kernels", {}).items():
         if KERNEL_SYMBOL[kernel] in name:
-            return v["traffic"]
-    return None
+            return v["traffic"], f"profiles/pmc_traffic.json, build {d['build_id']}"
+    return None, "kernel absent from the PMC summary"
 
 
-def roofline(prof, key):
+def roofline(prof, key, traffic=True):
     """The dominant kernel's roofline."""
     cand = {k: v for k, v in prof.items() if k in IMPL_BYTES_PER_ENTRY and v[1] > 0}
     if not cand:
@@ -178,14 +196,14 @@ def roofline(prof, key):
     algo = q * ALGO_BYTES_PER_BASE[dom]
     entries = units / launches
     impl = entries * IMPL_BYTES_PER_ENTRY[dom]
-    traffic = _pmc_traffic(dom)
+    traffic, traffic_src = _pmc_traffic(dom) if traffic else (None, "not collected for this leg")
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes": round(algo), "query_length": round(q),
             "impl_bytes": round(impl), "impl_GBps": round(impl / avg_s / 1e9, 1) if avg_s > 0 else 0.0,
-            "traffic_over_algorithmic": round(traffic / algo, 2) if traffic else None,
+            "traffic_over_algorithmic": round(traffic / algo, 2) if traffic else None, "traffic_source": traffic_src,
             "avg_launch_ms": round(avg_s * 1e3, 4), "mean_launch_ms": round(ms_tot / launches, 4),
             "launches": launches, "entries_per_launch": round(entries),
             "valu": {"achieved": round(fq, 2), "peak": round(FQMUL_PEAK_GPS, 1), "unit": "G Fq-mul/s",
@@ -194,13 +212,15 @@ def roofline(prof, key):
                      "peak_32bit_limbs": round(FQMUL_PEAK_GPS_32, 1)}}
 
 
-def c5_leg(ctx, rank, world, rounds, slots, dist):
-    """BASELINE config 5: `rounds` federated rounds of 8 clients x {training sgd_verified(8,4,3),
-    secure aggregation SecureMaskedUpdate(4,7)} (tests/full_system_simulation.mjs:1278-1343), both
-    keys resident.  Global proof k -> GPU k mod G; each rank pushes its share,
-    input.json text -> C parse -> GPU witness -> proof, through zkfl_groth16_full_prove_multi (the
-    two circuits' proofs interleaved on the device).  Total work is fixed: strong scaling.
-    Every proof is GPU-verified afterwards.  -> report dict (rank 0)."""
+def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
+    """BASELINE config 5: federated rounds of 8 clients x {training sgd_verified(8,4,3), secure
+    aggregation SecureMaskedUpdate(4,7)} (tests/full_system_simulation.mjs:1278-1343), both keys
+    resident, input.json text -> C parse -> GPU witness -> proof through zkfl_groth16_full_prove_multi
+    (the two circuits' proofs interleaved on the device).  Two measurements over the same keys:
+      strong: `rounds` rounds in total, global proof k -> GPU k mod G (SURVEY.md §8e);
+      weak:   `weak_rounds` rounds of 8 clients per GPU (each rank its own clients, ids offset by
+              8 x rank), so per-GPU work is fixed as G grows -- "batch-sharded across 8 MI355X".
+    Every proof is GPU-verified afterwards.  -> (strong report, weak report or None) (rank 0)."""
     from zkfl import circuits, clients, groth16, native, wprog, zkey
     t0 = time.perf_counter()
     circ = {"train": circuits.build("sgd_verified", 8, 4, 3, 1000), "secagg": circuits.build("secure_masked_update", 4, 7)}
@@ -212,41 +232,105 @@ def c5_leg(ctx, rank, world, rounds, slots, dist):
         images[nm] = wprog.compile_program(b)
         progs[nm] = native.WitnessProgram(ctx, images[nm])
         vks[nm] = groth16.vk_bytes(groth16.export_verification_key(zk, alphabeta=False))
-    jobs = []          # (circuit, input.json text) in the reference's order: per client training, secagg
-    for r in range(rounds + 1):                        # round 0 = warm-up
-        for tr, sa, _ in clients.federated_round(8, rnd=r + 1):
-            jobs += [(r, "train", json.dumps(tr)), (r, "secagg", json.dumps(sa))]
-    mine = [j for k, j in enumerate([j for j in jobs if j[0] > 0]) if k % world == rank]
-    warm = [j for k, j in enumerate([j for j in jobs if j[0] == 0]) if k % world == rank]
-    log(f"[bench r{rank}] c5: keys for {[(nm, b.n_constraints) for nm, b in circ.items()]}, "
-        f"{len(mine)} of {rounds * 16} proofs on this rank ({time.perf_counter() - t0:.1f} s)")
+
+    def jobs_of(nrounds, first_id):
+        jobs = []          # (round, circuit, input.json text) in the reference's order: per client training, secagg
+        for r in range(nrounds):
+            for tr, sa, _ in clients.federated_round(8, rnd=r + 1, first_id=first_id):
+                jobs += [(r, "train", json.dumps(tr)), (r, "secagg", json.dumps(sa))]
+        return jobs
 
     def run(js):
         return ctx.full_prove_multi([(keys[nm], progs[nm], native.parse_inputs(images[nm], txt)) for _, nm, txt in js])
 
+    def verified(js, out):
+        ok = 0
+        for nm in keys:
+            sel = [o for (_, n2, _), o in zip(js, out) if n2 == nm]
+            if sel:
+                pubs = b"".join(x.to_bytes(32, "little") for _, pub in sel for x in pub)
+                ok += sum(ctx.verify_batch(vks[nm], pubs, b"".join(p for p, _ in sel), keys[nm].n_public))
+        return _sum_over_ranks(ok, dist)
+
+    def timed(js):
+        _barrier(ctx, dist)
+        t_start = time.perf_counter()
+        out = run(js)
+        _barrier(ctx, dist)
+        return _max_over_ranks(time.perf_counter() - t_start, dist), out
+
+    all_jobs = jobs_of(rounds + 1, 1)                  # round 0 = warm-up
+    mine = [j for k, j in enumerate([j for j in all_jobs if j[0] > 0]) if k % world == rank]
+    warm = [j for k, j in enumerate([j for j in all_jobs if j[0] == 0]) if k % world == rank]
+    log(f"[bench r{rank}] c5: keys for {[(nm, b.n_constraints) for nm, b in circ.items()]}, "
+        f"{len(mine)} of {rounds * 16} proofs on this rank ({time.perf_counter() - t0:.1f} s)")
     run(warm)
-    _barrier(ctx, dist)
-    t_start = time.perf_counter()
-    out = run(mine)
-    _barrier(ctx, dist)
-    elapsed = _max_over_ranks(time.perf_counter() - t_start, dist)
-    ok = 0
-    for nm in keys:
-        sel = [o for (_, n2, _), o in zip(mine, out) if n2 == nm]
-        if sel:
-            pubs = b"".join(x.to_bytes(32, "little") for _, pub in sel for x in pub)
-            ok += sum(ctx.verify_batch(vks[nm], pubs, b"".join(p for p, _ in sel), keys[nm].n_public))
-    ok = _sum_over_ranks(ok, dist)
-    for x in list(progs.values()) + list(keys.values()):
-        x.close()
+    elapsed, out = timed(mine)
+    ok = verified(mine, out)
     if ok != rounds * 16:
         raise SystemExit(f"[bench r{rank}] c5: {rounds * 16 - ok} proofs do not verify")
-    return {"value": round(rounds * 16 / elapsed, 3), "unit": "proofs/s", "proofs": rounds * 16, "verified": ok,
-            "rounds": rounds, "ms_per_round": round(elapsed / rounds * 1e3, 3), "scaling": "strong",
-            "workload": "8 clients x {sgd_verified(8,4,3,1000) training, SecureMaskedUpdate(4,7) secagg} per "
-                        "round, proof k -> GPU k mod G, input.json -> C parse -> GPU witness groups per key -> proof "
-                        "(zkfl_groth16_full_prove_multi, both keys resident)",
-            "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
+    workload = ("8 clients x {sgd_verified(8,4,3,1000) training, SecureMaskedUpdate(4,7) secagg} per round, "
+                "input.json -> C parse -> GPU witness groups per key -> proof (zkfl_groth16_full_prove_multi, "
+                "both keys resident)")
+    strong = {"value": round(rounds * 16 / elapsed, 3), "unit": "proofs/s", "proofs": rounds * 16, "verified": ok,
+              "rounds": rounds, "ms_per_round": round(elapsed / rounds * 1e3, 3), "scaling": "strong",
+              "workload": workload + "; proof k -> GPU k mod G",
+              "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
+    weak = None
+    if weak_rounds:
+        mine_w = jobs_of(weak_rounds, 1 + 8 * rank)     # this GPU's own 8 clients, every round
+        elapsed_w, out_w = timed(mine_w)
+        ok_w = verified(mine_w, out_w)
+        total = world * weak_rounds * 16
+        if ok_w != total:
+            raise SystemExit(f"[bench r{rank}] c5 weak: {total - ok_w} proofs do not verify")
+        weak = {"value": round(total / elapsed_w, 3), "unit": "proofs/s", "proofs": total, "verified": ok_w,
+                "rounds_per_gpu": weak_rounds, "clients_per_gpu": 8, "scaling": "weak",
+                "ms_per_round": round(elapsed_w / weak_rounds * 1e3, 3),
+                "workload": workload + "; 8 clients per GPU (ids 8 x rank + 1..8), every GPU proves its own rounds"}
+    for x in list(progs.values()) + list(keys.values()):
+        x.close()
+    return strong, weak
+
+
+def extra_circuit_leg(ctx, rank, world, circuit, steps, slots, dist):
+    """Throughput on another training-circuit size (default: M19, the 2^19 domain the Report's
+    ~283 K-constraint N=128 circuit has under circom): same prover, same slots, every proof
+    GPU-verified; stage times and the G1 roofline from a serialized pass.  -> report dict."""
+    from zkfl import circuits, clients, native, wprog, zkey
+    name, params = CIRCUITS[circuit]
+    t0 = time.perf_counter()
+    b = circuits.build(name, *params)
+    batch, dim, depth, precision = params
+    objs = [clients.Client(rank * 2 + c + 1, batch, dim, depth, clients.JsLcg(777 + c)).training_input(
+        batch, precision, 100000000)[0] for c in range(2)]
+    inputs = [wprog.input_bytes(b, x) for x in objs]
+    zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x19, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
+    key = native.ProvingKey(ctx, zk)
+    key.set_slots(slots)
+    wp = native.WitnessProgram(ctx, wprog.compile_program(b))
+    res = wp.compute_resident(key, inputs)
+    wts = wp.compute(inputs)
+    log(f"[bench r{rank}] {circuit}: {b.n_constraints} constraints, domain {key.domain_size} "
+        f"(setup {time.perf_counter() - t0:.1f} s)")
+    n = steps * slots
+    elapsed, proofs = timed_run(key, [res[i % 2] for i in range(slots)], [res[i % 2] for i in range(n)],
+                                draw_rs(n), ctx, dist)
+    pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]
+    ok = _sum_over_ranks(verify_all(ctx, zk, proofs, lambda i: pubs[i % 2]), dist)
+    if ok != world * n:
+        raise SystemExit(f"[bench r{rank}] {circuit}: {world * n - ok} proofs do not verify")
+    prof, nprof = roofline_pass(key, ctx, res, slots)
+    for r_ in res:
+        r_.close()
+    wp.close()
+    rep = {"value": round(world * n / elapsed, 3), "unit": "proofs/s", "proofs": world * n, "verified": ok,
+           "workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
+           "constraints": b.n_constraints, "domain": key.domain_size, "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "stage_ms_isolated_per_proof": {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()},
+           "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key, traffic=False)}
+    key.close()
+    return rep
 
 
 POS_RP = (56, 57, 56, 60, 60, 63, 64, 63, 60, 66, 60, 65, 70, 60, 64, 68)     # circomlib R_P, t = 2..17
@@ -336,6 +420,56 @@ def _sum_over_ranks(x, dist):
     return int(t.item())
 
 
+class KeyInfo:
+    """The proving-key sizes the roofline needs (kept after the key itself is freed)."""
+
+    def __init__(self, n_vars, n_public, domain_size):
+        self.n_vars, self.n_public, self.domain_size = n_vars, n_public, domain_size
+
+
+def _distinct_over_ranks(device, dist):
+    """Number of distinct GPUs the ranks run on (ranks may share a device in tests)."""
+    if dist is None:
+        return 1
+    import torch
+    t = torch.zeros(64, dtype=torch.int64)
+    t[device % 64] = 1
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.sum().item())
+
+
+def launch_ranks(n):
+    """bench.py --gpus N without a launcher: N child processes of this script, one per GPU, with
+    the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).
+    Called before any HIP call in this process; rank 0's JSON line is the children's stdout.
+    Returns the first non-zero exit status (the others are then terminated)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code and not rc:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def report(args, world, elapsed, n_timed_all, verified_all, prof, nprof, key, config, extra):
     """The bench JSON line (rank 0).  `extra`: roofline / end_to_end / c5 / cpu_baseline fields."""
     stage_ms = {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()}  # median x launches
@@ -363,12 +497,22 @@ def main():
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     ap.add_argument("--e2e-steps", type=int, default=16, help="steps of the input.json -> proof leg (0: skip)")
     ap.add_argument("--c5-rounds", type=int, default=8, help="federated rounds of the config-5 leg (0: skip)")
+    ap.add_argument("--c5-weak-rounds", type=int, default=4,
+                    help="config-5 weak-scaling leg: federated rounds of 8 own clients per GPU (0: skip)")
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
+    ap.add_argument("--extra-circuit", default="M19", help="second training-circuit size leg ('' or none: skip)")
+    ap.add_argument("--extra-steps", type=int, default=4, help="timed steps of the extra-circuit leg")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no outside launcher: start one process per GPU here, before anything touches HIP
+        return launch_ranks(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         "(or drop the launcher and let bench.py start them)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     from zkfl import circuits, clients, native, wprog, zkey
     # libzkfl (and with it /opt/rocm's HIP runtime) is loaded before torch, whose wheel carries its
     # own libamdhip64 under the same soname: one HIP runtime per process.  torch.distributed is the
@@ -382,6 +526,10 @@ def main():
         dist = dist_mod
         dist.init_process_group(backend="gloo")
     device = local_rank % max(1, n_dev)     # ranks beyond the device count share devices (tests)
+    devices_used = _distinct_over_ranks(device, dist)
+    build_id, source_id = native.build_id(), native.source_id()
+    if build_id != source_id:
+        log(f"[bench r{rank}] WARNING: libzkfl.so build {build_id} is not this tree's sources ({source_id})")
 
     name, params = CIRCUITS[args.circuit]
     t0 = time.perf_counter()
@@ -423,19 +571,26 @@ def main():
     if verified_all != n_timed * world:
         raise SystemExit(f"[bench r{rank}] {n_timed * world - verified_all} timed proofs do not verify")
     prof, nprof = roofline_pass(key, ctx, res, args.slots)
+    kinfo = KeyInfo(key.n_vars, key.n_public, key.domain_size)
     e2e = None
     if args.e2e_steps:
         e2e = end_to_end_leg(key, wp, wprog.compile_program(b), [json.dumps(x) for x in input_objs], args.slots,
-                             args.e2e_steps, ctx, dist)
+                             args.e2e_steps, ctx, dist, zk, pubs)
         log(f"[bench r{rank}] end to end: {e2e}")
     for r_ in res:
         r_.close()
     wp.close()
     key.set_slots(1)
-    c5 = None
+    c5 = c5w = None
     if args.c5_rounds:
-        c5 = c5_leg(ctx, rank, world, args.c5_rounds, min(args.slots, 8), dist)
-        log(f"[bench r{rank}] config 5: {c5}")
+        c5, c5w = c5_leg(ctx, rank, world, args.c5_rounds, min(args.slots, 8), dist, args.c5_weak_rounds)
+        log(f"[bench r{rank}] config 5: {c5}; weak: {c5w}")
+    extra = None
+    if args.extra_circuit and args.extra_circuit != "none" and args.extra_circuit != args.circuit:
+        key.close()
+        key = None
+        extra = extra_circuit_leg(ctx, rank, world, args.extra_circuit, args.extra_steps, args.slots, dist)
+        log(f"[bench r{rank}] {args.extra_circuit}: {extra}")
     merkle = None
     if args.merkle_log2n:
         merkle = merkle_leg(ctx, rank, args.merkle_log2n)
@@ -451,21 +606,24 @@ def main():
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
         config = {"workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
-                  "constraints": b.n_constraints, "wires": b.n_wires, "domain": key.domain_size,
+                  "constraints": b.n_constraints, "wires": b.n_wires, "domain": kinfo.domain_size,
                   "global_batch": args.slots * world, "step": f"{args.slots} proofs per GPU (one per slot)",
                   "parallelism": f"replicas{world}", "slots_in_flight": args.slots,
                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}
-        line = report(args, world, elapsed, n_timed * world, verified_all, prof, nprof, key, config,
-                      {"oracle_match": oracle_match, "end_to_end": e2e, "c5": c5, "dataset_commit": merkle,
-                       "cpu_baseline": cpu})
+        line = report(args, world, elapsed, n_timed * world, verified_all, prof, nprof, kinfo, config,
+                      {"n_gpus": devices_used, "ranks": world, "build_id": build_id,
+                       "build_matches_sources": build_id == source_id, "oracle_match": oracle_match,
+                       "end_to_end": e2e, "c5": c5, "c5_weak": c5w, "extra_circuit": extra,
+                       "dataset_commit": merkle, "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")
-    key.close()
+    if key is not None:
+        key.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

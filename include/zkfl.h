@@ -56,6 +56,10 @@ typedef struct zkfl_witness zkfl_witness;
 typedef struct zkfl_wprog zkfl_wprog;
 
 int zkfl_version(void);
+/* First 16 hex digits of SHA-256 over the sources this library was built from (csrc/*.h, *.hip,
+ * *.cc sorted by name, then include/zkfl.h; the package Makefile).  bench.py prints it and smoke()
+ * checks it against the tree it runs from (zkfl/native.py::source_id). */
+const char* zkfl_build_id(void);
 const char* zkfl_last_error(void);
 int zkfl_device_count(int* count);
 
@@ -80,10 +84,12 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
 int zkfl_key_free(zkfl_key* key);
 int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
 /* Number of proofs kept in flight by zkfl_groth16_prove_batch (1..32, default 3).  Each slot
- * owns one HIP stream (ZKFL_SLOT_STREAMS=2|3: two or three) and its own scratch; proofs in
- * different slots overlap on the GPU.  HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
- * (default 4): set it to >= streams x slots (at most 24 helps on MI355X) in the environment
- * before the first HIP call, or the slots serialize. */
+ * owns one HIP stream and its own scratch (~0.6 GB for the 2^18 training circuit); proofs in
+ * different slots overlap on the GPU.  HIP maps a process's streams onto GPU_MAX_HW_QUEUES
+ * hardware queues (HIP default 4, which the GPU boxes export): set it in the environment before
+ * the first HIP call to at least the slot count, or the slots serialize.  Measured on MI355X
+ * (bench.py's default): 20 slots over 28 queues is the best configuration; 24+
+ * slots or 32 queues oversubscribe the hardware queues and lose throughput. */
 int zkfl_key_set_slots(zkfl_key* key, int slots);
 
 /* Full prove from a .wtns byte image (host).  pub_out may be NULL; otherwise receives
@@ -245,6 +251,30 @@ int zkfl_dataset_commit(zkfl_ctx* ctx, const uint8_t* values, size_t n, uint32_t
 /* Dev-ceremony fixed-base multiplications: out[i] = scalars[i] * generator, mont affine. */
 int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
 int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out);
+
+/* Ceremony primitives: the bulk group work of the snarkjs setup commands the reference runs once
+ * per circuit (tests/test_secureagg.cjs:25-57: `powersoftau new|contribute|prepare phase2`,
+ * `groth16 setup`; tests/full_system_simulation.mjs:713-730: `groth16 setup`, `zkey contribute`).
+ * The file handling around them is zkfl/ptau.py.  Points are mont affine
+ * (the LEM bytes of ptau / zkey sections; infinity = all zero), scalars std 32 B LE; G2 points are
+ * x.c0|x.c1|y.c0|y.c1 (128 B).
+ *
+ * out[i] = scalars[i] * points[i]: `powersoftau contribute` (tauG1[i] *= tau^i, ...) and
+ * `zkey contribute` (delta *= d, C and H *= 1/d). */
+int zkfl_setup_g1_scale(zkfl_ctx* ctx, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out);
+int zkfl_setup_g2_scale(zkfl_ctx* ctx, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out);
+/* out[j] = (1/N) sum_i w^-ij points[i], N = 2^logn (logn <= 28), w = Fr.w[logn] (ffjavascript:
+ * nqr = 5): the inverse FFT over the group that `powersoftau prepare phase2` applies to each
+ * 2^p prefix of tauG1 / tauG2 / alphaTauG1 / betaTauG1 (ptau sections 12-15), i.e. L_j(tau) G. */
+int zkfl_setup_g1_lagrange(zkfl_ctx* ctx, const uint8_t* points, uint32_t logn, uint8_t* out);
+int zkfl_setup_g2_lagrange(zkfl_ctx* ctx, const uint8_t* points, uint32_t logn, uint8_t* out);
+/* Sparse combinations out[r] = sum_{t in [rowptr[r], rowptr[r+1])} coefs[t] * bases[idx[t]]
+ * (rowptr: n_out + 1 entries, rowptr[0] = 0, < 2^32 - 1 terms; idx[t] < n_bases; empty row ->
+ * infinity): `groth16 setup`'s A_i, B1_i, B2_i, C_i, IC_i from the Lagrange bases. */
+int zkfl_setup_g1_lincomb(zkfl_ctx* ctx, const uint8_t* bases, size_t n_bases, size_t n_out, const uint64_t* rowptr,
+                          const uint32_t* idx, const uint8_t* coefs, uint8_t* out);
+int zkfl_setup_g2_lincomb(zkfl_ctx* ctx, const uint8_t* bases, size_t n_bases, size_t n_out, const uint64_t* rowptr,
+                          const uint32_t* idx, const uint8_t* coefs, uint8_t* out);
 
 #ifdef __cplusplus
 }

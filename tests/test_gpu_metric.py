@@ -155,6 +155,55 @@ def test_metric_full_prove_json_batch(metric):
     assert got == want
 
 
+def test_metric_full_prove_json_batch_reuses_witness_sets(metric):
+    """4 slots x 20 texts = 5 slot-groups: the pipeline's three device witness sets are each taken
+    again (groups 3 and 4) while earlier groups' proofs may still read theirs.  Every proof equals
+    the one-at-a-time proof of the same witness and (r, s)."""
+    import json
+    from zkfl import clients
+    _, _, key, wp, wts = metric
+    objs = [clients.Client(cid, 128, 4, 7, clients.JsLcg(12345 + cid)).training_input(128, 1000, 100000000)[0]
+            for cid in (1, 2, 3, 4)]
+    order = [0, 1, 2, 3, 1, 0, 3, 2, 2, 2, 0, 1, 3, 3, 1, 0, 0, 3, 1, 2]
+    rs = [_le(secrets.randbelow(R)) + _le(secrets.randbelow(R)) for _ in order]
+    key.set_slots(4)
+    got = key.full_prove_json_batch(wp, [json.dumps(objs[i]) for i in order], b"".join(rs))
+    key.set_slots(1)
+    res = [key.upload(w) for w in wts]
+    for j, (i, (proof, pub)) in enumerate(zip(order, got)):
+        assert proof == key.prove_resident(res[i], rs[j]), f"job {j} (client {i + 1})"
+        assert pub[0] == i + 1
+    key.set_slots(3)
+    for r_ in res:
+        r_.close()
+
+
+def test_domain_2_19_proof_bit_exact_vs_c_oracle(gpu_ctx):
+    """sgd_verified(139, 4, 7, 1000): > 2^18 constraints (the Report's ~283 K circom count for
+    N=128), domain 2^19 -- the 2x NTT / H-MSM size -- proof and all five MSMs equal the C oracle."""
+    from oracle import cbaseline
+    from zkfl import circuits, clients, native, wprog, zkey
+    b = circuits.build("sgd_verified", 139, 4, 7, 1000)
+    assert b.n_constraints > (1 << 18)
+    zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(tau=0x19, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
+    key = native.ProvingKey(gpu_ctx, zk)
+    wp = native.WitnessProgram(gpu_ctx, wprog.compile_program(b))
+    c = clients.Client(5, 139, 4, 7, clients.JsLcg(12350))
+    wt = wp.compute([wprog.input_bytes(b, c.training_input(139, 1000, 100000000)[0])])[0]
+    assert key.domain_size == 1 << 19
+    rs = _le(0xABCDEF) + _le(0xFEDCBA)
+    proof, pub = key.prove(wt, rs)
+    ref, ref_h, ref_parts = cbaseline.prove_parts(zk, wt, rs, key.domain_size, _threads())
+    assert proof == ref
+    hs, parts = key.debug_parts(wt)
+    assert hs == ref_h
+    for name in ("A", "B1", "B2", "C", "H"):
+        assert parts[name] == ref_parts[name], name
+    assert pub[0] == 5
+    wp.close()
+    key.close()
+
+
 def test_full_prove_json_batch_errors(gpu_ctx):
     """A malformed / incomplete text at index k: ZKFL_E_ARG naming input k; the key keeps working."""
     import json

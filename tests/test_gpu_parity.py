@@ -7,6 +7,7 @@ and matches the oracle on a basis) plus pairing verification of every proof.
 import json
 import os
 import random
+import zlib
 
 import pytest
 
@@ -123,7 +124,7 @@ def test_msm_g1_matches_oracle_pippenger(gpu_ctx):
 
 @pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max", "binedge"])
 def test_msm_g1_edge_cases(gpu_ctx, case):
-    rnd = random.Random(hash(case) & 0xFFFF)
+    rnd = random.Random(zlib.crc32(case.encode()))
     n = 3000
     ks = [rnd.randrange(1, R) for _ in range(n)]
     ss = [rnd.randrange(R) for _ in range(n)]
@@ -169,7 +170,7 @@ def test_msm_g2_identity(gpu_ctx, n):
 def test_msm_g2_edge_cases(gpu_ctx, case):
     """G2 runs on lane pairs (csrc/field.h Fq2PairOps): the exceptional additions (P + P inside a
     bucket, P + (-P), infinity bases) and a single-bucket skew must stay pair-uniform."""
-    rnd = random.Random(hash(case) & 0xFFFF)
+    rnd = random.Random(zlib.crc32(case.encode()))
     n = 1500
     ks = [rnd.randrange(1, R) for _ in range(n)]
     ss = [rnd.randrange(R) for _ in range(n)]

@@ -77,3 +77,12 @@ def test_two_rank_gloo_report(tmp_path):
     assert rep["ms_per_step"] >= 8 * 20 / 8 * 0.9
     assert abs(rep["value"] - 2 * 8 / (rep["ms_per_step"] * 8 / 1e3)) < 1e-3 * rep["value"] + 1e-6
     assert rep["metric"].startswith("Groth16 proofs/sec") and rep["verified"] == 16
+
+
+def test_bench_refuses_world_size_mismatch():
+    """WORLD_SIZE from a launcher must equal --gpus (checked before anything touches HIP)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in p.stderr

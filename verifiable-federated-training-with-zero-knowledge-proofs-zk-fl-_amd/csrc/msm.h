@@ -406,6 +406,11 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint3
 }
 
 // cnt[HB * nblk] (bin-major) -> exclusive offsets in place; bin_start[HB + 1]; *nnz.
+// The scan keeps all 32 K counters in LDS (~139 KB): gfx950's 160 KB per workgroup.  Any other
+// device target must use the rocPRIM sort (MSM_SORT_ROCPRIM=1).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !MSM_SORT_ROCPRIM
+#error "the bucket sort's scan needs gfx950's 160 KB of LDS: build with MSM_SORT_ROCPRIM=1 for this target"
+#endif
 static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* __restrict__ cnt, uint32_t nblk,
                                                                    uint32_t* __restrict__ bin_start,
                                                                    uint32_t* __restrict__ nnz) {

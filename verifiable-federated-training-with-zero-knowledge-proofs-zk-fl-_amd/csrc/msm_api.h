@@ -12,10 +12,15 @@ constexpr int MSM_C = 16;                  // window bits
 constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 // Knock-out builds for marginal-cost measurements (tools/ko_probe.py; proofs are WRONG, timing
-// only): 1 assembly, 2 radix sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
-// 64 the G1 accumulation kernel.  0 in every real build.
+// only): 1 assembly, 2 digit sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
+// 64 the G1 accumulation kernel.  0 in every real build; a non-zero value only compiles together
+// with ZK_KNOCKOUT_AB_ONLY (tools/build_ab.sh sets both), so a wrong-proof library cannot be built
+// by a stray define.
 #ifndef ZK_KNOCKOUT
 #define ZK_KNOCKOUT 0
+#endif
+#if ZK_KNOCKOUT != 0 && !defined(ZK_KNOCKOUT_AB_ONLY)
+#error "ZK_KNOCKOUT builds compute wrong proofs: timing A/B only (define ZK_KNOCKOUT_AB_ONLY to acknowledge)"
 #endif
 // 1: digits sorted by rocPRIM's radix sort (A/B builds); 0: the two-pass bucket sort in msm.h
 #ifndef MSM_SORT_ROCPRIM

@@ -39,6 +39,7 @@
 #include "msm_api.h"
 #include "ntt.h"
 #include "prof.h"
+#include "setup.h"
 #include "verify.h"
 #include "witness.h"
 #include "zkfl.h"
@@ -1694,6 +1695,63 @@ int zkfl_setup_g1_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8
 
 int zkfl_setup_g2_gen_mul(zkfl_ctx* ctx, const uint8_t* scalars, size_t n, uint8_t* out) {
   return run_gen_mul<Fq2Ops>(ctx, scalars, n, out, true);
+}
+
+// Ceremony primitives (csrc/setup.hip)
+static int setup_scale_abi(zkfl_ctx* ctx, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
+                           bool g2) {
+  if (!ctx || (n && (!points || !scalars || !out))) return fail(ZKFL_E_ARG, "setup scale: bad args");
+  hipError_t e = setup_scale(g2, ctx->st, points, scalars, n, out);
+  return e == hipSuccess ? ZKFL_OK : hip_fail(e, "setup scale");
+}
+
+int zkfl_setup_g1_scale(zkfl_ctx* ctx, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out) {
+  return setup_scale_abi(ctx, points, scalars, n, out, false);
+}
+
+int zkfl_setup_g2_scale(zkfl_ctx* ctx, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out) {
+  return setup_scale_abi(ctx, points, scalars, n, out, true);
+}
+
+static int setup_lagrange_abi(zkfl_ctx* ctx, const uint8_t* points, uint32_t logn, uint8_t* out, bool g2) {
+  if (!ctx || !points || !out) return fail(ZKFL_E_ARG, "setup lagrange: bad args");
+  if (logn > 28) return fail(ZKFL_E_ARG, "setup lagrange: logn > 28 (BN254 Fr 2-adicity)");
+  hipError_t e = setup_lagrange(g2, ctx->st, points, (int)logn, out);
+  return e == hipSuccess ? ZKFL_OK : hip_fail(e, "setup lagrange");
+}
+
+int zkfl_setup_g1_lagrange(zkfl_ctx* ctx, const uint8_t* points, uint32_t logn, uint8_t* out) {
+  return setup_lagrange_abi(ctx, points, logn, out, false);
+}
+
+int zkfl_setup_g2_lagrange(zkfl_ctx* ctx, const uint8_t* points, uint32_t logn, uint8_t* out) {
+  return setup_lagrange_abi(ctx, points, logn, out, true);
+}
+
+static int setup_lincomb_abi(zkfl_ctx* ctx, const uint8_t* bases, size_t n_bases, size_t n_out,
+                             const uint64_t* rowptr, const uint32_t* idx, const uint8_t* coefs, uint8_t* out,
+                             bool g2) {
+  if (!ctx || !rowptr || (n_out && !out)) return fail(ZKFL_E_ARG, "setup lincomb: bad args");
+  if (rowptr[0] != 0) return fail(ZKFL_E_ARG, "setup lincomb: rowptr[0] != 0");
+  for (size_t r = 0; r < n_out; r++)
+    if (rowptr[r + 1] < rowptr[r]) return fail(ZKFL_E_ARG, "setup lincomb: rowptr not monotonic at " + std::to_string(r));
+  const uint64_t nnz = rowptr[n_out];
+  if (nnz >= 0xffffffffull) return fail(ZKFL_E_ARG, "setup lincomb: more than 2^32 - 2 terms");
+  if (nnz && (!idx || !coefs || !bases)) return fail(ZKFL_E_ARG, "setup lincomb: bad args");
+  for (uint64_t t = 0; t < nnz; t++)  // no device access outside the bases
+    if (idx[t] >= n_bases) return fail(ZKFL_E_ARG, "setup lincomb: term " + std::to_string(t) + " base index out of range");
+  hipError_t e = setup_lincomb(g2, ctx->st, bases, n_bases, n_out, rowptr, idx, coefs, out);
+  return e == hipSuccess ? ZKFL_OK : hip_fail(e, "setup lincomb");
+}
+
+int zkfl_setup_g1_lincomb(zkfl_ctx* ctx, const uint8_t* bases, size_t n_bases, size_t n_out, const uint64_t* rowptr,
+                          const uint32_t* idx, const uint8_t* coefs, uint8_t* out) {
+  return setup_lincomb_abi(ctx, bases, n_bases, n_out, rowptr, idx, coefs, out, false);
+}
+
+int zkfl_setup_g2_lincomb(zkfl_ctx* ctx, const uint8_t* bases, size_t n_bases, size_t n_out, const uint64_t* rowptr,
+                          const uint32_t* idx, const uint8_t* coefs, uint8_t* out) {
+  return setup_lincomb_abi(ctx, bases, n_bases, n_out, rowptr, idx, coefs, out, true);
 }
 
 // ---------------------------------------------------------------------------

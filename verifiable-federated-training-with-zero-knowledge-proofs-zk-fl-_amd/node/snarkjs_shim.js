@@ -235,7 +235,36 @@ function done(p) {
   p.then((code) => process.exit(code || 0)).catch((e) => { console.error('[ERROR] snarkJS: ' + e.message); process.exit(1); });
 }
 
-if (require.main === module) {
+// The one-time ceremony commands (powersoftau new|contribute|prepare phase2, groth16 setup,
+// zkey new|contribute and their aliases; tests/test_secureagg.cjs:25-57,
+// tests/full_system_simulation.mjs:713-730) are served by the package's Python host, which drives
+// the same libzkfl (zkfl_setup_*: scalar multiplications, group FFTs and sparse combinations on the
+// GPU): `python3 -m zkfl <the same argv>` as a child process, its exit status passed through.
+const CEREMONY = new Set(['powersoftau', 'ptn', 'ptc', 'pt2', 'g16s', 'zkn', 'zkc']);
+
+function isCeremony(argv) {
+  const a = argv.filter((x) => !x.startsWith('-'));
+  return CEREMONY.has(a[0]) || (a[0] === 'groth16' && a[1] === 'setup') ||
+    (a[0] === 'zkey' && (a[1] === 'new' || a[1] === 'contribute'));
+}
+
+function runCeremony(argv) {
+  const { spawnSync } = require('child_process');
+  const pkg = path.join(__dirname, '..');
+  const env = Object.assign({}, process.env, {
+    PYTHONPATH: pkg + (process.env.PYTHONPATH ? path.delimiter + process.env.PYTHONPATH : ''),
+  });
+  const r = spawnSync(process.env.ZKFL_PYTHON || 'python3', ['-m', 'zkfl'].concat(argv), { stdio: 'inherit', env });
+  if (r.error) {
+    console.error('[ERROR] snarkJS: cannot start the zkfl ceremony host: ' + r.error.message);
+    return 1;
+  }
+  return r.status === null ? 1 : r.status;
+}
+
+if (require.main === module && isCeremony(process.argv.slice(2))) {
+  process.exit(runCeremony(process.argv.slice(2)));
+} else if (require.main === module) {
   const a = process.argv.slice(2).filter((x) => !x.startsWith('-'));
   const [cmd, sub] = a;
   const w = (f, o) => fs.writeFileSync(f, JSON.stringify(o, null, 1));
@@ -275,7 +304,12 @@ if (require.main === module) {
                   '       snarkjs groth16 verify <vkey.json> <public.json> <proof.json>\n' +
                   '       snarkjs wtns calculate <circuit.wasm> <input.json> <out.wtns>\n' +
                   '       snarkjs zkey export verificationkey <zkey> <vkey.json>\n' +
-                  '       snarkjs r1cs info <circuit.r1cs>');
+                  '       snarkjs r1cs info <circuit.r1cs>\n' +
+                  '       snarkjs powersoftau new bn128 <power> <out.ptau>\n' +
+                  '       snarkjs powersoftau contribute <in.ptau> <out.ptau> [-e=entropy] [--name=name]\n' +
+                  '       snarkjs powersoftau prepare phase2 <in.ptau> <out.ptau>\n' +
+                  '       snarkjs groth16 setup <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>\n' +
+                  '       snarkjs zkey contribute <in.zkey> <out.zkey> [--name=name] [-e=entropy]');
     process.exit(99);
   }
 }

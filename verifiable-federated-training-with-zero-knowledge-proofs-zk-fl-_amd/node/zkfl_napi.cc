@@ -19,6 +19,7 @@
 //   fullProve(ctx, key, prog, inputJsonString[, rsBuffer])
 //       -> Promise<{proof: Buffer(256), publicSignals: Buffer}>           (zkfl_groth16_full_prove_json)
 //   pairing(ctx, g1Buffer(64), g2Buffer(128)) -> Buffer(384)              (zkfl_pairing, vk_alphabeta_12)
+//   poseidon / vectorHash / merkleBuild                                    (node/circomlibjs, see below)
 #include <node_api.h>
 
 #include <cstring>
@@ -424,6 +425,66 @@ napi_value Pairing(napi_env env, napi_callback_info info) {
   return buf;
 }
 
+// Poseidon / vectorHash / Merkle trees on the GPU for the circomlibjs face (node/circomlibjs):
+// the harness's off-circuit commitments (tests/full_system_simulation.mjs:134-238).  Synchronous:
+// one small launch each, like circomlibjs's own synchronous `poseidon(...)`.
+//   poseidon(ctx, arity, n, inputs(n*arity*32)) -> Buffer(n*32)          (zkfl_poseidon_batch)
+//   vectorHash(ctx, len, n, values(n*len*32)) -> Buffer(n*32)            (zkfl_vector_hash_batch)
+//   merkleBuild(ctx, leaves(n*32), depth) -> Buffer((2^(depth+1)-1)*32)  (zkfl_merkle_build)
+bool get_ctx_buf(napi_env env, napi_value* argv, size_t argc, size_t need, void** ctx, void** data, size_t* len,
+                 size_t buf_arg) {
+  return argc >= need && napi_get_value_external(env, argv[0], ctx) == napi_ok &&
+         napi_get_buffer_info(env, argv[buf_arg], data, len) == napi_ok;
+}
+
+napi_value HashCall(napi_env env, napi_callback_info info, bool vector) {
+  size_t argc = 4;
+  napi_value argv[4];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *in = nullptr;
+  size_t len = 0;
+  uint32_t width = 0, n = 0;
+  if (!get_ctx_buf(env, argv, argc, 4, &ctx, &in, &len, 3) || napi_get_value_uint32(env, argv[1], &width) != napi_ok ||
+      napi_get_value_uint32(env, argv[2], &n) != napi_ok || len != (size_t)width * n * 32) {
+    napi_throw_type_error(env, nullptr, vector ? "vectorHash(ctx, len, n, valuesBuffer(n*len*32))"
+                                               : "poseidon(ctx, arity, n, inputsBuffer(n*arity*32))");
+    return nullptr;
+  }
+  std::vector<uint8_t> out((size_t)n * 32 + 32);
+  int rc = vector ? zkfl_vector_hash_batch(static_cast<zkfl_ctx*>(ctx), width, n, static_cast<const uint8_t*>(in), out.data())
+                  : zkfl_poseidon_batch(static_cast<zkfl_ctx*>(ctx), width, n, static_cast<const uint8_t*>(in), out.data());
+  if (rc) return throw_err(env, rc);
+  napi_value buf;
+  void* p;
+  napi_create_buffer_copy(env, (size_t)n * 32, out.data(), &p, &buf);
+  return buf;
+}
+
+napi_value Poseidon(napi_env env, napi_callback_info info) { return HashCall(env, info, false); }
+napi_value VectorHash(napi_env env, napi_callback_info info) { return HashCall(env, info, true); }
+
+napi_value MerkleBuild(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void *ctx = nullptr, *in = nullptr;
+  size_t len = 0;
+  uint32_t depth = 0;
+  if (!get_ctx_buf(env, argv, argc, 3, &ctx, &in, &len, 1) || napi_get_value_uint32(env, argv[2], &depth) != napi_ok ||
+      len % 32 || depth > ZKFL_MERKLE_MAX_DEPTH) {
+    napi_throw_type_error(env, nullptr, "merkleBuild(ctx, leavesBuffer(n*32), depth)");
+    return nullptr;
+  }
+  const size_t nodes = ((size_t)2 << depth) - 1;
+  std::vector<uint8_t> out(nodes * 32);
+  int rc = zkfl_merkle_build(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(in), len / 32, depth, out.data());
+  if (rc) return throw_err(env, rc);
+  napi_value buf;
+  void* p;
+  napi_create_buffer_copy(env, out.size(), out.data(), &p, &buf);
+  return buf;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -437,6 +498,9 @@ napi_value Init(napi_env env, napi_value exports) {
       {"witness", nullptr, Witness, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"fullProve", nullptr, FullProve, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"pairing", nullptr, Pairing, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"poseidon", nullptr, Poseidon, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"vectorHash", nullptr, VectorHash, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"merkleBuild", nullptr, MerkleBuild, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

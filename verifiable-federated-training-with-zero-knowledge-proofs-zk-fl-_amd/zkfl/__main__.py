@@ -32,7 +32,7 @@ import os
 import secrets
 import sys
 
-from . import circuits, groth16, native, r1cs_file, wprog, zkey
+from . import circuits, groth16, native, r1cs_file, snarkjs_cli, wprog, zkey
 
 
 def _circuit(args):
@@ -156,6 +156,9 @@ def cmd_verify(args):
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    if argv and argv[0] in snarkjs_cli.VERBS:   # snarkjs ceremony strings (zkfl/snarkjs_cli.py)
+        return snarkjs_cli.run(argv)
     ap = argparse.ArgumentParser(prog="python -m zkfl", description=__doc__.split("\n")[0])
     sub = ap.add_subparsers(dest="cmd", required=True)
 

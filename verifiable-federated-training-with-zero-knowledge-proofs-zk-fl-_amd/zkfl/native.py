@@ -25,6 +25,7 @@ _P = C.c_void_p
 _U8P = C.POINTER(C.c_uint8)
 SIGNATURES = {
     "zkfl_version": (C.c_int, []),
+    "zkfl_build_id": (C.c_char_p, []),
     "zkfl_last_error": (C.c_char_p, []),
     "zkfl_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "zkfl_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
@@ -51,6 +52,14 @@ SIGNATURES = {
     "zkfl_ntt_coset": (C.c_int, [_P, _U8P, C.c_uint32]),
     "zkfl_setup_g1_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_setup_g2_gen_mul": (C.c_int, [_P, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_setup_g1_scale": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_setup_g2_scale": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
+    "zkfl_setup_g1_lagrange": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U8P]),
+    "zkfl_setup_g2_lagrange": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U8P]),
+    "zkfl_setup_g1_lincomb": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_size_t, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint32), C.c_char_p, _U8P]),
+    "zkfl_setup_g2_lincomb": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_size_t, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint32), C.c_char_p, _U8P]),
     "zkfl_groth16_verify": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p]),
     "zkfl_groth16_verify_batch": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_size_t, C.c_char_p, C.c_size_t,
                                             C.c_char_p, C.POINTER(C.c_int32)]),
@@ -135,6 +144,25 @@ def poseidon_params(t: int):
     consts = _ints(bytes(c))[:(8 + rp.value) * t]
     pts = _ints(bytes(xy))
     return consts, pts[:t], pts[t:], rp.value
+
+
+def build_id() -> str:
+    """The loaded library's source hash (zkfl_build_id, set by the package Makefile)."""
+    return lib().zkfl_build_id().decode()
+
+
+def source_id(pkg_dir: str = _PKG_DIR) -> str:
+    """The same hash recomputed from the sources in this tree: csrc/*.h, *.hip, *.cc sorted by
+    name, then include/zkfl.h (the Makefile's ID_SRCS), SHA-256, first 16 hex digits."""
+    import glob
+    import hashlib
+    names = sorted(os.path.relpath(p, pkg_dir) for ext in ("h", "hip", "cc")
+                   for p in glob.glob(os.path.join(pkg_dir, "csrc", "*." + ext)))
+    h = hashlib.sha256()
+    for n in names + [os.path.join("..", "include", "zkfl.h")]:
+        with open(os.path.join(pkg_dir, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def device_count() -> int:
@@ -225,6 +253,55 @@ class Context:
         out = _buf(128 * n if n else 1)
         check(lib().zkfl_setup_g2_gen_mul(self.h, scalars, n, out))
         return bytes(out)[:128 * n]
+
+    # ceremony primitives (zkfl/ptau.py, zkfl/zkey.py::setup_from_ptau / zkey_contribute)
+    def _scale(self, fn, size, points: bytes, scalars: bytes) -> bytes:
+        n = len(scalars) // 32
+        if len(points) != size * n or len(scalars) != 32 * n:
+            raise ZkflError(-1, f"scale: {len(points)} B of points for {n} scalars")
+        out = _buf(size * n if n else 1)
+        check(fn(self.h, points, scalars, n, out))
+        return bytes(out)[:size * n]
+
+    def g1_scale(self, points: bytes, scalars: bytes) -> bytes:
+        """out[i] = k_i * P_i (mont affine points, std scalars)."""
+        return self._scale(lib().zkfl_setup_g1_scale, 64, points, scalars)
+
+    def g2_scale(self, points: bytes, scalars: bytes) -> bytes:
+        return self._scale(lib().zkfl_setup_g2_scale, 128, points, scalars)
+
+    def _lagrange(self, fn, size, points: bytes, logn: int) -> bytes:
+        if len(points) != size << logn:
+            raise ZkflError(-1, f"lagrange: expected {1 << logn} points")
+        out = _buf(size << logn)
+        check(fn(self.h, points, logn, out))
+        return bytes(out)
+
+    def g1_lagrange(self, points: bytes, logn: int) -> bytes:
+        """Inverse FFT over G1: [tau^i G] (2^logn points) -> [L_j(tau) G]."""
+        return self._lagrange(lib().zkfl_setup_g1_lagrange, 64, points, logn)
+
+    def g2_lagrange(self, points: bytes, logn: int) -> bytes:
+        return self._lagrange(lib().zkfl_setup_g2_lagrange, 128, points, logn)
+
+    def _lincomb(self, fn, size, bases: bytes, rowptr, idx, coefs: bytes) -> bytes:
+        import numpy as np
+        rp = np.ascontiguousarray(rowptr, dtype=np.uint64)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        n_out = len(rp) - 1
+        if len(coefs) != 32 * len(ix) or int(rp[-1]) != len(ix) or len(bases) % size:
+            raise ZkflError(-1, "lincomb: inconsistent term arrays")
+        out = _buf(size * n_out if n_out else 1)
+        check(fn(self.h, bases, len(bases) // size, n_out, rp.ctypes.data_as(C.POINTER(C.c_uint64)),
+                 ix.ctypes.data_as(C.POINTER(C.c_uint32)), coefs, out))
+        return bytes(out)[:size * n_out]
+
+    def g1_lincomb(self, bases: bytes, rowptr, idx, coefs: bytes) -> bytes:
+        """out[r] = sum_{t in row r} coefs[t] * bases[idx[t]] (rowptr: n_out + 1 offsets)."""
+        return self._lincomb(lib().zkfl_setup_g1_lincomb, 64, bases, rowptr, idx, coefs)
+
+    def g2_lincomb(self, bases: bytes, rowptr, idx, coefs: bytes) -> bytes:
+        return self._lincomb(lib().zkfl_setup_g2_lincomb, 128, bases, rowptr, idx, coefs)
 
     # verification (snarkjs groth16 verify)
     def verify(self, vk: bytes, public: bytes, proof: bytes) -> bool:

@@ -17,6 +17,7 @@ in DESIGN.md.  The fixed-base multiplications run on the GPU (libzkfl zkfl_setup
 
 from __future__ import annotations
 
+import hashlib
 import secrets
 import struct
 
@@ -182,6 +183,12 @@ def groth16_setup(builder, ctx, toxic: Toxic | None = None) -> bytes:
     hdr = struct.pack("<I", 32) + Q.to_bytes(32, "little") + struct.pack("<I", 32) + R.to_bytes(32, "little")
     hdr += struct.pack("<III", nv, npub, n)
     hdr += alpha1 + beta1 + beta2 + gamma2 + delta1 + delta2
+    sections = [(1, struct.pack("<I", 1)), (2, hdr), (3, ic), (4, _coef_bytes(builder)), (5, sec_a), (6, sec_b1),
+                (7, sec_b2), (8, sec_c), (9, sec_h)]
+    return _binfile(b"zkey", 1, sections + [(10, _cs_hash(sections) + struct.pack("<I", 0))])
+
+
+def _coef_bytes(builder) -> bytes:
     rows = _coef_table(builder)
     cache = {}
     parts = [struct.pack("<I", len(rows))]
@@ -191,11 +198,133 @@ def groth16_setup(builder, ctx, toxic: Toxic | None = None) -> bytes:
             vb = (v * R2_MONT % R).to_bytes(32, "little")
             cache[v] = vb
         parts.append(struct.pack("<III", m, c, s) + vb)
-    coeffs = b"".join(parts)
-    contrib = bytes(64) + struct.pack("<I", 0)   # csHash placeholder, no MPC contributions
-    sections = [(1, struct.pack("<I", 1)), (2, hdr), (3, ic), (4, coeffs), (5, sec_a), (6, sec_b1),
-                (7, sec_b2), (8, sec_c), (9, sec_h), (10, contrib)]
-    return _binfile(b"zkey", 1, sections)
+    return b"".join(parts)
+
+
+def _cs_hash(sections) -> bytes:
+    """zkey section 10's circuit hash: Blake2b-512 over the delta-independent part of the key (the
+    header up to gamma2, IC, A, B1, B2), so a contribution carries it unchanged.  snarkjs hashes the
+    uncompressed points of the initial key in its own order [ext]; this hash is the framework's (no
+    tool here reads it), computed the same way by every setup path."""
+    h = hashlib.blake2b(digest_size=64)
+    for typ, data in sections:
+        if typ == 2:
+            h.update(data[:468])
+        elif typ in (3, 5, 6, 7):
+            h.update(data)
+    return h.digest()
+
+
+def _sorted_terms(rows_of, n_rows):
+    """[(row, base, coef)] -> (rowptr u64[n_rows + 1], idx u32[nnz], coefs 32 B std each), rows ascending."""
+    import numpy as np
+    rows = np.fromiter((t[0] for t in rows_of), dtype=np.int64, count=len(rows_of))
+    order = np.argsort(rows, kind="stable")
+    rowptr = np.zeros(n_rows + 1, dtype=np.uint64)
+    np.cumsum(np.bincount(rows, minlength=n_rows), out=rowptr[1:])
+    idx = np.fromiter((rows_of[i][1] for i in order), dtype=np.uint32, count=len(rows_of))
+    cache = {}
+
+    def cb(v):
+        b = cache.get(v)
+        if b is None:
+            b = cache[v] = int(v).to_bytes(32, "little")
+        return b
+    coefs = b"".join(cb(rows_of[i][2]) for i in order)
+    return rowptr, idx, coefs
+
+
+def setup_from_ptau(cs, ptau_buf, ctx) -> bytes:
+    """snarkjs `groth16 setup <c>.r1cs <pot>.ptau <c>_0000.zkey` (zkey_new [ext]; the harness's
+    tests/full_system_simulation.mjs:713-716 and tests/test_secureagg.cjs:48-57).  cs: a
+    zkfl.r1cs.Builder or a circom .r1cs read by zkfl.r1cs_file.  Every query point is a sparse
+    combination of the ptau's Lagrange points, computed on the GPU (zkfl_setup_*_lincomb):
+        A_i  = sum_j a_ij L_j(tau) G1 (+ L_{m+k} for public k)     <- section 12
+        B1_i = sum_j b_ij L_j(tau) G1,  B2_i = ... G2               <- sections 12, 13
+        IC_i / C_i = sum_j (a_ij beta + b_ij alpha + c_ij) L_j(tau) G1   <- sections 15, 14, 12
+        H_j  = L^{2n}_{2j+1}(tau) G1                                <- section 12, block 2n
+    with gamma = delta = 1 (the header's gamma2 / delta1 / delta2 are the generators) until a
+    `zkey contribute` rescales delta.  alpha1 / beta1 / beta2 are the ptau's alphaTauG1[0],
+    betaTauG1[0], betaG2."""
+    from . import ptau as pt_mod
+    pt = pt_mod.Ptau(ptau_buf)
+    if not pt.prepared:
+        raise ValueError("Powers of tau is not prepared.")
+    n = domain_size_for(cs)
+    power = n.bit_length() - 1
+    if power > pt.power:
+        raise ValueError(f"circuit too big for this power of tau ceremony. {cs.n_constraints}*2 > 2**{pt.power}")
+    nv, npub, ncons = cs.n_wires, cs.n_public, cs.n_constraints
+    L = pt.lagrange(12, power)
+    L2 = pt.lagrange(13, power)
+    k_bases = L + pt.lagrange(14, power) + pt.lagrange(15, power)   # tau | alpha tau | beta tau
+    h2 = pt.lagrange(12, power + 1)
+    sec_h = b"".join(h2[64 * (2 * j + 1):64 * (2 * j + 2)] for j in range(n))
+    a_terms, b_terms, k_terms = [], [], []
+    for j, (A, B, C) in enumerate(cs.cons):
+        for w, c in A.items():
+            a_terms.append((w, j, c))
+            k_terms.append((w, 2 * n + j, c))          # beta * a_ij
+        for w, c in B.items():
+            b_terms.append((w, j, c))
+            k_terms.append((w, n + j, c))              # alpha * b_ij
+        for w, c in C.items():
+            k_terms.append((w, j, c))
+    for s in range(npub + 1):                          # public-input rows
+        a_terms.append((s, ncons + s, 1))
+        k_terms.append((s, 2 * n + ncons + s, 1))
+    ta, tb, tk = _sorted_terms(a_terms, nv), _sorted_terms(b_terms, nv), _sorted_terms(k_terms, nv)
+    sec_a = ctx.g1_lincomb(L, *ta)
+    sec_b1 = ctx.g1_lincomb(L, *tb)
+    sec_b2 = ctx.g2_lincomb(L2, *tb)
+    k = ctx.g1_lincomb(k_bases, *tk)
+    ic, sec_c = k[:64 * (npub + 1)], k[64 * (npub + 1):]
+    hdr = struct.pack("<I", 32) + Q.to_bytes(32, "little") + struct.pack("<I", 32) + R.to_bytes(32, "little")
+    hdr += struct.pack("<III", nv, npub, n)
+    hdr += (pt.points(4, 0, 1) + pt.points(5, 0, 1) + pt.section(6) + pt_mod.G2_ONE + pt_mod.G1_ONE
+            + pt_mod.G2_ONE)
+    sections = [(1, struct.pack("<I", 1)), (2, hdr), (3, ic), (4, _coef_bytes(cs)), (5, sec_a), (6, sec_b1),
+                (7, sec_b2), (8, sec_c), (9, sec_h)]
+    return _binfile(b"zkey", 1, sections + [(10, _cs_hash(sections) + struct.pack("<I", 0))])
+
+
+def zkey_contribute(buf, ctx, d: int, name: str = "") -> bytes:
+    """snarkjs `zkey contribute <old> <new> --name=<name> -e=<entropy>` with the secret d given
+    (tests/full_system_simulation.mjs:723-726): delta1, delta2 *= d; C and H (sections 8, 9) *= 1/d
+    on the GPU; a contribution record (deltaAfter, the (g1_s, g1_sx, g2_spx) key, transcript, type,
+    params) is appended to section 10 — a dev record, as in zkfl/ptau.py."""
+    from . import ptau as pt_mod
+    d %= R
+    if d == 0:
+        raise ValueError("zkey contribute: zero secret")
+    secs = pt_mod.read_sections(buf, b"zkey")
+    for t in range(1, 11):
+        if t not in secs:
+            raise ValueError(f"zkey: missing section {t}")
+    order = sorted(secs, key=lambda t: secs[t][0])
+    data = {t: bytes(buf[secs[t][0]:secs[t][0] + secs[t][1]]) for t in order}
+    hdr = bytearray(data[2])
+    if len(hdr) < 660:
+        raise ValueError("zkey: header")
+    dinv = pow(d, R - 2, R)
+    hdr[468:532] = ctx.g1_scale(bytes(hdr[468:532]), _scalars([d]))
+    hdr[532:660] = ctx.g2_scale(bytes(hdr[532:660]), _scalars([d]))
+    data[2] = bytes(hdr)
+    for t in (8, 9):
+        npts = len(data[t]) // 64
+        data[t] = ctx.g1_scale(data[t], _scalars([dinv]) * npts) if npts else data[t]
+    mpc = data[10]
+    if len(mpc) < 68:
+        raise ValueError("zkey: section 10")
+    cs_hash, count = mpc[:64], struct.unpack_from("<I", mpc, 64)[0]
+    s = pt_mod.derive_secret(str(d), "s")
+    sp = pt_mod.derive_secret(str(d), "sp")
+    g1 = ctx.g1_gen_mul(_scalars([s, s * d % R]))
+    g2spx = ctx.g2_gen_mul(_scalars([sp * d % R]))
+    transcript = hashlib.blake2b(mpc + hdr[468:532], digest_size=64).digest()
+    record = bytes(hdr[468:532]) + g1 + g2spx + transcript + struct.pack("<I", 0) + pt_mod._params_bytes(name)
+    data[10] = cs_hash + struct.pack("<I", count + 1) + mpc[68:] + record
+    return _binfile(b"zkey", 1, [(t, data[t]) for t in order])
 
 
 def zkey_header(buf: bytes) -> dict:
