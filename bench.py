@@ -69,8 +69,9 @@ CIRCUITS = {
     "M": ("sgd_verified", (128, 4, 7, 1000)),
     "C2": ("sgd_verified", (8, 4, 3, 1000)),
     # circom's compile of the Report's N=128 training circuit has ~283 K constraints (Report.pdf p.6
-    # Table 5) -> domain 2^19; this build's tighter R1CS reaches that count at BATCH = 139
-    "M19": ("sgd_verified", (139, 4, 7, 1000)),
+    # Table 5) -> domain 2^19; this build's tighter R1CS reaches that count (283,407) at BATCH = 124
+    # with a depth-8 dataset tree (a depth-7 tree holds at most 128 samples)
+    "M19": ("sgd_verified", (124, 4, 8, 1000)),
 }
 
 
@@ -181,17 +182,23 @@ def _pmc_traffic(kernel):
     return None, "kernel absent from the PMC summary"
 
 
-def roofline(prof, key, traffic=True):
+def roofline(prof, key, traffic=True, nprof=1):
     """The dominant kernel's roofline."""
     cand = {k: v for k, v in prof.items() if k in IMPL_BYTES_PER_ENTRY and v[1] > 0}
     if not cand:
         return None
     dom = max(cand, key=lambda k: cand[k][0])
     ms_tot, launches, units, med_ms = prof[dom]
-    avg_s = med_ms / 1e3        # median launch: robust to a one-off stalled dispatch
-    if dom == "msm_accumulate_g1":      # launches cycle A, B1, C, H
-        q = (2 * key.n_vars + (key.n_vars - key.n_public - 1) + key.domain_size) / 4
+    # mean launch time: the launches of a proof differ in size (A, B1 and the merged C + H), so the
+    # average query length below goes with the mean duration, not the median
+    avg_s = ms_tot / launches / 1e3
+    if dom == "msm_accumulate_g1":
+        # a proof's G1 launches: A, B1, then C + H as one merged MSM (3 per proof; 4 -- A, B1, C,
+        # H -- in a build without MSM_MERGE_CH): the average query length per launch
+        per_proof = max(1, round(launches / max(1, nprof)))
+        q = (2 * key.n_vars + (key.n_vars - key.n_public - 1) + key.domain_size) / per_proof
     else:
+        per_proof = 1
         q = key.n_vars
     algo = q * ALGO_BYTES_PER_BASE[dom]
     entries = units / launches
@@ -204,8 +211,8 @@ def roofline(prof, key, traffic=True):
             "algorithmic_bytes": round(algo), "query_length": round(q),
             "impl_bytes": round(impl), "impl_GBps": round(impl / avg_s / 1e9, 1) if avg_s > 0 else 0.0,
             "traffic_over_algorithmic": round(traffic / algo, 2) if traffic else None, "traffic_source": traffic_src,
-            "avg_launch_ms": round(avg_s * 1e3, 4), "mean_launch_ms": round(ms_tot / launches, 4),
-            "launches": launches, "entries_per_launch": round(entries),
+            "avg_launch_ms": round(avg_s * 1e3, 4), "median_launch_ms": round(med_ms, 4),
+            "launches": launches, "launches_per_proof": per_proof, "entries_per_launch": round(entries),
             "valu": {"achieved": round(fq, 2), "peak": round(FQMUL_PEAK_GPS, 1), "unit": "G Fq-mul/s",
                      "frac": round(fq / FQMUL_PEAK_GPS, 4),
                      "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (162 mad x 2.2), 29-bit limbs",
@@ -327,8 +334,9 @@ def extra_circuit_leg(ctx, rank, world, circuit, steps, slots, dist):
     rep = {"value": round(world * n / elapsed, 3), "unit": "proofs/s", "proofs": world * n, "verified": ok,
            "workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
            "constraints": b.n_constraints, "domain": key.domain_size, "ms_per_step": round(elapsed / steps * 1e3, 3),
-           "stage_ms_isolated_per_proof": {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()},
-           "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key, traffic=False)}
+           "stage_ms_isolated_per_proof": {k: round(v[0] / max(1, nprof), 3) for k, v in prof.items()},
+           "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key, traffic=False,
+                                   nprof=nprof)}
     key.close()
     return rep
 
@@ -472,14 +480,14 @@ def launch_ranks(n):
 
 def report(args, world, elapsed, n_timed_all, verified_all, prof, nprof, key, config, extra):
     """The bench JSON line (rank 0).  `extra`: roofline / end_to_end / c5 / cpu_baseline fields."""
-    stage_ms = {k: round(v[3] * v[1] / max(1, nprof), 3) for k, v in prof.items()}  # median x launches
+    stage_ms = {k: round(v[0] / max(1, nprof), 3) for k, v in prof.items()}  # summed event time per proof
     line = {
         "metric": METRIC, "value": round(n_timed_all / elapsed, 4), "unit": "proofs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (reference harness seeded client generator)",
         "config": config, "proofs_timed": n_timed_all, "verified": verified_all,
-        "roofline": roofline(prof, key) if key is not None else None,
+        "roofline": roofline(prof, key, nprof=nprof) if key is not None else None,
         "stage_ms_isolated_per_proof": stage_ms,
     }
     line.update(extra)

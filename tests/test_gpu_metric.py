@@ -179,17 +179,17 @@ def test_metric_full_prove_json_batch_reuses_witness_sets(metric):
 
 
 def test_domain_2_19_proof_bit_exact_vs_c_oracle(gpu_ctx):
-    """sgd_verified(139, 4, 7, 1000): > 2^18 constraints (the Report's ~283 K circom count for
+    """sgd_verified(124, 4, 8, 1000): 283,407 constraints (the Report's ~283 K circom count for
     N=128), domain 2^19 -- the 2x NTT / H-MSM size -- proof and all five MSMs equal the C oracle."""
     from oracle import cbaseline
     from zkfl import circuits, clients, native, wprog, zkey
-    b = circuits.build("sgd_verified", 139, 4, 7, 1000)
+    b = circuits.build("sgd_verified", 124, 4, 8, 1000)
     assert b.n_constraints > (1 << 18)
     zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(tau=0x19, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
     key = native.ProvingKey(gpu_ctx, zk)
     wp = native.WitnessProgram(gpu_ctx, wprog.compile_program(b))
-    c = clients.Client(5, 139, 4, 7, clients.JsLcg(12350))
-    wt = wp.compute([wprog.input_bytes(b, c.training_input(139, 1000, 100000000)[0])])[0]
+    c = clients.Client(5, 124, 4, 8, clients.JsLcg(12350))
+    wt = wp.compute([wprog.input_bytes(b, c.training_input(124, 1000, 100000000)[0])])[0]
     assert key.domain_size == 1 << 19
     rs = _le(0xABCDEF) + _le(0xFEDCBA)
     proof, pub = key.prove(wt, rs)

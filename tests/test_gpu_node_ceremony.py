@@ -10,8 +10,9 @@ node/circomlibjs as `circomlibjs`, installed with `npm install --offline` (both 
     finds pot17_final.ptau by the :677-695 search, sets the training circuit up with the :713-738
     strings, and proves; the server side verifies with the :865-868 string;
   * `import { buildPoseidon } from 'circomlibjs'` (:25) with the harness's own vectorHash /
-    gradientCommitment / buildMerkleTree (:139-223) reproduces data/test_input_v5.json's root_G and
-    root_D and the circomlibjs vectors.
+    gradientCommitment / buildMerkleTree (:139-223) reproduces data/test_input_v5.json's root_G, its
+    leaf hashes, root_D through the 8 paths, and the circomlibjs vectors; the GPU tree extension
+    equals the harness's tree.
 ZKFL_DETERMINISTIC_SETUP=1 makes the ceremony secrets a function of the -e entropy strings, so the
 keys can be compared with the known-tau ceremony.
 """
@@ -104,13 +105,25 @@ async function main() {
   const grad = d.gradPos.map((p, i) => BigInt(p) - BigInt(d.gradNeg[i]));
   const gField = grad.map(g => ((g % CONFIG.FIELD_PRIME) + CONFIG.FIELD_PRIME) % CONFIG.FIELD_PRIME);
   const leaves = d.features.map((f, i) => vectorHash([...f, d.labels[i]]));
-  const tree = buildMerkleTree(leaves, d.siblings[0].length);
-  const gpuTree = zkfl.buildMerkleTree(leaves, d.siblings[0].length);
+  // the fixture holds the batch's 8 samples of a larger dataset: root_D through their paths
+  // (getMerkleProof's siblings / pathIndices, :225-238), each hashed with the circomlibjs API
+  const pathRoots = leaves.map((leaf, i) => {
+    let cur = leaf;
+    d.siblings[i].forEach((sib, l) => {
+      cur = d.pathIndices[i][l] === '0' || d.pathIndices[i][l] === 0
+        ? F.toObject(poseidon([cur, BigInt(sib)])) : F.toObject(poseidon([BigInt(sib), cur]));
+    });
+    return cur.toString();
+  });
+  // buildMerkleTree (:198-223) over the 8 leaves, depth 3: the harness's loop vs the GPU tree
+  const tree = buildMerkleTree(leaves, 3);
+  const gpuTree = zkfl.buildMerkleTree(leaves, 3);
   const batch = poseidon.batch([[1, 2], [3, 4]]);
   console.log(JSON.stringify({
     root_G: gradientCommitment(gField, d.client_id, d.round).toString(),
-    root_D: tree[tree.length - 1][0].toString(),
-    gpu_root_D: gpuTree[gpuTree.length - 1][0].toString(),
+    path_roots: pathRoots,
+    tree: tree.map((lv) => lv.map((x) => x.toString())),
+    gpu_tree: gpuTree.map((lv) => lv.map((x) => x.toString())),
     p12: F.toString(poseidon([1, 2])), p0: F.toObject(poseidon([0])).toString(),
     p1: F.toObject(poseidon([1n])).toString(), batch0: batch[0].toString(),
     neg: F.toObject(poseidon([-1, '2'])).toString(), negRef: F.toObject(poseidon([CONFIG.FIELD_PRIME - 1n, 2])).toString(),
@@ -123,7 +136,9 @@ main().catch((e) => { console.error(e); process.exit(1); });
     p = _run(f"node roots.mjs {GOLDEN}", proj)
     r = json.loads(p.stdout.strip().splitlines()[-1])
     d = json.load(open(GOLDEN))
-    assert r["root_G"] == d["root_G"] and r["root_D"] == d["root_D"] == r["gpu_root_D"]
+    assert r["root_G"] == d["root_G"]
+    assert r["path_roots"] == [d["root_D"]] * 8
+    assert r["tree"] == r["gpu_tree"] and len(r["tree"]) == 4 and len(r["tree"][0]) == 8
     assert r["leaf0"] == r["sib"] == r["vh"]                   # level-0 sibling of leaf 1 = leaf 0
     assert r["p12"] == r["batch0"] == "7853200120776062878684798364095072458815029376092732009249414926327459813530"
     assert r["p0"] == "19014214495641488759237505126948346942972912379615652741039992445865937985820"

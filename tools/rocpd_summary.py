@@ -13,12 +13,13 @@
   rocpd_summary.py timeline RUN.db OUT.txt
       concurrency over the timed (throughput) region of a traced bench.py run: fraction of wall time
       with k kernels of each category running, from 10-us samples
-  rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json
+  rocpd_summary.py pmc FETCH.db WRITE.db CALIB.db OUT.json [BUILD_ID]
       per-kernel average FETCH_SIZE / WRITE_SIZE per launch (separate --pmc passes, as
       MI355X_MICROARCH.md §rocprofv3 PMC slots requires), plus the FETCH_SIZE calibration of the
       MSM gather pattern from tools/pmc_calib.hip (CALIB.db: --pmc FETCH_SIZE of pmc_calib):
       factor = known bytes / reported bytes for 64-B (G1) and 128-B (G2) records.
-      bench.py reads OUT.json (profiles/pmc_traffic.json) for the roofline "traffic" field.
+      bench.py reads OUT.json (profiles/pmc_traffic.json) for the roofline "traffic" field, and only
+      when BUILD_ID (the profiled libzkfl.so's zkfl_build_id) equals the library it has loaded.
 """
 import csv
 import json
@@ -48,14 +49,14 @@ def _pmc(db, counter):
     return {r[0]: (r[1], r[2]) for r in rows}  # KiB per launch
 
 
-def pmc(fetch_db, write_db, calib_db, out):
+def pmc(fetch_db, write_db, calib_db, out, build_id=None):
     fetch, write = _pmc(fetch_db, "FETCH_SIZE"), _pmc(write_db, "WRITE_SIZE")
     calib = _pmc(calib_db, "FETCH_SIZE")
     factors = {}
     for rb in (64, 128):
         k = [v for n, v in calib.items() if f"k_gather<{rb}>" in n]
         factors[rb] = (CALIB_LANES * rb) / (k[0][1] * 1024) if k else None
-    res = {"unit": "bytes per launch", "fetch_calibration": {
+    res = {"unit": "bytes per launch", "build_id": build_id, "fetch_calibration": {
         "g1_64B_records": factors[64], "g2_128B_records": factors[128],
         "method": "tools/pmc_calib.hip: 4 Mi lanes each gather one random record from a 4 GiB table; "
                   "factor = known bytes / FETCH_SIZE bytes"}, "kernels": {}}
@@ -83,7 +84,8 @@ def roofline(db, bench_log, out):
     for tag, sym in ROOFLINE_KERNELS.items():
         d = [r[0] for r in c.execute("select end-start from kernels where name like ? order by start",
                                      (f"%{sym}%",)).fetchall()]
-        launches = n if tag == rep["roofline"]["kernel"] else n // 4  # 4 G1 MSMs per G2 MSM
+        per = rep["roofline"].get("launches_per_proof", 4)            # G1 MSM launches per G2 MSM
+        launches = n if tag == rep["roofline"]["kernel"] else n // per
         last = sorted(x / 1e6 for x in d[-launches:])
         if last:
             mid = len(last) // 2
@@ -182,4 +184,4 @@ if __name__ == "__main__":
     elif sys.argv[1] == "roofline":
         roofline(sys.argv[2], sys.argv[3], sys.argv[4])
     else:
-        pmc(*sys.argv[2:6])
+        pmc(*sys.argv[2:7])

@@ -16,37 +16,17 @@
 namespace zkfl {
 namespace {
 
-// k * a (a affine); k: 8 little-endian u32 limbs, standard form
+// k * P for a standard-form scalar (8 little-endian u32 limbs): curve.h's double-and-add, the
+// routine the dev ceremony's k_gen_mul has always used (its limb loop unrolled, so the scalar
+// stays in registers)
 template <class F>
-__device__ XYZZ<F> smul_aff(const Affine<F>& a, const uint32_t k[8]) {
-  XYZZ<F> acc = xyzz_inf<F>();
-  if (aff_is_inf(a)) return acc;
-#pragma unroll 1
-  for (int i = 7; i >= 0; i--) {
-    const uint32_t w = k[i];
-#pragma unroll 1
-    for (int b = 31; b >= 0; b--) {
-      acc = xyzz_dbl<F>(acc);
-      if ((w >> b) & 1u) acc = xyzz_madd<F>(acc, a);
-    }
-  }
-  return acc;
+ZK_DEV XYZZ<F> smul_aff(const Affine<F>& a, const uint32_t k[8]) {
+  return xyzz_scalar_mul<F>(xyzz_from_affine<F>(a), k);
 }
 
 template <class F>
-__device__ XYZZ<F> smul_xyzz(const XYZZ<F>& p, const uint32_t k[8]) {
-  XYZZ<F> acc = xyzz_inf<F>();
-  if (xyzz_is_inf(p)) return acc;
-#pragma unroll 1
-  for (int i = 7; i >= 0; i--) {
-    const uint32_t w = k[i];
-#pragma unroll 1
-    for (int b = 31; b >= 0; b--) {
-      acc = xyzz_dbl<F>(acc);
-      if ((w >> b) & 1u) acc = xyzz_add<F>(acc, p);
-    }
-  }
-  return acc;
+ZK_DEV XYZZ<F> smul_xyzz(const XYZZ<F>& p, const uint32_t k[8]) {
+  return xyzz_scalar_mul<F>(p, k);
 }
 
 template <class F>

@@ -468,7 +468,7 @@ struct ProofSlot {
   MsmTail<FqOps> g1t[4];   // A, B1, C, H: accumulated, finished by one batched tail
   MsmScratch<Fq2Ops> g2s;
   MsmTail<Fq2Ops> g2t;
-  Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs
+  Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs (= h + n: the extra slots follow h)
   Fr* abc = nullptr;  // [3n]
   Fr* abc_head = nullptr;  // [ceil(K / ABC_L)] ABC segmented-sum partials
   Fr* abc_tail = nullptr;
@@ -486,6 +486,9 @@ struct ProofSlot {
 #ifndef ZK_NO_SHARE_B
 #define ZK_NO_SHARE_B 0  // 1: B2 sorts its own digits (A/B builds)
 #endif
+#ifndef MSM_MERGE_CH
+#define MSM_MERGE_CH 1   // 0: C and H as two MSMs with their own sorts and tails (A/B builds)
+#endif
 struct zkfl_key {
   zkfl_ctx* ctx = nullptr;
   uint32_t nVars = 0, nPub = 0, n = 0;
@@ -498,6 +501,11 @@ struct zkfl_key {
   uint32_t cshift = 0;       // packed terms: col | dict index << cshift in cols[]; 0 = wide
   MsmBases<FqOps> bA, bB1, bC, bH;
   MsmBases<Fq2Ops> bB2;
+  // C and H as ONE MSM (MSM_MERGE_CH): pi_C only needs their sum, so one sort and one tail serve
+  // both queries.  Bases: C's (scalars: the private wires) then H's (scalars: h, addressed through
+  // the extra pointer = the slot's h vector, whose extra slots 1, r, s, -rs follow it).  bC / bH
+  // stay for the parity hook (zkfl_debug_prove_parts returns C and H apart).
+  MsmBases<FqOps> bCH;
   bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
@@ -526,7 +534,7 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->extra, s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};
+  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -541,7 +549,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ProofSlot* s = new ProofSlot();
   *out = s;
   const size_t nV = k->nVars, n = k->n;
-  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n});
+  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n, k->bCH.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
   // One stream per slot by default: a slot's proof is a serial chain and throughput comes from
@@ -552,17 +560,17 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_b2, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
-  const size_t caps[4] = {k->bA.n, k->bB1.n, k->bC.n, k->bH.n};
+  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), k->bH.n};
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
   (void)nV;
-  ZK_CHECK(hipMalloc(&s->extra, 4 * 32));
+  ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
+  s->extra = s->h + n;
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
   const size_t abc_chunks = (k->K + ABC_L - 1) / ABC_L + 1;
   ZK_CHECK(hipMalloc(&s->abc_head, abc_chunks * 32));
   ZK_CHECK(hipMalloc(&s->abc_tail, abc_chunks * 32));
-  ZK_CHECK(hipMalloc(&s->h, n * 32));
   ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
   ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32 + 4 * sizeof(GlvScalar)));
@@ -663,6 +671,7 @@ void key_release(zkfl_key* k) {
   msm_bases_free_g1(k->bB1);
   msm_bases_free_g1(k->bC);
   msm_bases_free_g1(k->bH);
+  msm_bases_free_g1(k->bCH);
   msm_bases_free_g2(k->bB2);
   ntt_plan_free(k->ntt);
   void* ptrs[] = {k->rows, k->cols, k->coefs};
@@ -715,6 +724,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
+  // C + H as one MSM into tail 2 (res[2] = C' + H, res[3] = infinity); the parity hook (plain)
+  // keeps them apart
+  const bool merge = MSM_MERGE_CH && !plain && k->bCH.n > 0;
+  const int ntails = merge ? 3 : 4;
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
   const bool share = k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32);
@@ -725,7 +738,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   }
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
-  HIP_TRY(msm_tails_reset_g1(tails, 4, st), "msm reset");
+  HIP_TRY(msm_tails_reset_g1(tails, ntails, st), "msm reset");
   HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   if (share) {
     MsmTail<Fq2Ops>* t2 = &s->g2t;
@@ -742,7 +755,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   } else {
     HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   }
-  HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
+  if (!merge) HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
   int pi = prof->begin("abc", st);
   if (k->K) {
     const uint32_t K = (uint32_t)k->K;
@@ -761,11 +774,17 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
   prof->end(pi, st, 3.0 * (double)n);
   hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
-  HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
-          "msm H");
+  if (merge) {
+    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+            "msm C+H");
+    HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
+  } else {
+    HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
+            "msm H");
+  }
   {
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
-    HIP_TRY(msm_tails_g1(tails, outs, 4, st), "msm tails");
+    HIP_TRY(msm_tails_g1(tails, outs, ntails, st), "msm tails");
   }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (!plain && !(ZK_KNOCKOUT & 1)) {
@@ -1213,6 +1232,35 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
     if (e == hipSuccess) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
     if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, true);
+    if (e == hipSuccess && MSM_MERGE_CH) {
+      // C (private wires -> the witness) then H (h_j -> extra[j], the slot's h vector), then
+      // delta1 with -rs (extra[dom + 3]: the extra slots sit behind h)
+      std::vector<uint8_t> img;
+      std::vector<uint32_t> sidx;
+      img.reserve((nC + dom + 1) * 64);
+      sidx.reserve(nC + dom + 1);
+      for (size_t i = 0; i < nC; i++) {
+        const uint8_t* p = z.secC + i * 64;
+        if (!nonzero(p, 64)) continue;
+        img.insert(img.end(), p, p + 64);
+        sidx.push_back(nPub + 1 + (uint32_t)i);
+      }
+      for (size_t j = 0; j < dom; j++) {
+        const uint8_t* p = z.secH + j * 64;
+        if (!nonzero(p, 64)) continue;
+        img.insert(img.end(), p, p + 64);
+        sidx.push_back(X + (uint32_t)j);
+      }
+      img.insert(img.end(), delta1, delta1 + 64);
+      sidx.push_back(X + dom + 3);
+      e = bases_alloc_any(k->bCH, sidx.size());
+      void* d_img = nullptr;
+      if (e == hipSuccess) e = hipMalloc(&d_img, img.size());
+      if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = bases_set_map_any(k->bCH, d_img, sidx.data(), X, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (d_img) (void)hipFree(d_img);
+    }
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
