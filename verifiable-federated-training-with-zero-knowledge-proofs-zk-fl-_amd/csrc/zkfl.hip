@@ -118,13 +118,16 @@ __global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ 
   const uint32_t cmask = PACKED ? (1u << T.cshift) - 1u : 0xFFFFFFFFu;
   auto coef_of = [&](uint32_t t, uint32_t p) { return PACKED ? coefs[t >> T.cshift] : coefs[p]; };
   // row containing p0: largest r with rp[r] <= p0 (empty rows share their start with the next)
-  uint32_t lo = 0, hi = nrows - 1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (rp[mid] <= p0) lo = mid;
-    else hi = mid - 1;
-  }
-  uint32_t r = lo, rend = rp[r + 1];
+  auto row_of = [&](uint32_t p, uint32_t lo) {
+    uint32_t hi = nrows - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (rp[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  uint32_t r = row_of(p0, 0), rend = rp[r + 1];
   Fr acc = fp_zero<FrP>();
   bool first = true;
   // software-pipelined: term p+1's witness gather (and p+2's term word) are in flight while
@@ -145,10 +148,14 @@ __global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ 
       else abc[r] = acc;
       first = false;
       acc = fp_zero<FrP>();
-      do {
-        r++;
+      // next non-empty row: usually r + 1; a run of empty rows (the domain padding after the
+      // last constraint: ~241 K rows at 2^19) is skipped by binary search, not walked row by row
+      r++;
+      rend = rp[r + 1];
+      if (rend == p) {
+        r = row_of(p, r);
         rend = rp[r + 1];
-      } while (rend == p);
+      }
     }
     acc = fp_add(acc, fp_mul(cf, wv));
     wv = wn;
