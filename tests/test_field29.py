@@ -86,6 +86,23 @@ def test_mul_and_mulsum_at_lazy_extremes(f29):
         assert r < P + prod // (1 << 261) + 1  # Montgomery bound: no final subtraction
 
 
+def test_sqr_normalized_extremes(f29):
+    """f29_sqr (45 + 81 limb products) == f29_mul(a, a) in value and bound, for normalized a up to
+    all-MASK limbs (limb 8 included: the doubled cross products are the column-bound worst case)."""
+    rng = random.Random(2929)
+    vals = [[MASK] * 9, [MASK] * 8 + [0], [0] * 8 + [MASK], [1] + [0] * 8]
+    vals += [lazy_limbs(rng, 1 << 29)[0][:8] + [rng.randrange(1 << 29)] for _ in range(300)]
+    cases = [f"sqr {limbs(0, a)}" for a in vals] + [f"mul {limbs(0, a)} {limbs(0, a)}" for a in vals]
+    got = f29(cases)
+    n = len(vals)
+    for i, a in enumerate(vals):
+        va = sum(x << (29 * k) for k, x in enumerate(a))
+        (r,), (m,) = got[i], got[n + i]
+        assert r % P == va * va * RINV % P
+        assert r < P + va * va // (1 << 261) + 1
+        assert r == m, "square and product differ"
+
+
 def test_below256(f29):
     rng = random.Random(5)
     vals = [rng.randrange(6 * P) for _ in range(300)] + [(1 << 256) - 1, 1 << 256, 6 * P - 1, 0, 2 * P]
@@ -166,6 +183,12 @@ def test_point_formulas(f29):
         bx, by = b[0] * R % P, b[1] * R % P
         cases.append(f"madd {pt_str(pa)} {limbs(bx)} {limbs(by)}")
         want.append(g1_add(a, b))
+        # signed madd (the accumulation kernel's form): + b, and - b given as b with neg = 1
+        cases.append(f"madds {pt_str(pa)} {limbs(bx)} {limbs(by)} 0")
+        want.append(g1_add(a, b))
+        nb = (b[0], (P - b[1]) % P)
+        cases.append(f"madds {pt_str(pa)} {limbs(bx)} {limbs(by)} 1")
+        want.append(g1_add(a, nb))
         pb = to_xyzz(b, rng, not top)
         cases.append(f"add {pt_str(pa)} {pt_str(pb)}")
         want.append(g1_add(a, b))
@@ -187,6 +210,11 @@ def test_madd_chain_stays_in_range(f29):
         lines, exp = [], []
         for j in range(8):
             b = rng.choice(bases)
+            if j % 2:      # the kernel's signed form, random signs (odd accumulators)
+                neg = rng.randrange(2)
+                lines.append(f"madds {pt_str(acc[j])} {limbs(b[0] * R % P)} {limbs(b[1] * R % P)} {neg}")
+                exp.append(g1_add(acc_pts[j], (b[0], (P - b[1]) % P) if neg else b))
+                continue
             lines.append(f"madd {pt_str(acc[j])} {limbs(b[0] * R % P)} {limbs(b[1] * R % P)}")
             exp.append(g1_add(acc_pts[j], b))
         got = f29(lines)
@@ -217,13 +245,18 @@ def to_xyzz2(bn, pt, rng, top):
     out = []
     for v, k in ((X, 5), (Y, 5), (zz, 1), (zzz, 1)):
         for c in (v.c0, v.c1):
-            out.append(c * R % P + (k if top else rng.randrange(k + 1)) * P)
+            m = c * R % P
+            kk = k if top else rng.randrange(k + 1)
+            if top and v is X and m < 6 * P // 10:
+                kk = 6            # X up to 6.6p: the G2 invariant is X < 6.7p (f2_sqr bounds)
+            out.append(m + kk * P)
     return out
 
 
 def from_xyzz2(bn, c):
     F2 = bn.Fq2
-    assert all(v < 6 * P for v in c[:4]) and all(v < 2 * P for v in c[4:]), "range"
+    assert all(v < 67 * P // 10 for v in c[:2]) and all(v < 6 * P for v in c[2:4]) and all(v < 2 * P for v in c[4:]), \
+        "range"
     X, Y, ZZ, ZZZ = (F2(c[2 * i] * RINV, c[2 * i + 1] * RINV) for i in range(4))
     if ZZ.is_zero():
         return None

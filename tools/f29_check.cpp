@@ -1,7 +1,7 @@
 // Host-side driver for the 29-bit-limb field and point formulas (csrc/field29.h), used by
 // tests/test_field29.py: the formulas are __host__ __device__, so their bound analysis is
 // checked on the CPU against Python big integers.  One operation per stdin line:
-//   mul a b | mulsum2 a b c d | below256 a | dbl P | madd P x y | add P Q
+//   mul a b | sqr a | mulsum2 a b c d | below256 a | dbl P | madd P x y | madds P x y neg | add P Q
 //   g2dbl P | g2madd P x y | g2add P Q   (Fq2 values as two elements: c0 c1)
 // field elements as 9 comma-separated decimal limbs, points as X Y ZZ ZZZ; the result is
 // printed the same way.
@@ -58,6 +58,8 @@ struct PairHost {
   static V swap(const V& a) { return {a.l[1], a.l[0]}; }
   static V sel(const V& v1, const V& v0) { return {v0.l[0], v1.l[1]}; }
   static bool is_zero(const V& a) { return f29_is_zero(a.l[0]) && f29_is_zero(a.l[1]); }
+  static bool is_zero3(const V& a) { return f29_is_zero3(a.l[0]) && f29_is_zero3(a.l[1]); }
+  static V mul(const V& a, const V& b) { return {f29_mul(a.l[0], b.l[0]), f29_mul(a.l[1], b.l[1])}; }
   static V add(const V& a, const V& b) { return {f29_add_lazy(a.l[0], b.l[0]), f29_add_lazy(a.l[1], b.l[1])}; }
   static void norm(V& a) {
     f29_norm(a.l[0]);
@@ -115,6 +117,8 @@ int main() {
     if (op == "mul") {
       F29 a = rd(in), b = rd(in);
       wr(f29_mul(a, b));
+    } else if (op == "sqr") {
+      wr(f29_sqr(rd(in)));
     } else if (op == "mulsum2") {
       F29 a = rd(in), b = rd(in), c = rd(in), d = rd(in);
       wr(f29_mulsum2(a, b, c, d));
@@ -128,6 +132,14 @@ int main() {
       a.x = rd(in);
       a.y = rd(in);
       wrp(f29_madd(p, a));
+    } else if (op == "madds") {  // signed madd: base (x, y), minus it when neg != 0
+      XYZZ<FqOps29> p = rdp(in);
+      Affine<FqOps29> a;
+      a.x = rd(in);
+      a.y = rd(in);
+      int neg = 0;
+      in >> neg;
+      wrp(f29_madd_signed(p, a, neg != 0));
     } else if (op == "add") {
       XYZZ<FqOps29> p = rdp(in), q = rdp(in);
       wrp(f29_add(p, q));

@@ -107,6 +107,16 @@ ZK_DEV XYZZ<F> xyzz_dbl_affine(const Affine<F>& a) {
   return r;
 }
 
+template <class F>
+ZK_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a);
+
+// p + a or p - a (the MSM accumulation's signed digit); representations may fold the sign into
+// the formula instead of negating the base (field29.h)
+template <class F>
+ZK_DEV XYZZ<F> xyzz_madd_signed(const XYZZ<F>& p, const Affine<F>& a, bool neg) {
+  return xyzz_madd<F>(p, neg ? aff_neg<F>(a) : a);
+}
+
 // p + a (a affine), madd-2008-s
 template <class F>
 ZK_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {

@@ -152,6 +152,18 @@ ZK_HD bool f29_is_zero(const F29& a) {
   return z == 0 || e == 0;
 }
 
+// normalized a < 3p: a == 0 mod p (0, p or 2p)
+ZK_HD bool f29_is_zero3(const F29& a) {
+  uint32_t z = 0, e = 0, e2 = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    z |= a.v[i];
+    e |= a.v[i] ^ P29::P[i];
+    e2 |= a.v[i] ^ P29::P2[i];
+  }
+  return z == 0 || e == 0 || e2 == 0;
+}
+
 // normalized a < 6p -> normalized, < 2^256 (one conditional subtraction of 2p when a >= 2^256)
 ZK_HD F29 f29_below256(const F29& a) {
   F29 t;
@@ -223,6 +235,45 @@ ZK_HD F29 f29_mul(const F29& a, const F29& b) {
   return f29_mont<1>(x, y);
 }
 
+// Montgomery square a^2 2^-261 of a NORMALIZED a (every limb < 2^29): the cross products
+// a_i a_j (i < j) are taken once against the doubled limb 2 a_i < 2^30, so 45 limb products
+// instead of 81 (+ the 81 of the reduction).  Column bound: <= 4 cross products < 2^59 and one
+// square < 2^58, plus 9 reduction products < 2^58: 18 x 2^58 < 2^63.  Same value, same
+// Montgomery bound (< p + a^2 / 2^261) as f29_mul(a, a).
+ZK_HD F29 f29_sqr(const F29& a) {
+  uint32_t a2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;
+  uint32_t m[9];
+  F29 r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t acc[2] = {carry, 0};
+    int t = 0;
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      const int j = k - i;
+      if (i < j) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)a2[i] * a.v[j];
+      else if (i == j) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)a.v[i] * a.v[i];
+      if (i < k) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)m[i] * P29::P[k - i];
+    }
+    f29_keep(acc[0]);
+    f29_keep(acc[1]);
+    uint64_t c = acc[0] + acc[1];
+    if (k < 9) {
+      m[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
+      c += (uint64_t)m[k] * P29::P[0];
+    } else {
+      r.v[k - 9] = (uint32_t)c & P29::MASK;
+    }
+    carry = c >> 29;
+  }
+  r.v[8] = (uint32_t)carry;
+  return r;
+}
+
 // (a b + c d) 2^-261 with one reduction
 ZK_HD F29 f29_mulsum2(const F29& a, const F29& b, const F29& c, const F29& d) {
   const F29 x[2] = {a, c}, y[2] = {b, d};
@@ -239,7 +290,7 @@ struct FqOps29 {
   static ZK_DEV T one() { return f29_const(P29::ONE); }
   static ZK_DEV bool is_zero(const T& a) { return f29_is_zero(a); }
   static ZK_DEV T mul(const T& a, const T& b) { return f29_mul(a, b); }
-  static ZK_DEV T sqr(const T& a) { return f29_mul(a, a); }
+  static ZK_DEV T sqr(const T& a) { return f29_mul(a, a); }  // a may be lazy here: not f29_sqr
   static ZK_DEV T neg(const T& a) {  // a < p -> p - a in (0, p]
     T r = f29_ksub(P29::K1_1, f29_zero(), a);
     f29_norm(r);
@@ -265,15 +316,16 @@ ZK_HD XYZZ<FqOps29> f29_inf() {
 //   Y3 = M SX + nY W < p + (3.64 * 6.07 + 7 * 1.14) p / 169 < 1.18p; ZZ3, ZZZ3 < 1.03p.
 ZK_HD XYZZ<FqOps29> f29_dbl(const XYZZ<FqOps29>& p) {
   if (f29_is_zero(p.ZZ)) return p;
-  const F29 U = f29_add_lazy(p.Y, p.Y);
-  const F29 V = f29_mul(U, U);
+  F29 U = f29_add_lazy(p.Y, p.Y);
+  f29_norm(U);  // squared below (f29_sqr takes normalized limbs)
+  const F29 V = f29_sqr(U);
   const F29 W = f29_mul(U, V);
   const F29 S = f29_mul(p.X, V);
-  const F29 X2 = f29_mul(p.X, p.X);
+  const F29 X2 = f29_sqr(p.X);
   F29 M = f29_add_lazy(f29_add_lazy(X2, X2), X2);
   f29_norm(M);
   XYZZ<FqOps29> r;
-  r.X = f29_ksub3(P29::K3_2, f29_mul(M, M), S, S, f29_zero());
+  r.X = f29_ksub3(P29::K3_2, f29_sqr(M), S, S, f29_zero());
   f29_norm(r.X);
   const F29 SX = f29_ksub(P29::K5_1, S, r.X);
   const F29 nY = f29_ksub(P29::K7_1, f29_zero(), p.Y);
@@ -298,14 +350,69 @@ ZK_HD XYZZ<FqOps29> f29_madd(const XYZZ<FqOps29>& p, const Affine<FqOps29>& a) {
   F29 R = f29_ksub(P29::K7_1, S2, p.Y);
   f29_norm(P);
   f29_norm(R);
-  const F29 PP = f29_mul(P, P);
+  const F29 PP = f29_sqr(P);
   if (f29_is_zero(PP)) {
-    if (f29_is_zero(f29_mul(R, R))) return f29_dbl({a.x, a.y, f29_const(P29::ONE), f29_const(P29::ONE)});
+    if (f29_is_zero(f29_sqr(R))) return f29_dbl({a.x, a.y, f29_const(P29::ONE), f29_const(P29::ONE)});
     return f29_inf();
   }
   const F29 PPP = f29_mul(P, PP);
   const F29 Q = f29_mul(p.X, PP);
-  const F29 RR = f29_mul(R, R);
+  const F29 RR = f29_sqr(R);
+  XYZZ<FqOps29> r;
+  r.X = f29_ksub3(P29::K4_3, RR, PPP, Q, Q);
+  f29_norm(r.X);
+  const F29 QX = f29_ksub(P29::K6_1, Q, r.X);
+  const F29 nY = f29_ksub(P29::K7_1, f29_zero(), p.Y);
+  r.Y = f29_mulsum2(R, QX, nY, PPP);
+  r.ZZ = f29_mul(p.ZZ, PP);
+  r.ZZZ = f29_mul(p.ZZZ, PPP);
+  return r;
+}
+
+// madd of the base (x, y) or, for neg, of (x, -y) -- the MSM accumulation's signed digit.
+// Instead of negating y (a subtraction, a carry pass and a select per limb) the sign is applied
+// to S2 = y ZZZ1 < 1.03p: t = 2p - S2 for neg (borrowed 2p, lazy, limbs < 2^30), else S2, and
+// R = t + 7p - Y1 < 9.03p (normalized: squared); RR < p + 9.03^2 p / 169 = 1.49p;
+// X3 = RR + 4p - PPP - 2Q < 5.49p; Y3 < p + (9.03 * 7.05 + 7 * 1.07) p / 169 < 1.43p; the rest as
+// f29_madd.  A base at infinity is stored as (0, 0); a canonical base is never p, and y = 0 is
+// no point of the prime-order group, so a plain all-limbs-zero test suffices for it.
+ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29>& a, bool neg) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) z |= a.x.v[i] | a.y.v[i];
+  if (z == 0) return p;
+  if (f29_is_zero(p.ZZ)) {
+    F29 y = a.y;
+    if (neg) {
+      y = f29_ksub(P29::K1_1, f29_zero(), a.y);
+      f29_norm(y);
+    }
+    return {a.x, y, f29_const(P29::ONE), f29_const(P29::ONE)};
+  }
+  const F29 U2 = f29_mul(a.x, p.ZZ);
+  const F29 S2 = f29_mul(a.y, p.ZZZ);
+  F29 t;
+#pragma unroll
+  for (int i = 0; i < 9; i++) t.v[i] = neg ? P29::K2_1[i] - S2.v[i] : S2.v[i];
+  F29 P = f29_ksub(P29::K7_1, U2, p.X);
+  F29 R = f29_ksub(P29::K7_1, t, p.Y);
+  f29_norm(P);
+  f29_norm(R);
+  const F29 PP = f29_sqr(P);
+  if (f29_is_zero(PP)) {
+    if (f29_is_zero(f29_sqr(R))) {
+      F29 y = a.y;
+      if (neg) {
+        y = f29_ksub(P29::K1_1, f29_zero(), a.y);
+        f29_norm(y);
+      }
+      return f29_dbl({a.x, y, f29_const(P29::ONE), f29_const(P29::ONE)});
+    }
+    return f29_inf();
+  }
+  const F29 PPP = f29_mul(P, PP);
+  const F29 Q = f29_mul(p.X, PP);
+  const F29 RR = f29_sqr(R);
   XYZZ<FqOps29> r;
   r.X = f29_ksub3(P29::K4_3, RR, PPP, Q, Q);
   f29_norm(r.X);
@@ -332,8 +439,8 @@ ZK_HD XYZZ<FqOps29> f29_add(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
   F29 R = f29_ksub(P29::K2_1, S2, S1);
   f29_norm(P);
   f29_norm(R);
-  const F29 PP = f29_mul(P, P);
-  const F29 RR = f29_mul(R, R);
+  const F29 PP = f29_sqr(P);
+  const F29 RR = f29_sqr(R);
   if (f29_is_zero(PP)) {
     if (f29_is_zero(RR)) return f29_dbl(p);
     return f29_inf();
@@ -361,9 +468,11 @@ ZK_HD XYZZ<FqOps29> f29_add(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
 // An Fq2 product is one sum of two Fq products per lane with one reduction:
 //   lane 0: a0 b0 + (K - a1) b1,  lane 1: a1 b0 + a0 b1     (f2_mul; a normalized, K > a)
 // so a product of a < A p and b < B p is < p + (A + K) B p / 169 per component; the column bound
-// needs a normalized and b normalized or lazy with limbs < 2^30.  Bounds per formula below, in
-// units of p, for each component; invariant between operations as for G1: X, Y < 6p,
-// ZZ, ZZZ < 2p, normalized.
+// needs a normalized and b normalized or lazy with limbs < 2^30.  A square is ONE product per lane
+// (f2_sqr: (a0 + a1)(a0 + K - a1) and (2 a0) a1) instead of a sum of two, at the price of a looser
+// bound, < p + 2 A (A + K) p / 169.  Bounds per formula below, in units of p, for each component;
+// invariant between operations: X < 6.7p, Y < 6p, ZZ, ZZZ < 2p, normalized (X is looser than
+// G1's 6p: the squares' bound carries into X3).
 // ---------------------------------------------------------------------------
 template <class L>
 struct G2P29 {
@@ -376,6 +485,20 @@ ZK_HD typename L::V f2_mul(const typename L::V& a, const typename L::V& b, const
   const V pa = L::swap(a), pb = L::swap(b);
   const V zero = L::zero();
   return L::mulsum2(a, L::sel(pb, b), L::sel(pa, L::ksub(k, zero, pa)), L::sel(b, pb));
+}
+
+// a^2 over Fq2 (a normalized, a < A p, K >= A p): one Montgomery product per lane
+//   lane 0: (a0 + a1) (a0 + K - a1) = a0^2 - a1^2,   lane 1: (a0 + a0) a1 = 2 a0 a1
+// x = the sum, normalized (limbs < 2^29); y lazy (lane 0: limbs < 2^29 + 2^30) or normalized, so a
+// column holds <= 9 products < 3 x 2^58 + 9 reduction products: < 36 x 2^58.
+// Bound: lane 0 < p + 2 A (A + K) p / 169, lane 1 < p + 2 A^2 p / 169.
+template <class L>
+ZK_HD typename L::V f2_sqr(const typename L::V& a, const uint32_t (&k)[9]) {
+  using V = typename L::V;
+  const V pa = L::swap(a);
+  V x = L::add(pa, L::sel(pa, a));  // lane 0: a1 + a0, lane 1: a0 + a0
+  L::norm(x);
+  return L::mul(x, L::sel(a, L::ksub(k, a, pa)));  // lane 1: a1, lane 0: a0 + K - a1
 }
 
 // A B - Y D over Fq2 (a normalized A < kA, Y < kY; B, D normalized): four products per lane
@@ -398,9 +521,10 @@ ZK_HD G2P29<L> f2_inf() {
 }
 
 // dbl-2008-s-1.  U = 2Y < 12p (normalized); V = U^2 < p + (12 + 13) 12/169 p = 2.78p;
-// W = V U < 1.48p; S = V X < 1.24p; X^2 < 1.46p; M = 3 X^2 < 4.38p (normalized);
-// M^2 < 1.24p; X3 = M^2 + 3p - 2S < 4.24p; SX = S + 5p - X3 < 6.24p (normalized);
-// Y3 = M SX - Y W < p + ((4.38 + 5) 6.24 + (7 + 6) 1.48)/169 p < 1.47p; ZZ3, ZZZ3 < 1.07p.
+// W = V U < 1.48p; S = V X < p + (2.78 + 4) 6.7/169 p = 1.27p; X^2 < p + (6.7 + 7) 6.7/169 p = 1.55p;
+// M = 3 X^2 < 4.65p (normalized); M^2 < 1.27p; X3 = M^2 + 3p - 2S < 4.27p; SX = S + 5p - X3
+// < 6.27p (normalized); Y3 = M SX - Y W < p + ((4.65 + 5) 6.27 + (7 + 6) 1.48)/169 p < 1.47p;
+// ZZ3, ZZZ3 < 1.07p.
 template <class L>
 ZK_HD G2P29<L> f2_dbl(const G2P29<L>& p) {
   using V = typename L::V;
@@ -425,10 +549,12 @@ ZK_HD G2P29<L> f2_dbl(const G2P29<L>& p) {
 }
 
 // madd-2008-s.  x, y <= p (canonical base, y possibly negated); U2, S2 < 1.04p;
-// P = U2 + 7p - X1, R < 8.04p (normalized); PP, R^2 < p + (8.04 + 9) 8.04/169 p = 1.81p;
-// PPP = PP P < 1.18p; Q = PP X1 < 1.14p; X3 = R^2 + 4p - PPP - 2Q < 5.81p;
-// QX = Q + 6p - X3 < 7.14p (normalized); Y3 = R QX - Y1 PPP
-// < p + ((8.04 + 9) 7.14 + (7 + 6) 1.18)/169 p < 1.81p; ZZ3, ZZZ3 < 1.06p.
+// P = U2 + 7p - X1, R < 8.04p (normalized); PP, R^2 (f2_sqr, K = 9p) < p + 2 8.04 17.04/169 p
+// = 2.62p -- a multiple of p below 3p when P == 0, so the zero tests take 0, p and 2p;
+// PPP = PP P < p + (2.62 + 3) 8.04/169 p = 1.27p; Q = PP X1 < p + 5.62 6.7/169 p = 1.23p;
+// X3 = R^2 + 4p - PPP - 2Q < 6.62p (4p > PPP + 2Q = 3.73p); QX = Q + 7p - X3 < 8.23p (normalized);
+// Y3 = R QX - Y1 PPP < p + ((8.04 + 9) 8.23 + (7 + 6) 1.27)/169 p < 1.93p;
+// ZZ3 < p + (2 + 3) 2.62/169 p = 1.08p, ZZZ3 < 1.04p.
 template <class L>
 ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typename L::V& ay) {
   using V = typename L::V;
@@ -440,18 +566,18 @@ ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typenam
   V R = L::ksub(P29::K7_1, S2, p.Y);
   L::norm(P);
   L::norm(R);
-  const V PP = f2_mul<L>(P, P, P29::K9_1);
-  if (L::is_zero(PP)) {
-    if (L::is_zero(f2_mul<L>(R, R, P29::K9_1))) return f2_dbl<L>({ax, ay, L::one(), L::one()});
+  const V PP = f2_sqr<L>(P, P29::K9_1);
+  if (L::is_zero3(PP)) {
+    if (L::is_zero3(f2_sqr<L>(R, P29::K9_1))) return f2_dbl<L>({ax, ay, L::one(), L::one()});
     return f2_inf<L>();
   }
-  const V PPP = f2_mul<L>(PP, P, P29::K2_1);
-  const V Q = f2_mul<L>(PP, p.X, P29::K2_1);
-  const V RR = f2_mul<L>(R, R, P29::K9_1);
+  const V PPP = f2_mul<L>(PP, P, P29::K3_1);
+  const V Q = f2_mul<L>(PP, p.X, P29::K3_1);
+  const V RR = f2_sqr<L>(R, P29::K9_1);
   G2P29<L> r;
   r.X = L::ksub3(P29::K4_3, RR, PPP, Q, Q);
   L::norm(r.X);
-  V QX = L::ksub(P29::K6_1, Q, r.X);
+  V QX = L::ksub(P29::K7_1, Q, r.X);
   L::norm(QX);
   r.Y = f2_mulsub<L>(R, QX, P29::K9_1, p.Y, PPP, P29::K7_1);
   r.ZZ = f2_mul<L>(p.ZZ, PP, P29::K3_1);
@@ -459,11 +585,11 @@ ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typenam
   return r;
 }
 
-// add-2008-s.  U1, U2, S1, S2 = (ZZ or ZZZ) (X or Y) < p + (2 + 3) 6/169 p = 1.18p;
-// P = U2 + 2p - U1, R < 3.18p (normalized); PP, R^2 < 1.14p; PPP < 1.07p; Q < 1.04p;
-// X3 = R^2 + 4p - PPP - 2Q < 5.14p; QX < 7.04p (normalized);
-// Y3 = R QX - S1 PPP < p + ((3.18 + 4) 7.04 + (2 + 1.18) 1.07)/169 p < 1.32p;
-// ZZ1 ZZ2 < 1.06p, ZZ3 = (ZZ1 ZZ2) PP < 1.04p (ZZZ likewise).
+// add-2008-s.  U1, U2, S1, S2 = (ZZ or ZZZ) (X or Y) < p + (2 + 3) 6.7/169 p = 1.2p;
+// P = U2 + 2p - U1, R < 3.2p (normalized); PP, R^2 (f2_sqr, K = 4p) < p + 2 3.2 7.2/169 p
+// = 1.28p; PPP < p + 3.28 3.2/169 p = 1.07p; Q < 1.03p; X3 = R^2 + 4p - PPP - 2Q < 5.28p;
+// QX < 7.03p (normalized); Y3 = R QX - S1 PPP < p + ((3.2 + 4) 7.03 + (2 + 1.2) 1.07)/169 p < 1.32p;
+// ZZ1 ZZ2 < 1.06p, ZZ3 = (ZZ1 ZZ2) PP < 1.03p (ZZZ likewise).
 template <class L>
 ZK_HD G2P29<L> f2_add(const G2P29<L>& p, const G2P29<L>& q) {
   using V = typename L::V;
@@ -477,14 +603,14 @@ ZK_HD G2P29<L> f2_add(const G2P29<L>& p, const G2P29<L>& q) {
   V R = L::ksub(P29::K2_1, S2, S1);
   L::norm(P);
   L::norm(R);
-  const V PP = f2_mul<L>(P, P, P29::K4_1);
+  const V PP = f2_sqr<L>(P, P29::K4_1);
   if (L::is_zero(PP)) {
-    if (L::is_zero(f2_mul<L>(R, R, P29::K4_1))) return f2_dbl<L>(p);
+    if (L::is_zero(f2_sqr<L>(R, P29::K4_1))) return f2_dbl<L>(p);
     return f2_inf<L>();
   }
   const V PPP = f2_mul<L>(PP, P, P29::K2_1);
   const V Q = f2_mul<L>(PP, U1, P29::K2_1);
-  const V RR = f2_mul<L>(R, R, P29::K4_1);
+  const V RR = f2_sqr<L>(R, P29::K4_1);
   G2P29<L> r;
   r.X = L::ksub3(P29::K4_3, RR, PPP, Q, Q);
   L::norm(r.X);
@@ -518,6 +644,11 @@ struct Pair29Dev {
     const uint32_t z = f29_is_zero(a) ? 1u : 0u;
     return (z & pair_swap_u32(z)) != 0;
   }
+  static ZK_DEV bool is_zero3(const V& a) {
+    const uint32_t z = f29_is_zero3(a) ? 1u : 0u;
+    return (z & pair_swap_u32(z)) != 0;
+  }
+  static ZK_DEV V mul(const V& a, const V& b) { return f29_mul(a, b); }
   static ZK_DEV V add(const V& a, const V& b) { return f29_add_lazy(a, b); }
   static ZK_DEV void norm(V& a) { f29_norm(a); }
   static ZK_DEV V ksub(const uint32_t (&k)[9], const V& a, const V& b) { return f29_ksub(k, a, b); }
@@ -546,6 +677,16 @@ template <>
 ZK_DEV XYZZ<FqOps29> xyzz_madd<FqOps29>(const XYZZ<FqOps29>& p, const Affine<FqOps29>& a) {
   return f29_madd(p, a);
 }
+// F29_SIGNED_MADD 0: negate the base and use f29_madd (A/B of the sign folding)
+#ifndef F29_SIGNED_MADD
+#define F29_SIGNED_MADD 1
+#endif
+#if F29_SIGNED_MADD
+template <>
+ZK_DEV XYZZ<FqOps29> xyzz_madd_signed<FqOps29>(const XYZZ<FqOps29>& p, const Affine<FqOps29>& a, bool neg) {
+  return f29_madd_signed(p, a, neg);
+}
+#endif
 template <>
 ZK_DEV XYZZ<FqOps29> xyzz_add<FqOps29>(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
   return f29_add(p, q);

@@ -614,7 +614,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
       k2 = keys[p + 2];
       v2 = vals[p + 2];
     }
-    acc = xyzz_madd<F>(acc, (v0 & 0x80000000u) ? aff_neg<F>(a) : a);
+    acc = xyzz_madd_signed<F>(acc, a, (v0 & 0x80000000u) != 0);
     const bool last = p + 1 == p1;
     if (last || k1 != cur) {
       const bool open_left = first_run && p0 > 0 && keys[p0 - 1] == cur;
@@ -940,7 +940,8 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
   hipLaunchKernelGGL(k_msm_bin_count, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx, b.extra_start,
                      b.n, per_blk, cnt);
   hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
-  if (!(ZK_KNOCKOUT & 2)) {
+  if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
+    pl.ko_sorted = 1;
     hipLaunchKernelGGL(k_msm_bin_scatter, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
                        b.extra_start, b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
     hipLaunchKernelGGL(k_msm_bin_sort, dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st, bin_start, pl.keys_in, pl.vals_in,

@@ -86,6 +86,7 @@ struct MsmScratch {
   uint32_t* vals_out = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  int ko_sorted = 0;             // sort knock-out builds only: this scratch holds a sort already
 };
 
 // Per MSM of a proof: what the accumulation leaves for the tail (stitching + reduction), so the

@@ -200,7 +200,13 @@ __global__ void __launch_bounds__(256) k_abc_rows(const uint32_t* __restrict__ r
 __global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h) {
   size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
+#if ZK_KNOCKOUT & 4
+  // NTT knock-out (timing only): a*b - c vanishes on the domain, so without the coset shift h would
+  // be zero and the H MSM would lose its digits too; a*b + c keeps h a full-size scalar vector
+  Fr v = fp_add(fp_mul(abc[j], abc[n + j]), abc[2 * n + j]);
+#else
   Fr v = fp_sub(fp_mul(abc[j], abc[n + j]), abc[2 * n + j]);
+#endif
   h[j] = fp_from_mont(v);
 }
 
@@ -472,6 +478,9 @@ struct ProofSlot {
   hipStream_t st_main = nullptr, st_g2 = nullptr;
   hipEvent_t ev_ready = nullptr, ev_b2 = nullptr, ev_done = nullptr;
   MsmScratch<FqOps> g1s;   // digit/sort scratch shared by the four G1 MSMs
+#if ZK_KNOCKOUT & 2
+  MsmScratch<FqOps> g1s_ko[3];  // sort knock-out (timing only): A, B, C+H keep their first sort
+#endif
   MsmTail<FqOps> g1t[4];   // A, B1, C, H: accumulated, finished by one batched tail
   MsmScratch<Fq2Ops> g2s;
   MsmTail<Fq2Ops> g2t;
@@ -538,6 +547,9 @@ void slot_release(ProofSlot* s) {
   for (hipStream_t st : {s->st_main, s->st_g2})
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s);
+#if ZK_KNOCKOUT & 2
+  for (MsmScratch<FqOps>& x : s->g1s_ko) msm_scratch_free_g1(x);
+#endif
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
@@ -567,6 +579,13 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_b2, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
+#if ZK_KNOCKOUT & 2
+  for (MsmScratch<FqOps>& x : s->g1s_ko) {  // zeroed: an index past a stale sort is base 0
+    ZK_CHECK(msm_scratch_alloc_g1(x, cap1, st));
+    ZK_CHECK(hipMemsetAsync(x.keys_out, 0, cap1 * MSM_W * sizeof(uint16_t), st));
+    ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * MSM_W * sizeof(uint32_t), st));
+  }
+#endif
   const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), k->bH.n};
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
@@ -746,21 +765,26 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   }
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   HIP_TRY(msm_tails_reset_g1(tails, ntails, st), "msm reset");
-  HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+#if ZK_KNOCKOUT & 2
+  MsmScratch<FqOps>&sA = s->g1s_ko[0], &sB = s->g1s_ko[1], &sCH = s->g1s_ko[2];
+#else
+  MsmScratch<FqOps>&sA = s->g1s, &sB = s->g1s, &sCH = s->g1s;
+#endif
+  HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   if (share) {
     MsmTail<Fq2Ops>* t2 = &s->g2t;
     G2P* o2 = s->resB2;
     HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
-    HIP_TRY(msm_sort_g1(k->bB1, s->g1s, s->g1t[1].nnz, W, E, st), "msm B1 sort");
-    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s.keys_out, s->g1s.vals_out, s->g1t[1], st, prof,
+    HIP_TRY(msm_sort_g1(k->bB1, sB, s->g1t[1].nnz, W, E, st), "msm B1 sort");
+    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, sB.keys_out, sB.vals_out, s->g1t[1], st, prof,
                                      "msm_accumulate_g1"), "msm B1");
     HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
-    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s.keys_out, s->g1s.vals_out, s->g2t, st, prof,
+    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, sB.keys_out, sB.vals_out, s->g2t, st, prof,
                                      "msm_accumulate_g2"), "msm B2");
     HIP_TRY(msm_tails_g2(&t2, &o2, 1, st), "msm B2 tail");
     HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
   } else {
-    HIP_TRY(msm_accumulate_g1(k->bB1, s->g1s, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
+    HIP_TRY(msm_accumulate_g1(k->bB1, sB, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   }
   if (!merge) HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
   int pi = prof->begin("abc", st);
@@ -782,7 +806,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   prof->end(pi, st, 3.0 * (double)n);
   hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
   if (merge) {
-    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+    HIP_TRY(msm_accumulate_g1(k->bCH, sCH, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
     HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
   } else {
