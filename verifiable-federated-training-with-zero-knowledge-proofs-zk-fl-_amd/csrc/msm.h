@@ -51,6 +51,10 @@ namespace zkfl {
 #ifndef MSM_G2_WAVES
 #define MSM_G2_WAVES 2
 #endif
+// minimum waves per SIMD of the batch-affine apply/accumulate kernel (msm_affine.h)
+#ifndef MSM_G1_AFF_WAVES
+#define MSM_G1_AFF_WAVES 3
+#endif
 // 1: the next entry's base is loaded while the current one is added (one affine point of
 // registers); 0: loaded after it, latency hidden by the other waves only.  Without it G1 at 4
 // waves/SIMD spills 3 VGPRs instead of 19 (1.71 -> 1.65 ms per proof) and G2 fits 3 waves/SIMD
@@ -637,6 +641,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
 }
 
+}  // namespace zkfl
+#include "msm_affine.h"
+namespace zkfl {
+
 // Item count of stitching level `level` (>= 1), derived on the device from nnz.
 template <class S>
 ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
@@ -860,6 +868,8 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
   s.sort_tmp_bytes = (MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_HB + 1) * sizeof(uint32_t);
 #endif
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
+  if constexpr (std::is_same<F, FqOps>::value)
+    if (MSM_G1_AFFINE) ZK_CHECK(msm_aff_alloc(s.aff, cap));
   return hipSuccess;
 }
 
@@ -868,6 +878,7 @@ void msm_scratch_free(MsmScratch<F>& s) {
   void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  msm_aff_free(s.aff);
   s = MsmScratch<F>();
 }
 
@@ -976,7 +987,14 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
-  if (!((ZK_KNOCKOUT & 64) && LN == 1))
+  bool done = false;
+  if constexpr (std::is_same<F, FqOps>::value) {
+    if (MSM_G1_AFFINE && t.aff && t.aff->lanes && !(ZK_KNOCKOUT & 64)) {  // batch-affine rounds
+      ZK_CHECK(msm_aff_accumulate<MSM_G1_AFF_WAVES>(b, keys, vals, t, *t.aff, st));
+      done = true;
+    }
+  }
+  if (!done && !((ZK_KNOCKOUT & 64) && LN == 1))
     hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, keys, vals,
                        b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
@@ -991,6 +1009,7 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
                           const uint32_t* d_extra, hipStream_t st, Profiler* prof = nullptr,
                           const char* tag = nullptr) {
   ZK_CHECK(msm_sort(b, pl, t.nnz, d_scalars, d_extra, st));
+  if (pl.aff.lanes) t.aff = &pl.aff;  // G1: accumulate through the batch-affine rounds
   return msm_accumulate_sorted(b, pl.keys_out, pl.vals_out, t, st, prof, tag);
 }
 

@@ -38,8 +38,19 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef MSM_SORT_BIN_THREADS
 #define MSM_SORT_BIN_THREADS 1024
 #endif
+// 1: batch-affine rounds in front of the G1 accumulation (msm_affine.h, A/B builds); 0 (default):
+// XYZZ only.  Measured on MI355X: correct (50 GPU parity tests, metric-size proofs equal the C
+// oracle) but 347 vs 421 proofs/s -- 2,818 VALU instructions per entry against 2,509 for the XYZZ
+// kernel (profiles/r03_affine_v2_kernels_counters.txt)
+#ifndef MSM_G1_AFFINE
+#define MSM_G1_AFFINE 0
+#endif
 #ifndef MSM_G1_L
+#if MSM_G1_AFFINE
+#define MSM_G1_L 32
+#else
 #define MSM_G1_L 16
+#endif
 #endif
 #ifndef MSM_STITCH_SG
 #define MSM_STITCH_SG 8
@@ -75,6 +86,21 @@ struct MsmBases {
   uint32_t extra_start = 0xFFFFFFFFu;
 };
 
+// Device scratch of the batch-affine rounds (msm_affine.h), shared by the G1 MSMs a slot runs one
+// after another.
+struct MsmAffScratch {
+  size_t lanes = 0, wgs = 0;
+  uint32_t* pref = nullptr;      // [2][MSM_L / 2][9][lanes] exclusive prefix products, rounds 1 and 2
+  uint32_t* tree = nullptr;      // [wgs][512][9] workgroup product heaps (node 1 = root, leaves 256..511)
+  uint32_t* wgprod = nullptr;    // [wgs][9]
+  uint32_t* wginv = nullptr;     // [wgs][9]
+  Affine<FqOps>* pts[1] = {nullptr};  // [MSM_L / 2][lanes] round-1 sums
+  uint16_t* key1 = nullptr;      // [MSM_L][lanes] item list after round 1 (descending positions)
+  uint32_t* ref1 = nullptr;      // [MSM_L][lanes]
+  uint8_t* cnt1 = nullptr;       // [lanes]
+  uint32_t* mask2 = nullptr;     // [lanes] round-2 pairing bits (pair i = items 2i, 2i + 1)
+};
+
 // Mutable, per in-flight proof (one stream at a time): digit/sort scratch shared by the MSMs a
 // slot runs one after another.
 template <class F>
@@ -87,6 +113,7 @@ struct MsmScratch {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int ko_sorted = 0;             // sort knock-out builds only: this scratch holds a sort already
+  MsmAffScratch aff;             // G1 with MSM_G1_AFFINE: the batch-affine rounds' scratch
 };
 
 // Per MSM of a proof: what the accumulation leaves for the tail (stitching + reduction), so the
@@ -102,6 +129,7 @@ struct MsmTail {
   XYZZ<F>* red_a = nullptr;     // weighted-reduction block outputs
   XYZZ<F>* red_s = nullptr;
   uint32_t* nnz = nullptr;      // number of non-zero digits of the last run (device)
+  const MsmAffScratch* aff = nullptr;  // G1: batch-affine scratch to accumulate with (not owned)
 };
 
 constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs of a proof)
