@@ -63,6 +63,10 @@ FQMUL_PEAK_GPS_32 = 1024 * 32 * 2.4 / (128 * 2.2 + 128 * 1.8)
 KERNEL_SYMBOL = {"msm_accumulate_g1": "k_msm_accumulate<zkfl::FqOps",   # FqOps29 (G1 compute type)
                  "msm_accumulate_g2": "k_msm_accumulate<zkfl::Fq2"}     # Fq2PairOps
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# SQ / GRBM counters of the shipped kernels (tools/sq_r03.sh): the effective clock of the G1
+# accumulation under load (GRBM_GUI_ACTIVE / 8 / duration) prices the VALU ceiling at the clock the
+# chip actually holds (DVFS), beside the 2.4 GHz figure
+SQ_COUNTERS = os.path.join(ROOT, "profiles", "sq_counters.json")
 PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "assemble", "prove")
 
 CIRCUITS = {
@@ -182,6 +186,22 @@ def _pmc_traffic(kernel):
     return None, "kernel absent from the PMC summary"
 
 
+def _measured_clock(kernel):
+    """(GHz, provenance) of `kernel`'s effective clock from the committed SQ/GRBM counter summary."""
+    from zkfl import native
+    try:
+        with open(SQ_COUNTERS) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, "no counter summary (profiles/sq_counters.json)"
+    for name, v in d.get("kernels", {}).items():
+        if KERNEL_SYMBOL[kernel].replace("zkfl::", "") in name.replace("zkfl::", "") and v.get("clock_GHz"):
+            same = d.get("build_id") == native.build_id()
+            return v["clock_GHz"], (f"profiles/sq_counters.json ({'this build' if same else 'build ' + str(d.get('build_id'))}"
+                                    f", single-slot PMC run: GRBM_GUI_ACTIVE / 8 / kernel duration)")
+    return None, "kernel absent from the counter summary"
+
+
 def roofline(prof, key, traffic=True, nprof=1):
     """The dominant kernel's roofline."""
     cand = {k: v for k, v in prof.items() if k in IMPL_BYTES_PER_ENTRY and v[1] > 0}
@@ -206,6 +226,8 @@ def roofline(prof, key, traffic=True, nprof=1):
     traffic, traffic_src = _pmc_traffic(dom) if traffic else (None, "not collected for this leg")
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
+    clk, clk_src = _measured_clock(dom) if traffic else (None, "not collected for this leg")
+    peak_clk = FQMUL_PEAK_GPS * clk / 2.4 if clk else None
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes": round(algo), "query_length": round(q),
@@ -216,7 +238,10 @@ def roofline(prof, key, traffic=True, nprof=1):
             "valu": {"achieved": round(fq, 2), "peak": round(FQMUL_PEAK_GPS, 1), "unit": "G Fq-mul/s",
                      "frac": round(fq / FQMUL_PEAK_GPS, 4),
                      "peak_basis": "ISA issue rates: 1024 SIMD x 32 lanes x 2.4 GHz / (162 mad x 2.2), 29-bit limbs",
-                     "peak_32bit_limbs": round(FQMUL_PEAK_GPS_32, 1)}}
+                     "peak_32bit_limbs": round(FQMUL_PEAK_GPS_32, 1),
+                     "measured_clock_GHz": clk, "peak_at_measured_clock": round(peak_clk, 1) if peak_clk else None,
+                     "frac_at_measured_clock": round(fq / peak_clk, 4) if peak_clk else None,
+                     "clock_source": clk_src}}
 
 
 def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):

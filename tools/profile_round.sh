@@ -18,4 +18,7 @@ python3 "$R/tools/rocpd_summary.py" kernels "$OUT/ks/run_results.db" "$OUT/kerne
 python3 "$R/tools/rocpd_summary.py" roofline "$OUT/ks/run_results.db" "$OUT/bench_ks.log" "$OUT/roofline_pass.json"
 BID=$(cd "$R" && python3 -c "import sys; sys.path.insert(0, 'verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd'); from zkfl import native; print(native.build_id())")
 python3 "$R/tools/rocpd_summary.py" pmc "$OUT/fetch/run_results.db" "$OUT/write/run_results.db" "$OUT/calib/run_results.db" "$OUT/pmc_traffic.json" "$BID"
+bash "$R/tools/sq_r03.sh" > "$OUT/sq.log" 2>&1
+cp "$R/gpurun_out/sq3/sq_r03.json" "$OUT/sq_counters.json"
+cp "$R/gpurun_out/sq3/sq_r03.txt" "$OUT/sq_counters.txt"
 echo "profiles written to $OUT"
