@@ -587,8 +587,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     v1 = vals[p0 + 1];
   }
 #if MSM_LDS_PF
-  // lane l's piece q of buffer b lands at pf[b][q][l] (an LDS-DMA writes base + lane x 16 B)
-  __shared__ uint4 pf[2][4][64];
+  // lane l's piece q of buffer b lands at pf[b][q][l] (an LDS-DMA writes base + lane x 16 B).  A
+  // native 4 x u32 vector type: with HIP's uint4 struct the reads below were lowered to 32
+  // ds_read_u16 plus ~100 byte-reassembly instructions per entry (gfx950, ROCm 7.2)
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  __shared__ v4u pf[2][4][64];
   const uint32_t ln = threadIdx.x;
   auto fetch = [&](uint32_t idx, int b) {
 #pragma unroll
@@ -606,7 +609,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int b = it++ & 1;
     uint4 u[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) u[q] = pf[b][q][ln];  // the compiler waits for the DMA (vmcnt)
+    for (int q = 0; q < 4; q++) {  // ds_read_b128; the compiler waits for the DMA (vmcnt)
+      const v4u x = pf[b][q][ln];
+      u[q] = make_uint4(x.x, x.y, x.z, x.w);
+    }
     const Affine<F> a = IO::from_pieces(u);
     if (p + 1 < p1) fetch(v1 & 0x7FFFFFFFu, b ^ 1);
 #else
