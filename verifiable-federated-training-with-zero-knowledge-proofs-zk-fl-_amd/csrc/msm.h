@@ -607,9 +607,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   for (uint32_t p = (uint32_t)p0; p < p1; p++) {
 #if MSM_LDS_PF
     const int b = it++ & 1;
+    // the LDS-DMA of this buffer must have landed: with the native vector type the compiler no
+    // longer connects these reads to the global_load_lds writes and dropped the vmcnt wait on the
+    // first iteration (wrong first base, found by the GPU proof tests) -- so wait explicitly
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 u[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {  // ds_read_b128; the compiler waits for the DMA (vmcnt)
+    for (int q = 0; q < 4; q++) {  // ds_read_b128
       const v4u x = pf[b][q][ln];
       u[q] = make_uint4(x.x, x.y, x.z, x.w);
     }

@@ -12,7 +12,7 @@ import os
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # ZKFL_LIB: an alternative build of the library (A/B experiments); default the in-tree one
-LIB_PATH = os.environ.get("ZKFL_LIB") or os.path.join(_PKG_DIR, "libzkfl.so")
+LIB_PATH = os.path.abspath(os.environ["ZKFL_LIB"]) if os.environ.get("ZKFL_LIB") else os.path.join(_PKG_DIR, "libzkfl.so")
 
 ZKFL_OK = 0
 ERRORS = {
