@@ -223,10 +223,11 @@ def roofline(prof, key, traffic=True, nprof=1):
     algo = q * ALGO_BYTES_PER_BASE[dom]
     entries = units / launches
     impl = entries * IMPL_BYTES_PER_ENTRY[dom]
-    traffic, traffic_src = _pmc_traffic(dom) if traffic else (None, "not collected for this leg")
+    collect = traffic
+    traffic, traffic_src = _pmc_traffic(dom) if collect else (None, "not collected for this leg")
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
-    clk, clk_src = _measured_clock(dom) if traffic else (None, "not collected for this leg")
+    clk, clk_src = _measured_clock(dom) if collect else (None, "not collected for this leg")
     peak_clk = FQMUL_PEAK_GPS * clk / 2.4 if clk else None
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
