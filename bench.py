@@ -371,6 +371,61 @@ POS_RP = (56, 57, 56, 60, 60, 63, 64, 63, 60, 66, 60, 65, 70, 60, 64, 68)     # 
 MAC_PEAK_PER_S = 1024 * 32 * 2.4e9 / (2.2 + 1.8)   # v_mad_u64_u32 + v_addc pairs/s (ISA issue rates)
 
 
+def split_leg(ctx, rank, world, zk, wts, full_key, dist, n=8, warm=2):
+    """One proof split over ALL ranks (optional row; zkfl/split.py): every rank loads
+    shard `rank` of the key, proves its share of each proof's MSMs, the parts are all-gathered and
+    rank 0 assembles.  Proofs are issued one at a time, so this is LATENCY: ms per proof from
+    rank 0's (r, s) broadcast to its assembled proof, against rank 0's unsplit proof on one GPU
+    (same key, one proof in flight).  Every split proof is GPU-verified and equals the unsplit proof
+    of the same (r, s)."""
+    from zkfl import native, split
+    key = native.ProvingKey(ctx, zk, shard=rank, n_shards=world)
+    ws = [key.upload(w) for w in wts[:2]]
+    grp = dist.group.WORLD if dist is not None else None
+    lat, proofs = [], []
+    rs_all = draw_rs(warm + n)  # read on rank 0 only (split_prove broadcasts the root's)
+    for i in range(warm + n):
+        _barrier(ctx, dist)
+        t0 = time.perf_counter()
+        out = split.split_prove(lambda r: key.prove_part_batch([ws[i % len(ws)]], r),
+                                lambda parts, k, r: ctx.assemble(parts, k, r), 1, rs_all[64 * i:64 * i + 64], grp)
+        t1 = time.perf_counter()
+        if i >= warm and rank == 0:
+            lat.append((t1 - t0) * 1e3)
+            proofs.append(out[0])
+    for w in ws:
+        w.close()
+    key.close()
+    res = None
+    if rank == 0:
+        # the unsplit baseline: same witnesses, one proof in flight on the full key
+        fws = [full_key.upload(w) for w in wts[:2]]
+        one, same = [], 0
+        for i in range(warm + n):
+            t0 = time.perf_counter()
+            p = full_key.prove_batch([fws[i % 2]], rs_all[64 * i:64 * i + 64])
+            if i >= warm:
+                one.append((time.perf_counter() - t0) * 1e3)
+                same += p[0] == proofs[i - warm]
+        for w in fws:
+            w.close()
+        pubs = [w[76 + 32:76 + 32 * (1 + full_key.n_public)] for w in wts[:2]]
+        verified = verify_all(ctx, zk, proofs, lambda i: pubs[(i + warm) % 2])
+        lat.sort()
+        one.sort()
+        res = {"gpus": world, "proofs": n, "verified": verified, "equal_to_unsplit": same,
+               "ms_per_proof_median": round(lat[n // 2], 3),
+               "ms_per_proof_min": round(lat[0], 3), "single_gpu_ms_median": round(one[n // 2], 3),
+               "speedup": round(one[n // 2] / lat[n // 2], 3),
+               "path": "shard k of G: base i of each query with i % G == k (zkfl_zkey_load_shard) -> ABC + NTT "
+                       "(whole) + this shard's MSMs -> 384 B part -> all_gather (gloo) -> rank 0: parts summed "
+                       "+ assembly on the GPU (zkfl_groth16_assemble)",
+               "exchange_bytes_per_rank": 384}
+        if verified != n or same != n:
+            raise SystemExit(f"[bench] split proofs: {verified}/{n} verify, {same}/{n} equal the unsplit proof")
+    return res
+
+
 def pos_macs(t):
     """Multiply-add pairs of one csrc/poseidon.h permutation of width t: S-boxes are 3 Montgomery
     products (128 pairs each); an MDS row is groups of <= 5 products with one reduction (64 per
@@ -536,6 +591,8 @@ def main():
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     ap.add_argument("--extra-circuit", default="M19", help="second training-circuit size leg ('' or none: skip)")
     ap.add_argument("--extra-steps", type=int, default=4, help="timed steps of the extra-circuit leg")
+    ap.add_argument("--split-proofs", type=int, default=8,
+                    help="split-proof leg: proofs, one at a time, each split over all ranks (0: skip)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -611,6 +668,10 @@ def main():
         e2e = end_to_end_leg(key, wp, wprog.compile_program(b), [json.dumps(x) for x in input_objs], args.slots,
                              args.e2e_steps, ctx, dist, zk, pubs)
         log(f"[bench r{rank}] end to end: {e2e}")
+    split_res = None
+    if args.split_proofs:
+        split_res = split_leg(ctx, rank, world, zk, wts, key, dist, args.split_proofs)
+        log(f"[bench r{rank}] split proof: {split_res}")
     for r_ in res:
         r_.close()
     wp.close()
@@ -648,7 +709,7 @@ def main():
                       {"n_gpus": devices_used, "ranks": world, "build_id": build_id,
                        "build_matches_sources": build_id == source_id, "oracle_match": oracle_match,
                        "end_to_end": e2e, "c5": c5, "c5_weak": c5w, "extra_circuit": extra,
-                       "dataset_commit": merkle, "cpu_baseline": cpu})
+                       "dataset_commit": merkle, "split_proof": split_res, "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")

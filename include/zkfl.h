@@ -118,6 +118,33 @@ int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_
 int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_witness* const* w,
                              const uint8_t* rs, uint8_t* proofs_out);
 
+/* One proof split across GPUs (optional row: a proof too large for one device's
+ * latency budget).  The reference proves each client on one CPU (`groth16 prove`,
+ * tests/full_system_simulation.mjs:773-776); these calls divide that same prove over G processes,
+ * one per GPU, with the caller's collective (RCCL all_gather over xGMI, zkfl/split.py) in between:
+ *
+ *   zkfl_zkey_load_shard   every rank loads the same zkey keeping base i of each query (A, B1, B2,
+ *                          C, H) only when i % n_shards == shard, and the alpha/beta/delta
+ *                          augmentation bases only on shard 0.  The QAP rows and NTT are whole.
+ *   zkfl_groth16_prove_part_batch   per rank, per proof: ABC + coset NTT over the FULL witness
+ *                          (h is needed whole; redundant on every rank, ~0.4 ms), then this shard's
+ *                          share of the five MSMs.  rs is REQUIRED (n x 64 B, the same r, s on every
+ *                          rank: rank 0 draws them and broadcasts).  parts_out: n x 384 B =
+ *                          A' (64) | B1' (64) | B2' (128) | C' (64) | H (64), std affine, infinity =
+ *                          zero bytes (the zkfl_debug_prove_parts layout, here WITH the alpha/beta/
+ *                          delta/r/s terms on shard 0; C' may already include H, then H = infinity).
+ *   zkfl_groth16_assemble  after the all_gather: parts = n x n_parts x 384 B (proof-major); the parts
+ *                          of each proof are summed and pi_c = C' + H + s pi_a + r B1' is formed on
+ *                          the GPU -> n x 256 B proofs, byte-identical to zkfl_groth16_prove_batch
+ *                          with the same r, s.  Needs no key.  A coordinate >= q -> ZKFL_E_ARG. */
+int zkfl_zkey_load_shard(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t n_shards,
+                         zkfl_key** out);
+int zkfl_key_shard(const zkfl_key* key, uint32_t* shard, uint32_t* n_shards);
+int zkfl_groth16_prove_part_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
+                                  const uint8_t* rs, uint8_t* parts_out);
+int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t* parts, const uint8_t* rs,
+                          uint8_t* proofs_out);
+
 /* Parity hooks: the deterministic core of one proof.
  * h_out: domain_size x 32 B std (coset evaluations a*b-c, the H-MSM scalars) or NULL;
  * msm_out: A (64) | B1 (64) | B2 (128) | C (64) | H (64) std affine MSM results over the

@@ -1,0 +1,160 @@
+"""One proof split over G shards (optional row) — MI355X (-m gpu).
+
+zkfl_zkey_load_shard / zkfl_groth16_prove_part_batch / zkfl_groth16_assemble (include/zkfl.h):
+  * every shard's 384-byte part equals the CPU model's part (tests/split_model.py, built from the
+    oracle's prover) byte for byte, for G = 2 and 3 on config 2's circuit;
+  * the assembled proof equals the unsplit GPU proof with the same (r, s), and the oracle's;
+  * at the metric size M (2^18 domain) the 2-shard proof equals the unsplit proof;
+  * the collective protocol (zkfl/split.py) with 2 real ranks on device 0 over gloo gives the same
+    proofs as one GPU (tests/split_worker.py);
+  * assemble rejects a coordinate >= q.
+Reference call site replaced: `npx snarkjs groth16 prove` (tests/full_system_simulation.mjs:773-776).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from oracle import bn254 as bn
+from oracle import groth16 as og
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R = bn.R
+TOXIC = dict(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4)
+
+
+def _le(x):
+    return int(x).to_bytes(32, "little")
+
+
+def _setup(ctx, name, *params):
+    from zkfl import circuits, clients, native, wprog, zkey
+    b = circuits.build(name, *params)
+    zk = zkey.groth16_setup(b, ctx, zkey.Toxic(**TOXIC))
+    wp = native.WitnessProgram(ctx, wprog.compile_program(b))
+    B, D, Dp, P = params
+    inputs = [wprog.input_bytes(b, clients.Client(cid, B, D, Dp, clients.JsLcg(777 + cid))
+                                .training_input(B, P, 100000000)[0]) for cid in (1, 2)]
+    wts = wp.compute(inputs)
+    wp.close()
+    return b, zk, wts
+
+
+@pytest.fixture(scope="module")
+def small(gpu_ctx):
+    return _setup(gpu_ctx, "sgd_verified", 8, 4, 3, 1000)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_parts_equal_model_and_assemble_equals_unsplit(gpu_ctx, small, world):
+    from split_model import part
+    from zkfl import native
+    _, zk, wts = small
+    z = og.parse_zkey(zk)
+    full = native.ProvingKey(gpu_ctx, zk)
+    rss = [_le(0x1234567) + _le(0x7654321), _le(R - 1) + _le(R - 2)]
+    rs = b"".join(rss)
+    keys = [native.ProvingKey(gpu_ctx, zk, shard=k, n_shards=world) for k in range(world)]
+    try:
+        parts = []  # [shard][proof]
+        for k, key in enumerate(keys):
+            ws = [key.upload(w) for w in wts]
+            parts.append(key.prove_part_batch(ws, rs))
+            for w in ws:
+                w.close()
+        for i, wt in enumerate(wts):
+            w = og.parse_wtns(wt)
+            h = og.compute_h(z, w)
+            r = int.from_bytes(rss[i][:32], "little")
+            s = int.from_bytes(rss[i][32:], "little")
+            for k in range(world):
+                assert parts[k][i] == part(z, w, h, r, s, k, world), f"proof {i}, shard {k}: part differs"
+        blob = b"".join(parts[k][i] for i in range(len(wts)) for k in range(world))
+        proofs = gpu_ctx.assemble(blob, world, rs)
+        ws = [full.upload(w) for w in wts]
+        unsplit = full.prove_batch(ws, rs)
+        for w in ws:
+            w.close()
+        assert proofs == unsplit
+        for i, wt in enumerate(wts):
+            r = int.from_bytes(rss[i][:32], "little")
+            s = int.from_bytes(rss[i][32:], "little")
+            assert proofs[i] == og.proof_bytes(og.prove(z, og.parse_wtns(wt), r, s))
+    finally:
+        for key in keys:
+            key.close()
+        full.close()
+
+
+def test_metric_two_shards_equal_unsplit(gpu_ctx):
+    from zkfl import native
+    _, zk, wts = _setup(gpu_ctx, "sgd_verified", 128, 4, 7, 1000)
+    rs = _le(0xABCDEF) + _le(0x123456) + _le(R - 5) + _le(7)
+    full = native.ProvingKey(gpu_ctx, zk)
+    assert full.domain_size == 1 << 18
+    keys = [native.ProvingKey(gpu_ctx, zk, shard=k, n_shards=2) for k in range(2)]
+    try:
+        parts = []
+        for key in keys:
+            ws = [key.upload(w) for w in wts]
+            parts.append(key.prove_part_batch(ws, rs))
+            for w in ws:
+                w.close()
+        blob = b"".join(parts[k][i] for i in range(2) for k in range(2))
+        proofs = gpu_ctx.assemble(blob, 2, rs)
+        ws = [full.upload(w) for w in wts]
+        assert proofs == full.prove_batch(ws, rs)
+        for w in ws:
+            w.close()
+    finally:
+        for key in keys:
+            key.close()
+        full.close()
+
+
+def test_assemble_rejects_bad_coordinates(gpu_ctx):
+    from zkfl import native
+    bad = bytearray(384)
+    bad[0:32] = bn.Q.to_bytes(32, "little")  # x == q: not canonical
+    with pytest.raises(native.ZkflError) as e:
+        gpu_ctx.assemble(bytes(bad), 1, _le(1) + _le(2))
+    assert e.value.code == -1
+    # all-infinity parts are legal: pi_a = pi_b = infinity, pi_c = infinity
+    out = gpu_ctx.assemble(bytes(384 * 2), 2, _le(1) + _le(2))
+    assert out == [bytes(256)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_split_prover_two_ranks_one_device(tmp_path, gpu_ctx, small):
+    """zkfl.split.SplitProver with 2 real ranks (both on device 0, gloo): rank 0's proofs equal the
+    unsplit GPU proofs for the same (r, s)."""
+    from zkfl import native
+    _, zk, wts = small
+    rs = _le(0x51) + _le(0x52) + _le(0x53) + _le(0x54)
+    out = tmp_path / "proofs.bin"
+    env = dict(os.environ)
+    env["ZKFL_HW_QUEUES"] = "8"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "split_worker.py"), "--out", str(out), "--rs", rs.hex()]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    got = out.read_bytes()
+    full = native.ProvingKey(gpu_ctx, zk)
+    ws = [full.upload(w) for w in wts]
+    want = full.prove_batch(ws, rs)
+    for w in ws:
+        w.close()
+    full.close()
+    assert got == b"".join(want)

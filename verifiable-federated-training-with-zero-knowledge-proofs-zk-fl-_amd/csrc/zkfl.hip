@@ -78,6 +78,13 @@ bool lt_r(const uint32_t* v) {  // v < r
   return false;
 }
 
+bool lt_q(const uint32_t* v) {  // v < q (base field)
+  for (int i = 7; i >= 0; i--) {
+    if (v[i] != Q_LIMBS[i]) return v[i] < Q_LIMBS[i];
+  }
+  return false;
+}
+
 int parse_wtns(const uint8_t* buf, size_t len, WtnsView& out) {
   std::string err;
   int rc = wtns_parse(buf, len, out, err);  // csrc/host_parse.cc
@@ -330,6 +337,11 @@ ZK_DEV G1P quad_add(const G1P& p, const G1P& o, int q) {
 // The critical path is 132 quad doublings + 33 quad additions + 2 additions + one inversion.
 __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                   const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
+  // one block per proof: block b reads res[5b..], resB2[b], ks[4b..] and writes proof[64b..]
+  res += 5 * blockIdx.x;
+  resB2 += blockIdx.x;
+  ks += 4 * blockIdx.x;
+  proof += 64 * blockIdx.x;
   __shared__ G1P tab[4][8];
   __shared__ G1P part[6];  // the four products, C' + H, then the sum of parts 2 + 3
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -402,6 +414,74 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   }
 }
 
+// Proof parts of a split proof (zkfl_groth16_assemble): block b sums the n_parts partial results
+// of proof b -- parts[b][j] = A' (16 words) | B1' (16) | B2' (32) | C' (16) | H (16), std affine,
+// infinity all zero -- into res[5b + {0, 1, 2, 3}] (A', B1', C', H) and resB2[b].  Lanes 0..3 take
+// the G1 points, lane 4 the G2 point; n_parts is the world size, so a serial sum per lane.
+template <class F>
+__device__ Affine<F> load_affine_std(const uint32_t* in);
+
+template <>
+__device__ Affine<FqOps> load_affine_std<FqOps>(const uint32_t* in) {
+  Affine<FqOps> a;
+  for (int i = 0; i < 8; i++) {
+    a.x.v[i] = in[i];
+    a.y.v[i] = in[8 + i];
+  }
+  if (aff_is_inf(a)) return a;  // all zero stays the zkey's infinity encoding
+  a.x = fp_to_mont(a.x);
+  a.y = fp_to_mont(a.y);
+  return a;
+}
+
+template <>
+__device__ Affine<Fq2Ops> load_affine_std<Fq2Ops>(const uint32_t* in) {
+  Affine<Fq2Ops> a;
+  for (int i = 0; i < 8; i++) {
+    a.x.c0.v[i] = in[i];
+    a.x.c1.v[i] = in[8 + i];
+    a.y.c0.v[i] = in[16 + i];
+    a.y.c1.v[i] = in[24 + i];
+  }
+  if (aff_is_inf(a)) return a;
+  a.x = {fp_to_mont(a.x.c0), fp_to_mont(a.x.c1)};
+  a.y = {fp_to_mont(a.y.c0), fp_to_mont(a.y.c1)};
+  return a;
+}
+
+constexpr int PART_WORDS = 96;  // 384 B
+
+__global__ void __launch_bounds__(64) k_parts_sum(const uint32_t* __restrict__ parts, int n_parts,
+                                                  G1P* __restrict__ res, G2P* __restrict__ resB2) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const uint32_t* p = parts + (size_t)b * n_parts * PART_WORDS;
+  if (lane < 4) {
+    const int off = lane == 0 ? 0 : lane == 1 ? 16 : lane == 2 ? 64 : 80;  // A', B1', C', H
+    G1P acc = xyzz_inf<FqOps>();
+    for (int j = 0; j < n_parts; j++)
+      acc = xyzz_add<FqOps>(acc, xyzz_from_affine<FqOps>(load_affine_std<FqOps>(p + j * PART_WORDS + off)));
+    res[5 * b + lane] = acc;
+  } else if (lane == 4) {
+    G2P acc = xyzz_inf<Fq2Ops>();
+    for (int j = 0; j < n_parts; j++)
+      acc = xyzz_add<Fq2Ops>(acc, xyzz_from_affine<Fq2Ops>(load_affine_std<Fq2Ops>(p + j * PART_WORDS + 32)));
+    resB2[b] = acc;
+  }
+}
+
+// A split proof's part (zkfl_groth16_prove_part_batch): the slot's MSM results -> std affine,
+// A' | B1' | B2' | C' | H (PART_WORDS), one lane per point so the five inversions run side by side
+__global__ void __launch_bounds__(64) k_part_out(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                 uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x;
+  if (lane < 4) {
+    const int off = lane == 0 ? 0 : lane == 1 ? 16 : lane == 2 ? 64 : 80;
+    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(res[lane]), out + off);
+  } else if (lane == 4) {
+    store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), out + 32);
+  }
+}
+
 // MSM result(s) -> std affine bytes (parity hooks)
 template <class F>
 __global__ void __launch_bounds__(64) k_point_out(const XYZZ<F>* __restrict__ p, int n, uint32_t* __restrict__ out) {
@@ -471,6 +551,8 @@ struct zkfl_ctx {
   Profiler prof;
   VkDev* vk = nullptr;       // last prepared verification key (reused while the vk bytes repeat)
   PosTables* pos = nullptr;  // Poseidon constants of every width (first hashing call)
+  void* asm_buf = nullptr;   // zkfl_groth16_assemble's device buffers (grown on demand, reused)
+  size_t asm_cap = 0;
 };
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
@@ -493,10 +575,12 @@ struct ProofSlot {
   G2P* resB2 = nullptr;   // [1]
   Fr* d_rs = nullptr;     // r, s (64 B) | GLV halves s1, s2, r1, r2 (4 x 32 B)
   uint32_t* d_proof = nullptr;  // [64]
-  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128)
+  uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
+  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (384 at 512)
   bool busy = false;
   size_t job = 0;                 // index of the in-flight proof in its batch
   uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
+  uint8_t* out_part = nullptr;    // split proofs: where the 384 part bytes go (nullable)
 };
 
 #ifndef ZK_NO_SHARE_B
@@ -526,6 +610,10 @@ struct zkfl_key {
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
   int max_slots = 3;
+  // Split proofs (zkfl_zkey_load_shard): this key holds base i of every query only when
+  // i % nshards == shard, and the alpha/beta/delta augmentation bases only on shard 0, so its
+  // MSMs are this shard's share of each proof's sums.
+  uint32_t shard = 0, nshards = 1;
   struct WitPipe* wpipe = nullptr;  // batched witnesses of the single-key full-prove entry points
 };
 
@@ -553,7 +641,7 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof};  // extra lives in h
+  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof, s->d_parts};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -601,7 +689,8 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
   ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32 + 4 * sizeof(GlvScalar)));
   ZK_CHECK(hipMalloc(&s->d_proof, 256));
-  ZK_CHECK(hipHostMalloc(&s->pinned, 512));
+  ZK_CHECK(hipMalloc(&s->d_parts, 384));
+  ZK_CHECK(hipHostMalloc(&s->pinned, 1024));
   return hipStreamSynchronize(st);
 }
 
@@ -733,6 +822,8 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 //          pi_b, pi_c), proof D2H [ev_done]
 //   g2   : wait(ev_ready) MSM B2 [ev_b2]
 // plain = 1 (parity hook): alpha/beta/delta/r/s terms zeroed, nothing assembled.
+// plain = 2 (split proof): the full augmentation (on shard 0's bases), no assembly; the part
+// A' | B1' | B2' | C' + H | infinity goes to pinned + 512 (zkfl_groth16_prove_part_batch).
 int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
@@ -745,14 +836,14 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   int pp = prof->begin("prove", st);
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
           "upload r,s");
-  hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain);
+  hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain == 1);
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
   // C + H as one MSM into tail 2 (res[2] = C' + H, res[3] = infinity); the parity hook (plain)
   // keeps them apart
-  const bool merge = MSM_MERGE_CH && !plain && k->bCH.n > 0;
+  const bool merge = MSM_MERGE_CH && plain != 1 && k->bCH.n > 0;
   const int ntails = merge ? 3 : 4;
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
@@ -818,6 +909,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(msm_tails_g1(tails, outs, ntails, st), "msm tails");
   }
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
+  if (plain == 2) {
+    hipLaunchKernelGGL(k_part_out, dim3(1), dim3(64), 0, st, s->res, s->resB2, s->d_parts);
+    HIP_TRY(hipMemcpyAsync(s->pinned + 512, s->d_parts, 384, hipMemcpyDeviceToHost, st), "download part");
+  }
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
     hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
@@ -834,6 +929,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
 int wait_slot(ProofSlot* s) {
   HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
   if (s->out_proof) memcpy(s->out_proof, s->pinned, 256);
+  if (s->out_part) memcpy(s->out_part, s->pinned + 512, 384);
   s->busy = false;
   return ZKFL_OK;
 }
@@ -846,6 +942,7 @@ struct Job {
   hipEvent_t w_ready = nullptr;  // the witness group of the full-prove pipe (full_prove_piped)
   const uint8_t* rs = nullptr;  // 64 B or nullptr (CSPRNG)
   uint8_t* proof_out = nullptr;
+  uint8_t* part_out = nullptr;  // split proof: this shard's part instead of a proof
 };
 
 // The batch scheduler behind every prove entry point: job i goes to the next slot of its key
@@ -875,12 +972,13 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
       if (rc) break;
     }
     s->job = i;
-    s->out_proof = J.proof_out;
+    s->out_proof = J.part_out ? nullptr : J.proof_out;
+    s->out_part = J.part_out;
     if (J.w_ready) {
       hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
       if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
     }
-    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, 0);
+    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0);
     if (rc) break;
     s->busy = true;
   }
@@ -1118,6 +1216,7 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
   ctx->prof.reset();
   vk_free(ctx->vk);
   pos_tables_free(ctx->pos);
+  if (ctx->asm_buf) (void)hipFree(ctx->asm_buf);
   (void)hipStreamDestroy(ctx->st);
   delete ctx;
   return ZKFL_OK;
@@ -1153,8 +1252,11 @@ int zkfl_ctx_synchronize(zkfl_ctx* ctx) {
   return ZKFL_OK;
 }
 
-int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out) {
+namespace {
+int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t nshards,
+                   zkfl_key** out) {
   if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
+  if (nshards < 1 || nshards > 1024 || shard >= nshards) return fail(ZKFL_E_ARG, "shard must be < n_shards <= 1024");
   ZkeyHost z;
   {
     std::string err;
@@ -1180,6 +1282,8 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
   k->logn = logn;
   k->nC = nC;
   k->K = ncoef;
+  k->shard = shard;
+  k->nshards = nshards;
   auto cleanup = [&](int code) {
     key_release(k);
     return code;
@@ -1222,6 +1326,13 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       const uint8_t* pt;
       uint32_t sidx;
     };
+    // this shard's share of a query: element i when i % nshards == shard; the augmentation
+    // bases once, on shard 0
+    auto mine = [&](size_t i) { return nshards == 1 || i % nshards == shard; };
+    const bool aug_here = shard == 0;
+    // H with one shard keeps every point and no index map (scalar j = h[j]); sharded, it is
+    // compacted like the others, its map indexing h directly (no extra slots)
+    const bool h_identity = nshards == 1;
     // Build the compacted (host) base image + index map, upload, expand.
     std::vector<uint32_t> sidx_b1, sidx_b2;
     auto build = [&](auto& mb, size_t psz, const uint8_t* sec, size_t cnt, uint32_t scalar_off,
@@ -1233,14 +1344,15 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       sidx.reserve(cnt + aug.size());
       for (size_t i = 0; i < cnt; i++) {
         const uint8_t* p = sec + i * psz;
-        if (!identity && !nonzero(p, psz)) continue;
+        if (!mine(i) || (!identity && !nonzero(p, psz))) continue;
         img.insert(img.end(), p, p + psz);
         sidx.push_back(scalar_off + (uint32_t)i);
       }
-      for (const Aug& a : aug) {
-        img.insert(img.end(), a.pt, a.pt + psz);
-        sidx.push_back(a.sidx);
-      }
+      if (aug_here)
+        for (const Aug& a : aug) {
+          img.insert(img.end(), a.pt, a.pt + psz);
+          sidx.push_back(a.sidx);
+        }
       if (keep) *keep = sidx;
       hipError_t e = bases_alloc_any(mb, sidx.size());
       if (e != hipSuccess || sidx.empty()) return e;
@@ -1248,7 +1360,9 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       e = hipMalloc(&d_img, img.size());
       if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
       const uint32_t* hs = identity ? nullptr : sidx.data();
-      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, identity ? 0xFFFFFFFFu : X, st);
+      // aug.size() == 0 (H): no extra slots, the map indexes the main scalars only
+      const uint32_t xs = (identity || aug.size() == 0) ? 0xFFFFFFFFu : X;
+      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, xs, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (d_img) (void)hipFree(d_img);
       return e;
@@ -1262,7 +1376,7 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
     if (e == hipSuccess) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
-    if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, true);
+    if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, h_identity);
     if (e == hipSuccess && MSM_MERGE_CH) {
       // C (private wires -> the witness) then H (h_j -> extra[j], the slot's h vector), then
       // delta1 with -rs (extra[dom + 3]: the extra slots sit behind h)
@@ -1272,18 +1386,20 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
       sidx.reserve(nC + dom + 1);
       for (size_t i = 0; i < nC; i++) {
         const uint8_t* p = z.secC + i * 64;
-        if (!nonzero(p, 64)) continue;
+        if (!mine(i) || !nonzero(p, 64)) continue;
         img.insert(img.end(), p, p + 64);
         sidx.push_back(nPub + 1 + (uint32_t)i);
       }
       for (size_t j = 0; j < dom; j++) {
         const uint8_t* p = z.secH + j * 64;
-        if (!nonzero(p, 64)) continue;
+        if (!mine(j) || !nonzero(p, 64)) continue;
         img.insert(img.end(), p, p + 64);
         sidx.push_back(X + (uint32_t)j);
       }
-      img.insert(img.end(), delta1, delta1 + 64);
-      sidx.push_back(X + dom + 3);
+      if (aug_here) {
+        img.insert(img.end(), delta1, delta1 + 64);
+        sidx.push_back(X + dom + 3);
+      }
       e = bases_alloc_any(k->bCH, sidx.size());
       void* d_img = nullptr;
       if (e == hipSuccess) e = hipMalloc(&d_img, img.size());
@@ -1304,6 +1420,16 @@ int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out
 #undef KTRY
   *out = k;
   return ZKFL_OK;
+}
+}  // namespace
+
+int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out) {
+  return zkey_load_impl(ctx, buf, len, 0, 1, out);
+}
+
+int zkfl_zkey_load_shard(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t n_shards,
+                         zkfl_key** out) {
+  return zkey_load_impl(ctx, buf, len, shard, n_shards, out);
 }
 
 int zkfl_key_free(zkfl_key* key) {
@@ -1384,6 +1510,76 @@ int zkfl_groth16_prove_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_
     J.proof_out = proofs_out + 256 * i;
     return ZKFL_OK;
   });
+}
+
+int zkfl_key_shard(const zkfl_key* key, uint32_t* shard, uint32_t* n_shards) {
+  if (!key) return fail(ZKFL_E_ARG, "null key");
+  if (shard) *shard = key->shard;
+  if (n_shards) *n_shards = key->nshards;
+  return ZKFL_OK;
+}
+
+int zkfl_groth16_prove_part_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const zkfl_witness* const* w,
+                                  const uint8_t* rs, uint8_t* parts_out) {
+  if (!ctx || !key || (n && (!w || !rs || !parts_out))) return fail(ZKFL_E_ARG, "prove_part: null argument");
+  for (size_t i = 0; i < n; i++) {
+    if (!w[i] || w[i]->key != key) return fail(ZKFL_E_MISMATCH, "witness uploaded for another key");
+  }
+  return run_jobs(ctx, n, [&](size_t i, Job& J) {
+    J.key = key;
+    J.w = w[i]->d;
+    J.rs = rs + 64 * i;
+    J.part_out = parts_out + 384 * i;
+    return ZKFL_OK;
+  });
+}
+
+int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t* parts, const uint8_t* rs,
+                          uint8_t* proofs_out) {
+  if (!ctx || (n && (!parts || !rs || !proofs_out)) || n_parts < 1 || n_parts > 1024)
+    return fail(ZKFL_E_ARG, "assemble: bad arguments");
+  if (n == 0) return ZKFL_OK;
+  // every coordinate canonical (< q): the parts cross a process boundary
+  for (size_t i = 0; i < n * n_parts * 12; i++)
+    if (!lt_q(reinterpret_cast<const uint32_t*>(parts + 32 * i)))
+      return fail(ZKFL_E_ARG, "assemble: part coordinate " + std::to_string(i) + " is not < q");
+  std::vector<uint8_t> ks(n * 4 * sizeof(GlvScalar));
+  for (size_t i = 0; i < n; i++) {
+    uint32_t rsl[16];
+    int rc = get_rs(rs + 64 * i, rsl);
+    if (rc) return rc;
+    GlvScalar* k = reinterpret_cast<GlvScalar*>(ks.data()) + 4 * i;
+    glv_split(rsl + 8, k[0], k[1]);  // s -> pi_A's multiplier
+    glv_split(rsl, k[2], k[3]);      // r -> B1's multiplier
+  }
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->st;
+  // one device buffer, carved: parts | res (5 G1P per proof) | resB2 | GLV halves | proofs
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_res = up(n * n_parts * 384), o_b2 = o_res + up(n * 5 * sizeof(G1P)),
+               o_ks = o_b2 + up(n * sizeof(G2P)), o_pf = o_ks + up(ks.size()), total = o_pf + n * 256;
+  if (total > ctx->asm_cap) {
+    if (ctx->asm_buf) (void)hipFree(ctx->asm_buf);
+    ctx->asm_buf = nullptr;
+    ctx->asm_cap = 0;
+    HIP_TRY(hipMalloc(&ctx->asm_buf, total), "assemble buffers");
+    ctx->asm_cap = total;
+  }
+  uint8_t* base = static_cast<uint8_t*>(ctx->asm_buf);
+  void *d_parts = base, *d_res = base + o_res, *d_b2 = base + o_b2, *d_ks = base + o_ks, *d_proof = base + o_pf;
+  hipError_t e = hipMemcpyAsync(d_parts, parts, n * n_parts * 384, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_ks, ks.data(), ks.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_parts_sum, dim3((uint32_t)n), dim3(64), 0, st, (const uint32_t*)d_parts, (int)n_parts,
+                       (G1P*)d_res, (G2P*)d_b2);
+    hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n), dim3(192), 0, st, (const G1P*)d_res, (const G2P*)d_b2,
+                       (const GlvScalar*)d_ks, (uint32_t*)d_proof);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(proofs_out, d_proof, n * 256, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "assemble");
+  return ZKFL_OK;
 }
 
 int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, const zkfl_witness* const* w,
@@ -1699,6 +1895,7 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   if (rc == ZKFL_OK && s->busy) rc = wait_slot(s);
   if (rc == ZKFL_OK) {
     s->out_proof = nullptr;
+    s->out_part = nullptr;
     rc = enqueue_proof(ctx, key, s, w->d, zeros, 1);
   }
   if (rc == ZKFL_OK) rc = wait_slot(s);

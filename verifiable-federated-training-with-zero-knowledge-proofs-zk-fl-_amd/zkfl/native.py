@@ -36,6 +36,10 @@ SIGNATURES = {
     "zkfl_ctx_profile_reset": (C.c_int, [_P]),
     "zkfl_ctx_synchronize": (C.c_int, [_P]),
     "zkfl_zkey_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "zkfl_zkey_load_shard": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
+    "zkfl_key_shard": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "zkfl_groth16_prove_part_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
+    "zkfl_groth16_assemble": (C.c_int, [_P, C.c_size_t, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
     "zkfl_key_free": (C.c_int, [_P]),
     "zkfl_key_info": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "zkfl_key_set_slots": (C.c_int, [_P, C.c_int]),
@@ -393,6 +397,17 @@ class Context:
                         [int.from_bytes(pb[32 * j:32 * j + 32], "little") for j in range(k.n_public)]))
         return res
 
+    def assemble(self, parts: bytes, n_parts: int, rs: bytes) -> list:
+        """Split proofs: parts = n x n_parts x 384 B (proof-major, zkfl_groth16_prove_part_batch's
+        layout), rs = n x 64 B -> n proofs of 256 B (zkfl_groth16_assemble)."""
+        n = len(rs) // 64
+        if len(rs) != 64 * n or len(parts) != 384 * n * n_parts:
+            raise ZkflError(-1, "assemble: parts / rs sizes disagree")
+        out = _buf(256 * max(1, n))
+        check(lib().zkfl_groth16_assemble(self.h, n, n_parts, parts, rs, out))
+        ob = bytes(out)
+        return [ob[256 * i:256 * i + 256] for i in range(n)]
+
     def pairing(self, g1: bytes, g2: bytes, final_exp: bool = True) -> bytes:
         """e(P_i, Q_i) for n pairs (std affine); 384 B std Fq12 each (toObject order)."""
         n = len(g1) // 64
@@ -406,10 +421,16 @@ class Context:
 class ProvingKey:
     """A .zkey made device-resident (bases expanded per MSM window)."""
 
-    def __init__(self, ctx: Context, zkey: bytes):
+    def __init__(self, ctx: Context, zkey: bytes, shard: int = 0, n_shards: int = 1):
+        """shard / n_shards: keep only this shard's share of every query (split proofs,
+        zkfl_zkey_load_shard); the default is the whole key."""
         h = _P()
-        check(lib().zkfl_zkey_load(ctx.h, zkey, len(zkey), C.byref(h)))
+        if n_shards == 1 and shard == 0:
+            check(lib().zkfl_zkey_load(ctx.h, zkey, len(zkey), C.byref(h)))
+        else:
+            check(lib().zkfl_zkey_load_shard(ctx.h, zkey, len(zkey), shard, n_shards, C.byref(h)))
         self.h = h
+        self.shard, self.n_shards = shard, n_shards
         self.ctx = ctx
         nv, npub, dom = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib().zkfl_key_info(h, C.byref(nv), C.byref(npub), C.byref(dom)))
@@ -454,6 +475,18 @@ class ProvingKey:
         check(lib().zkfl_groth16_prove_batch(self.ctx.h, self.h, n, arr, rs, out))
         ob = bytes(out)
         return [ob[256 * i:256 * i + 256] for i in range(n)]
+
+    def prove_part_batch(self, ws, rs: bytes) -> list:
+        """This shard's parts of n proofs (rs REQUIRED, n x 64 B, the same on every shard)
+        -> [384 B] (zkfl_groth16_prove_part_batch)."""
+        n = len(ws)
+        if rs is None or len(rs) != 64 * n:
+            raise ZkflError(-1, "prove_part_batch: rs must be n x 64 bytes")
+        arr = (_P * max(1, n))(*[w.h for w in ws])
+        out = _buf(384 * max(1, n))
+        check(lib().zkfl_groth16_prove_part_batch(self.ctx.h, self.h, n, arr, rs, out))
+        ob = bytes(out)
+        return [ob[384 * i:384 * i + 384] for i in range(n)]
 
     def full_prove_batch(self, prog: "WitnessProgram", inputs, rs: bytes | None = None):
         """input vectors (wprog.input_bytes / parse_inputs) -> [(proof 256 B, [public ints])]:
