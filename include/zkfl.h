@@ -56,8 +56,8 @@ typedef struct zkfl_witness zkfl_witness;
 typedef struct zkfl_wprog zkfl_wprog;
 
 int zkfl_version(void);
-/* First 16 hex digits of SHA-256 over the sources this library was built from (csrc/*.h, *.hip,
- * *.cc sorted by name, then include/zkfl.h; the package Makefile).  bench.py prints it and smoke()
+/* First 16 hex digits of SHA-256 over the sources this library was built from (the csrc .h, .hip
+ * and .cc files sorted by name, then include/zkfl.h; the package Makefile).  bench.py prints it and smoke()
  * checks it against the tree it runs from (zkfl/native.py::source_id). */
 const char* zkfl_build_id(void);
 const char* zkfl_last_error(void);

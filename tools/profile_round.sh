@@ -10,9 +10,9 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o run -- python3 "$R/bench.py" --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none > "$OUT/bench_ks.log" 2>&1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o run -- python3 "$R/bench.py" --steps 8 --warmup 1 --slots 2 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none > "$OUT/fetch.log" 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run -- python3 "$R/bench.py" --steps 8 --warmup 1 --slots 2 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none > "$OUT/write.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o run -- python3 "$R/bench.py" --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 > "$OUT/bench_ks.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o run -- python3 "$R/bench.py" --steps 8 --warmup 1 --slots 2 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 > "$OUT/fetch.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run -- python3 "$R/bench.py" --steps 8 --warmup 1 --slots 2 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 > "$OUT/write.log" 2>&1
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/calib" -o run -- "$R/tools/pmc_calib" > "$OUT/calib.log" 2>&1
 python3 "$R/tools/rocpd_summary.py" kernels "$OUT/ks/run_results.db" "$OUT/kernel_stats.csv"
 python3 "$R/tools/rocpd_summary.py" roofline "$OUT/ks/run_results.db" "$OUT/bench_ks.log" "$OUT/roofline_pass.json"
