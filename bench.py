@@ -418,9 +418,9 @@ def split_leg(ctx, rank, world, zk, wts, full_key, dist, n=8, warm=2):
                "ms_per_proof_min": round(lat[0], 3), "single_gpu_ms_median": round(one[n // 2], 3),
                "speedup": round(one[n // 2] / lat[n // 2], 3),
                "path": "shard k of G: base i of each query with i % G == k (zkfl_zkey_load_shard) -> ABC + NTT "
-                       "(whole) + this shard's MSMs -> 384 B part -> all_gather (gloo) -> rank 0: parts summed "
+                       "(whole) + this shard's MSMs -> 768 B part (XYZZ, no inversion) -> all_gather (gloo) -> rank 0: parts summed "
                        "+ assembly on the GPU (zkfl_groth16_assemble)",
-               "exchange_bytes_per_rank": 384}
+               "exchange_bytes_per_rank": 768}
         if verified != n or same != n:
             raise SystemExit(f"[bench] split proofs: {verified}/{n} verify, {same}/{n} equal the unsplit proof")
     return res

@@ -121,7 +121,7 @@ int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, con
 /* One proof split across GPUs (optional row: a proof too large for one device's
  * latency budget).  The reference proves each client on one CPU (`groth16 prove`,
  * tests/full_system_simulation.mjs:773-776); these calls divide that same prove over G processes,
- * one per GPU, with the caller's collective (RCCL all_gather over xGMI, zkfl/split.py) in between:
+ * one per GPU, with the caller's all-gather in between (zkfl/split.py: torch.distributed; RCCL or gloo):
  *
  *   zkfl_zkey_load_shard   every rank loads the same zkey keeping base i of each query (A, B1, B2,
  *                          C, H) only when i % n_shards == shard, and the alpha/beta/delta
@@ -129,11 +129,13 @@ int zkfl_groth16_prove_multi(zkfl_ctx* ctx, size_t n, zkfl_key* const* keys, con
  *   zkfl_groth16_prove_part_batch   per rank, per proof: ABC + coset NTT over the FULL witness
  *                          (h is needed whole; redundant on every rank, ~0.4 ms), then this shard's
  *                          share of the five MSMs.  rs is REQUIRED (n x 64 B, the same r, s on every
- *                          rank: rank 0 draws them and broadcasts).  parts_out: n x 384 B =
- *                          A' (64) | B1' (64) | B2' (128) | C' (64) | H (64), std affine, infinity =
- *                          zero bytes (the zkfl_debug_prove_parts layout, here WITH the alpha/beta/
- *                          delta/r/s terms on shard 0; C' may already include H, then H = infinity).
- *   zkfl_groth16_assemble  after the all_gather: parts = n x n_parts x 384 B (proof-major); the parts
+ *                          rank: rank 0 draws them and broadcasts).  parts_out: n x 768 B =
+ *                          A' (128) | B1' (128) | B2' (256) | C' (128) | H (128), each an XYZZ point
+ *                          (x = X/ZZ, y = Y/ZZZ; G1: X|Y|ZZ|ZZZ, G2: the same with c0|c1 per
+ *                          coordinate), every coordinate 32 B std-form LE, ZZ = 0 is infinity --
+ *                          projective, so a shard pays no inversion; the alpha/beta/delta/r/s terms
+ *                          are on shard 0; C' may already include H, then H = infinity.
+ *   zkfl_groth16_assemble  after the all_gather: parts = n x n_parts x 768 B (proof-major); the parts
  *                          of each proof are summed and pi_c = C' + H + s pi_a + r B1' is formed on
  *                          the GPU -> n x 256 B proofs, byte-identical to zkfl_groth16_prove_batch
  *                          with the same r, s.  Needs no key.  A coordinate >= q -> ZKFL_E_ARG. */

@@ -1,8 +1,8 @@
 """One proof split over G shards (optional row) — MI355X (-m gpu).
 
 zkfl_zkey_load_shard / zkfl_groth16_prove_part_batch / zkfl_groth16_assemble (include/zkfl.h):
-  * every shard's 384-byte part equals the CPU model's part (tests/split_model.py, built from the
-    oracle's prover) byte for byte, for G = 2 and 3 on config 2's circuit;
+  * every shard's 768-byte part (XYZZ points) equals the CPU model's part (tests/split_model.py,
+    built from the oracle's prover) point for point, for G = 2 and 3 on config 2's circuit;
   * the assembled proof equals the unsplit GPU proof with the same (r, s), and the oracle's;
   * at the metric size M (2^18 domain) the 2-shard proof equals the unsplit proof;
   * the collective protocol (zkfl/split.py) with 2 real ranks on device 0 over gloo gives the same
@@ -51,7 +51,7 @@ def small(gpu_ctx):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_parts_equal_model_and_assemble_equals_unsplit(gpu_ctx, small, world):
-    from split_model import part
+    from split_model import affine, part
     from zkfl import native
     _, zk, wts = small
     z = og.parse_zkey(zk)
@@ -72,7 +72,7 @@ def test_parts_equal_model_and_assemble_equals_unsplit(gpu_ctx, small, world):
             r = int.from_bytes(rss[i][:32], "little")
             s = int.from_bytes(rss[i][32:], "little")
             for k in range(world):
-                assert parts[k][i] == part(z, w, h, r, s, k, world), f"proof {i}, shard {k}: part differs"
+                assert affine(parts[k][i]) == affine(part(z, w, h, r, s, k, world)), f"proof {i}, shard {k}"
         blob = b"".join(parts[k][i] for i in range(len(wts)) for k in range(world))
         proofs = gpu_ctx.assemble(blob, world, rs)
         ws = [full.upload(w) for w in wts]
@@ -118,13 +118,13 @@ def test_metric_two_shards_equal_unsplit(gpu_ctx):
 
 def test_assemble_rejects_bad_coordinates(gpu_ctx):
     from zkfl import native
-    bad = bytearray(384)
-    bad[0:32] = bn.Q.to_bytes(32, "little")  # x == q: not canonical
+    bad = bytearray(768)
+    bad[0:32] = bn.Q.to_bytes(32, "little")  # X == q: not canonical
     with pytest.raises(native.ZkflError) as e:
         gpu_ctx.assemble(bytes(bad), 1, _le(1) + _le(2))
     assert e.value.code == -1
     # all-infinity parts are legal: pi_a = pi_b = infinity, pi_c = infinity
-    out = gpu_ctx.assemble(bytes(384 * 2), 2, _le(1) + _le(2))
+    out = gpu_ctx.assemble(bytes(768 * 2), 2, _le(1) + _le(2))
     assert out == [bytes(256)]
 
 

@@ -414,71 +414,72 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   }
 }
 
-// Proof parts of a split proof (zkfl_groth16_assemble): block b sums the n_parts partial results
-// of proof b -- parts[b][j] = A' (16 words) | B1' (16) | B2' (32) | C' (16) | H (16), std affine,
-// infinity all zero -- into res[5b + {0, 1, 2, 3}] (A', B1', C', H) and resB2[b].  Lanes 0..3 take
-// the G1 points, lane 4 the G2 point; n_parts is the world size, so a serial sum per lane.
+// Parts of a split proof (zkfl_groth16_prove_part_batch / zkfl_groth16_assemble): a shard's MSM
+// results as XYZZ points, every coordinate in standard form (so the parts cross process boundaries
+// in a defined encoding without an inversion per point): A' (32 words) | B1' (32) | B2' (64: each
+// coordinate c0, c1) | C' (32) | H (32); ZZ = 0 is infinity.
+constexpr int PART_WORDS = 192;  // 768 B
+__device__ constexpr int PART_OFF[5] = {0, 32, 128, 160, 64};  // A', B1', C', H (G1), B2' (G2)
+
+__device__ void st_std(const Fq& a, uint32_t* out) {
+  const Fq x = fp_from_mont(a);
+  for (int i = 0; i < 8; i++) out[i] = x.v[i];
+}
+__device__ void st_std(const Fq2& a, uint32_t* out) {
+  st_std(a.c0, out);
+  st_std(a.c1, out + 8);
+}
+__device__ void ld_std(Fq& a, const uint32_t* in) {
+  for (int i = 0; i < 8; i++) a.v[i] = in[i];
+  a = fp_to_mont(a);
+}
+__device__ void ld_std(Fq2& a, const uint32_t* in) {
+  ld_std(a.c0, in);
+  ld_std(a.c1, in + 8);
+}
 template <class F>
-__device__ Affine<F> load_affine_std(const uint32_t* in);
-
-template <>
-__device__ Affine<FqOps> load_affine_std<FqOps>(const uint32_t* in) {
-  Affine<FqOps> a;
-  for (int i = 0; i < 8; i++) {
-    a.x.v[i] = in[i];
-    a.y.v[i] = in[8 + i];
-  }
-  if (aff_is_inf(a)) return a;  // all zero stays the zkey's infinity encoding
-  a.x = fp_to_mont(a.x);
-  a.y = fp_to_mont(a.y);
-  return a;
+__device__ void st_xyzz_std(const XYZZ<F>& p, uint32_t* out) {
+  constexpr int w = sizeof(typename F::T) / 4;
+  st_std(p.X, out);
+  st_std(p.Y, out + w);
+  st_std(p.ZZ, out + 2 * w);
+  st_std(p.ZZZ, out + 3 * w);
+}
+template <class F>
+__device__ XYZZ<F> ld_xyzz_std(const uint32_t* in) {
+  constexpr int w = sizeof(typename F::T) / 4;
+  XYZZ<F> p;
+  ld_std(p.X, in);
+  ld_std(p.Y, in + w);
+  ld_std(p.ZZ, in + 2 * w);
+  ld_std(p.ZZZ, in + 3 * w);
+  return p;
 }
 
-template <>
-__device__ Affine<Fq2Ops> load_affine_std<Fq2Ops>(const uint32_t* in) {
-  Affine<Fq2Ops> a;
-  for (int i = 0; i < 8; i++) {
-    a.x.c0.v[i] = in[i];
-    a.x.c1.v[i] = in[8 + i];
-    a.y.c0.v[i] = in[16 + i];
-    a.y.c1.v[i] = in[24 + i];
-  }
-  if (aff_is_inf(a)) return a;
-  a.x = {fp_to_mont(a.x.c0), fp_to_mont(a.x.c1)};
-  a.y = {fp_to_mont(a.y.c0), fp_to_mont(a.y.c1)};
-  return a;
+// the slot's MSM results -> its part (one lane per point)
+__global__ void __launch_bounds__(64) k_part_out(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                 uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x;
+  if (lane < 4) st_xyzz_std<FqOps>(res[lane], out + PART_OFF[lane]);
+  else if (lane == 4) st_xyzz_std<Fq2Ops>(resB2[0], out + PART_OFF[4]);
 }
 
-constexpr int PART_WORDS = 96;  // 384 B
-
+// block b sums the n_parts parts of proof b (parts[b][j]) into res[5b + {0, 1, 2, 3}] (A', B1', C',
+// H) and resB2[b]: lanes 0..3 the G1 points, lane 4 the G2 point, a serial sum over the world size
 __global__ void __launch_bounds__(64) k_parts_sum(const uint32_t* __restrict__ parts, int n_parts,
                                                   G1P* __restrict__ res, G2P* __restrict__ resB2) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const uint32_t* p = parts + (size_t)b * n_parts * PART_WORDS;
   if (lane < 4) {
-    const int off = lane == 0 ? 0 : lane == 1 ? 16 : lane == 2 ? 64 : 80;  // A', B1', C', H
     G1P acc = xyzz_inf<FqOps>();
     for (int j = 0; j < n_parts; j++)
-      acc = xyzz_add<FqOps>(acc, xyzz_from_affine<FqOps>(load_affine_std<FqOps>(p + j * PART_WORDS + off)));
+      acc = xyzz_add<FqOps>(acc, ld_xyzz_std<FqOps>(p + j * PART_WORDS + PART_OFF[lane]));
     res[5 * b + lane] = acc;
   } else if (lane == 4) {
     G2P acc = xyzz_inf<Fq2Ops>();
     for (int j = 0; j < n_parts; j++)
-      acc = xyzz_add<Fq2Ops>(acc, xyzz_from_affine<Fq2Ops>(load_affine_std<Fq2Ops>(p + j * PART_WORDS + 32)));
+      acc = xyzz_add<Fq2Ops>(acc, ld_xyzz_std<Fq2Ops>(p + j * PART_WORDS + PART_OFF[4]));
     resB2[b] = acc;
-  }
-}
-
-// A split proof's part (zkfl_groth16_prove_part_batch): the slot's MSM results -> std affine,
-// A' | B1' | B2' | C' | H (PART_WORDS), one lane per point so the five inversions run side by side
-__global__ void __launch_bounds__(64) k_part_out(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
-                                                 uint32_t* __restrict__ out) {
-  const int lane = threadIdx.x;
-  if (lane < 4) {
-    const int off = lane == 0 ? 0 : lane == 1 ? 16 : lane == 2 ? 64 : 80;
-    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(res[lane]), out + off);
-  } else if (lane == 4) {
-    store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), out + 32);
   }
 }
 
@@ -576,11 +577,11 @@ struct ProofSlot {
   Fr* d_rs = nullptr;     // r, s (64 B) | GLV halves s1, s2, r1, r2 (4 x 32 B)
   uint32_t* d_proof = nullptr;  // [64]
   uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
-  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (384 at 512)
+  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (768 at 512)
   bool busy = false;
   size_t job = 0;                 // index of the in-flight proof in its batch
   uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
-  uint8_t* out_part = nullptr;    // split proofs: where the 384 part bytes go (nullable)
+  uint8_t* out_part = nullptr;    // split proofs: where the 768 part bytes go (nullable)
 };
 
 #ifndef ZK_NO_SHARE_B
@@ -689,8 +690,8 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
   ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32 + 4 * sizeof(GlvScalar)));
   ZK_CHECK(hipMalloc(&s->d_proof, 256));
-  ZK_CHECK(hipMalloc(&s->d_parts, 384));
-  ZK_CHECK(hipHostMalloc(&s->pinned, 1024));
+  ZK_CHECK(hipMalloc(&s->d_parts, PART_WORDS * 4));
+  ZK_CHECK(hipHostMalloc(&s->pinned, 2048));
   return hipStreamSynchronize(st);
 }
 
@@ -911,7 +912,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (plain == 2) {
     hipLaunchKernelGGL(k_part_out, dim3(1), dim3(64), 0, st, s->res, s->resB2, s->d_parts);
-    HIP_TRY(hipMemcpyAsync(s->pinned + 512, s->d_parts, 384, hipMemcpyDeviceToHost, st), "download part");
+    HIP_TRY(hipMemcpyAsync(s->pinned + 512, s->d_parts, PART_WORDS * 4, hipMemcpyDeviceToHost, st), "download part");
   }
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
@@ -929,7 +930,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
 int wait_slot(ProofSlot* s) {
   HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
   if (s->out_proof) memcpy(s->out_proof, s->pinned, 256);
-  if (s->out_part) memcpy(s->out_part, s->pinned + 512, 384);
+  if (s->out_part) memcpy(s->out_part, s->pinned + 512, PART_WORDS * 4);
   s->busy = false;
   return ZKFL_OK;
 }
@@ -1529,7 +1530,7 @@ int zkfl_groth16_prove_part_batch(zkfl_ctx* ctx, zkfl_key* key, size_t n, const 
     J.key = key;
     J.w = w[i]->d;
     J.rs = rs + 64 * i;
-    J.part_out = parts_out + 384 * i;
+    J.part_out = parts_out + PART_WORDS * 4 * i;
     return ZKFL_OK;
   });
 }
@@ -1540,7 +1541,7 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
     return fail(ZKFL_E_ARG, "assemble: bad arguments");
   if (n == 0) return ZKFL_OK;
   // every coordinate canonical (< q): the parts cross a process boundary
-  for (size_t i = 0; i < n * n_parts * 12; i++)
+  for (size_t i = 0; i < n * n_parts * (PART_WORDS / 8); i++)
     if (!lt_q(reinterpret_cast<const uint32_t*>(parts + 32 * i)))
       return fail(ZKFL_E_ARG, "assemble: part coordinate " + std::to_string(i) + " is not < q");
   std::vector<uint8_t> ks(n * 4 * sizeof(GlvScalar));
@@ -1556,7 +1557,7 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
   hipStream_t st = ctx->st;
   // one device buffer, carved: parts | res (5 G1P per proof) | resB2 | GLV halves | proofs
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t o_res = up(n * n_parts * 384), o_b2 = o_res + up(n * 5 * sizeof(G1P)),
+  const size_t o_res = up(n * n_parts * PART_WORDS * 4), o_b2 = o_res + up(n * 5 * sizeof(G1P)),
                o_ks = o_b2 + up(n * sizeof(G2P)), o_pf = o_ks + up(ks.size()), total = o_pf + n * 256;
   if (total > ctx->asm_cap) {
     if (ctx->asm_buf) (void)hipFree(ctx->asm_buf);
@@ -1567,7 +1568,7 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
   }
   uint8_t* base = static_cast<uint8_t*>(ctx->asm_buf);
   void *d_parts = base, *d_res = base + o_res, *d_b2 = base + o_b2, *d_ks = base + o_ks, *d_proof = base + o_pf;
-  hipError_t e = hipMemcpyAsync(d_parts, parts, n * n_parts * 384, hipMemcpyHostToDevice, st);
+  hipError_t e = hipMemcpyAsync(d_parts, parts, n * n_parts * PART_WORDS * 4, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(d_ks, ks.data(), ks.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_parts_sum, dim3((uint32_t)n), dim3(64), 0, st, (const uint32_t*)d_parts, (int)n_parts,

@@ -15,6 +15,10 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.abspath(os.environ["ZKFL_LIB"]) if os.environ.get("ZKFL_LIB") else os.path.join(_PKG_DIR, "libzkfl.so")
 
 ZKFL_OK = 0
+# one shard's part of a split proof: A' | B1' | B2' | C' | H as XYZZ points (X, Y, ZZ, ZZZ), every
+# coordinate std-form 32 B LE (G2: c0, c1); ZZ = 0 is infinity (include/zkfl.h)
+PART_BYTES = 768
+PART_LAYOUT = {"A": (0, 128), "B1": (128, 256), "B2": (256, 512), "C": (512, 640), "H": (640, 768)}
 ERRORS = {
     -1: "ZKFL_E_ARG", -2: "ZKFL_E_FORMAT", -3: "ZKFL_E_PRIME", -4: "ZKFL_E_MISMATCH",
     -5: "ZKFL_E_DEVICE", -6: "ZKFL_E_OOM", -7: "ZKFL_E_CONSTRAINT",
@@ -398,10 +402,10 @@ class Context:
         return res
 
     def assemble(self, parts: bytes, n_parts: int, rs: bytes) -> list:
-        """Split proofs: parts = n x n_parts x 384 B (proof-major, zkfl_groth16_prove_part_batch's
+        """Split proofs: parts = n x n_parts x 768 B (proof-major, zkfl_groth16_prove_part_batch's
         layout), rs = n x 64 B -> n proofs of 256 B (zkfl_groth16_assemble)."""
         n = len(rs) // 64
-        if len(rs) != 64 * n or len(parts) != 384 * n * n_parts:
+        if len(rs) != 64 * n or len(parts) != PART_BYTES * n * n_parts:
             raise ZkflError(-1, "assemble: parts / rs sizes disagree")
         out = _buf(256 * max(1, n))
         check(lib().zkfl_groth16_assemble(self.h, n, n_parts, parts, rs, out))
@@ -478,15 +482,15 @@ class ProvingKey:
 
     def prove_part_batch(self, ws, rs: bytes) -> list:
         """This shard's parts of n proofs (rs REQUIRED, n x 64 B, the same on every shard)
-        -> [384 B] (zkfl_groth16_prove_part_batch)."""
+        -> [768 B] (zkfl_groth16_prove_part_batch)."""
         n = len(ws)
         if rs is None or len(rs) != 64 * n:
             raise ZkflError(-1, "prove_part_batch: rs must be n x 64 bytes")
         arr = (_P * max(1, n))(*[w.h for w in ws])
-        out = _buf(384 * max(1, n))
+        out = _buf(PART_BYTES * max(1, n))
         check(lib().zkfl_groth16_prove_part_batch(self.ctx.h, self.h, n, arr, rs, out))
         ob = bytes(out)
-        return [ob[384 * i:384 * i + 384] for i in range(n)]
+        return [ob[PART_BYTES * i:PART_BYTES * (i + 1)] for i in range(n)]
 
     def full_prove_batch(self, prog: "WitnessProgram", inputs, rs: bytes | None = None):
         """input vectors (wprog.input_bytes / parse_inputs) -> [(proof 256 B, [public ints])]:

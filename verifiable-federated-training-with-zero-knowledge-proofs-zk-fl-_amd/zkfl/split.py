@@ -8,8 +8,9 @@ over G GPUs, one process per GPU.
     rank k: zkey shard k of G (zkfl_zkey_load_shard: base i of every query when i % G == k,
             the alpha/beta/delta augmentation on shard 0), the FULL witness, the same (r, s)
       -> ABC + coset NTT (whole, redundant on every rank) + this shard's share of the 5 MSMs
-      -> a 384-byte part: A' | B1' | B2' | C'+H | H, std affine (zkfl_groth16_prove_part_batch)
-    all_gather of the parts (384 B per proof per rank: a latency-bound exchange, not a bandwidth
+      -> a 768-byte part: A' | B1' | B2' | C'+H | H as XYZZ points, std-form coordinates
+         (zkfl_groth16_prove_part_batch; no inversion on the shard)
+    all_gather of the parts (768 B per proof per rank: a latency-bound exchange, not a bandwidth
     one -- EC addition is not a collective reduction op, so gather + add on the root)
     rank 0: sum the parts and assemble pi_c = C' + H + s pi_a + r B1' on its GPU
             (zkfl_groth16_assemble) -> 256-byte proofs, byte-identical to an unsplit proof with
@@ -19,7 +20,7 @@ over G GPUs, one process per GPU.
 runs on the CPU in tests (tests/test_split_cpu.py drives it over gloo with the CPU oracle as the
 device) and with libzkfl on MI355X (tests/test_gpu_split.py, bench.py's split leg).  The exchange
 uses the group's backend: gloo moves the parts as host tensors (they come back from the device
-anyway, 384 B each); an nccl (RCCL) group moves them as device tensors over xGMI.  The tests and
+anyway, 768 B each); an nccl (RCCL) group moves them as device tensors over xGMI.  The tests and
 the bench use gloo: RCCL refuses two ranks on one device, which is all a 1-GPU lease has.
 """
 
@@ -28,6 +29,7 @@ from __future__ import annotations
 import secrets
 
 R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+PART_BYTES = 768  # native.PART_BYTES (kept here so the protocol imports without the library)
 
 
 def draw_rs(n: int) -> bytes:
@@ -46,8 +48,8 @@ def split_prove(part_fn, assemble_fn, n: int, rs: bytes | None = None, group=Non
                 root: int = 0):
     """Prove n proofs split over the group's ranks.
 
-    part_fn(rs) -> list of n 384-byte parts (this rank's shard);
-    assemble_fn(parts, n_parts, rs) -> list of n 256-byte proofs, parts = n x n_parts x 384 B;
+    part_fn(rs) -> list of n PART_BYTES-byte parts (this rank's shard);
+    assemble_fn(parts, n_parts, rs) -> list of n 256-byte proofs, parts = n x n_parts x PART_BYTES;
     rs: n x 64 B (read on the root only) or None (the root draws them);
     device: where the collective's tensors live (cuda:k for nccl, cpu for gloo).
     Returns the proofs on the root, None elsewhere."""
@@ -70,15 +72,15 @@ def split_prove(part_fn, assemble_fn, n: int, rs: bytes | None = None, group=Non
     dist.broadcast(rs_t, src=dist.get_global_rank(group, root) if group is not None else root, group=group)
     rs = bytes(rs_t.cpu().numpy().tobytes())
     parts = part_fn(rs)
-    if len(parts) != n or any(len(p) != 384 for p in parts):
-        raise ValueError("part_fn must return n parts of 384 bytes")
+    if len(parts) != n or any(len(p) != PART_BYTES for p in parts):
+        raise ValueError(f"part_fn must return n parts of {PART_BYTES} bytes")
     mine = torch.frombuffer(bytearray(b"".join(parts)), dtype=torch.uint8).to(dev)
     gathered = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(gathered, mine, group=group)
     if rank != root:
         return None
-    # rank-major [world][n][384] -> proof-major [n][world][384]
-    stack = torch.stack(gathered).view(world, n, 384).transpose(0, 1).contiguous()
+    # rank-major [world][n][part] -> proof-major [n][world][part]
+    stack = torch.stack(gathered).view(world, n, PART_BYTES).transpose(0, 1).contiguous()
     return assemble_fn(bytes(stack.cpu().numpy().tobytes()), world, rs)
 
 
