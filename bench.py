@@ -373,8 +373,8 @@ MAC_PEAK_PER_S = 1024 * 32 * 2.4e9 / (2.2 + 1.8)   # v_mad_u64_u32 + v_addc pair
 
 def split_leg(ctx, rank, world, zk, wts, full_key, dist, n=8, warm=2):
     """One proof split over ALL ranks (optional row; zkfl/split.py): every rank loads
-    shard `rank` of the key, proves its share of each proof's MSMs, the parts are all-gathered and
-    rank 0 assembles.  Proofs are issued one at a time, so this is LATENCY: ms per proof from
+    shard `rank` of the key and the same witnesses `wts`, proves its share of each proof's MSMs, the
+    parts are all-gathered and rank 0 assembles.  Proofs are issued one at a time, so this is LATENCY: ms per proof from
     rank 0's (r, s) broadcast to its assembled proof, against rank 0's unsplit proof on one GPU
     (same key, one proof in flight).  Every split proof is GPU-verified and equals the unsplit proof
     of the same (r, s)."""
@@ -670,7 +670,11 @@ def main():
         log(f"[bench r{rank}] end to end: {e2e}")
     split_res = None
     if args.split_proofs:
-        split_res = split_leg(ctx, rank, world, zk, wts, key, dist, args.split_proofs)
+        # every shard of a split proof needs the SAME witness: rank 0's first two clients on all ranks
+        common = [wprog.input_bytes(b, clients.Client(c + 1, batch, dim, depth, clients.JsLcg(12345 + c))
+                                    .training_input(batch, precision, 100000000)[0]) for c in range(2)]
+        split_wts = wp.compute(common) if world > 1 else wts[:2]
+        split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
         log(f"[bench r{rank}] split proof: {split_res}")
     for r_ in res:
         r_.close()

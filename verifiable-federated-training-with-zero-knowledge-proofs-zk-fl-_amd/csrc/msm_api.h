@@ -49,7 +49,7 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #if MSM_G1_AFFINE
 #define MSM_G1_L 32
 #else
-#define MSM_G1_L 24
+#define MSM_G1_L 16
 #endif
 #endif
 #ifndef MSM_STITCH_SG

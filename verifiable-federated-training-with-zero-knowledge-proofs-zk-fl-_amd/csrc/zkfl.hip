@@ -35,6 +35,7 @@
 #include "glv.h"
 #include "host_parse.h"
 #include "field.h"
+#include "field29.h"
 #include "merkle.h"
 #include "msm_api.h"
 #include "ntt.h"
@@ -326,6 +327,27 @@ ZK_DEV G1P quad_add(const G1P& p, const G1P& o, int q) {
   return r;
 }
 
+// Fq inverse on one lane by the binary extended Euclidean algorithm (field29.h, f29_inv_bgcd):
+// Montgomery 2^256 form in and out, a != 0.  The proof's last affine conversion (pi_c) sits on the
+// assembly's critical path, where Fermat's chain of ~380 dependent 32-bit products took ~0.4 ms.
+ZK_DEV Fq fq_inv_bgcd(const Fq& a) {
+  Fq c, k = fp_zero<FqP>();
+#pragma unroll
+  for (int i = 0; i < 8; i++) c.v[i] = P29::C261[i];
+  const Fq a261 = fp_mul(a, c);  // A 2^256 -> A 2^261 (the 29-bit engine's Montgomery domain)
+  Fq r;
+  f29_unpack(r.v, f29_inv_bgcd(f29_pack(a261.v)));  // A^-1 2^261, canonical
+  k.v[7] = 1u << 27;  // 2^251: x 2^261 -> x 2^256
+  return fp_mul(r, k);
+}
+
+ZK_DEV Affine<FqOps> g1_to_affine_bgcd(const G1P& p) {
+  if (xyzz_is_inf<FqOps>(p)) return {fp_zero<FqP>(), fp_zero<FqP>()};
+  const Fq iZZZ = fq_inv_bgcd(p.ZZZ);
+  const Fq iZ = fp_mul(p.ZZ, iZZZ);  // ZZ / ZZZ = 1 / Z
+  return {fp_mul(p.X, fp_mul(iZ, iZ)), fp_mul(p.Y, iZZZ)};
+}
+
 // Proof assembly, one block of three waves (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
 //   wave 0, quads 0..3 (lanes 0..15): k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)),
@@ -410,7 +432,7 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   __syncthreads();
   if (wave == 0 && g == 0) {
     const G1P C = quad_add(quad_add(t01, part[5], q), part[4], q);
-    if (q == 0) store_affine_std<FqOps>(xyzz_to_affine<FqOps>(C), proof + 48);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(C), proof + 48);
   }
 }
 
