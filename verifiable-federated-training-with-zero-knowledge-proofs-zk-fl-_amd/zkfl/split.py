@@ -53,12 +53,16 @@ def split_prove(part_fn, assemble_fn, n: int, rs: bytes | None = None, group=Non
     rs: n x 64 B (read on the root only) or None (the root draws them);
     device: where the collective's tensors live (cuda:k for nccl, cpu for gloo).
     Returns the proofs on the root, None elsewhere."""
-    import torch
-    import torch.distributed as dist
+    import sys
 
-    if not (dist.is_available() and dist.is_initialized()):  # one process: no collective
+    dist = sys.modules.get("torch.distributed")
+    if dist is None or not (dist.is_available() and dist.is_initialized()):
+        # one process, no collective -- and no torch import: loading torch's runtime libraries into
+        # a prover process that never uses them measurably slowed its later host-bound work
         rs = draw_rs(n) if rs is None else rs
         return assemble_fn(b"".join(part_fn(rs)), 1, rs)
+    import torch
+
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = torch.device("cpu") if device is None else torch.device(device)
     # the root's (r, s) to every rank: each shard folds them into its augmentation terms
