@@ -262,68 +262,132 @@ __device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out)
 // control flow stays uniform inside a quad.  A chain of point operations then costs one
 // multiply latency per level (doubling 3, addition 4) instead of one per product (9 / 14).
 // ---------------------------------------------------------------------------
+// The quad operations are written once over a field policy QF (T, mul, add, sub, dbl, is_zero,
+// zero, one, bcast<K>, pick4).  k_assemble runs them on Q29: canonical (< p) values in the 29-bit
+// engine's limbs and Montgomery domain (field29.h), so a product is one f29_mul (81 + 81
+// v_mad_u64_u32, two column chains: ~2.5x shorter single-lane latency than the 32-bit fp_mul) and
+// one conditional subtraction -- no bound bookkeeping, every value stays canonical:
+//   a, b < p -> f29_mul < p + p^2 / 2^261 < 1.006p;  a + b < 2p;  a + p - b in (0, 2p).
 // lane K of the caller's quad to all four lanes: DPP quad_perm [K,K,K,K] (a VALU move, no
 // LDS-path round trip as with ds_bpermute)
-template <int K>
-ZK_DEV Fq quad_bcast(const Fq& v) {
-  Fq r;
+template <int K, int N>
+ZK_DEV void quad_bcast_words(const uint32_t (&v)[N], uint32_t (&r)[N]) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], K * 0x55, 0xF, 0xF, false);
-  return r;
+  for (int i = 0; i < N; i++) r[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i], K * 0x55, 0xF, 0xF, false);
+}
+template <int N>
+ZK_DEV void pick4_words(int q, const uint32_t (&a)[N], const uint32_t (&b)[N], const uint32_t (&c)[N],
+                        const uint32_t (&d)[N], uint32_t (&r)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; i++) r[i] = (q & 2) ? ((q & 1) ? d[i] : c[i]) : ((q & 1) ? b[i] : a[i]);
 }
 
-ZK_DEV Fq pick4(int q, Fq a, Fq b, Fq c, Fq d) {
+struct Q29 {
+  using T = F29;
+  static ZK_DEV T mul(const T& a, const T& b) { return f29_canon_sub<1>(f29_mul(a, b)); }
+  static ZK_DEV T add(const T& a, const T& b) {
+    T r = f29_add_lazy(a, b);
+    f29_norm(r);
+    return f29_canon_sub<1>(r);
+  }
+  static ZK_DEV T sub(const T& a, const T& b) { return f29_canon_sub<1>(f29_sub_canon(a, b)); }
+  static ZK_DEV T dbl(const T& a) { return add(a, a); }
+  static ZK_DEV bool is_zero(const T& a) { return f29_is_zero(a); }
+  static ZK_DEV T zero() { return f29_zero(); }
+  static ZK_DEV T one() { return f29_const(P29::ONE); }
+  template <int K>
+  static ZK_DEV T bcast(const T& v) {
+    T r;
+    quad_bcast_words<K, 9>(v.v, r.v);
+    return r;
+  }
   // operands by value: over references the select chain becomes a select of addresses, which
   // pins every operand to the stack
-  Fq r;
+  static ZK_DEV T pick4(int q, T a, T b, T c, T d) {
+    T r;
+    pick4_words<9>(q, a.v, b.v, c.v, d.v, r.v);
+    return r;
+  }
+  // Fq (Montgomery 2^256, canonical) <-> this representation
+  static ZK_DEV T from_fq(const Fq& x) {
+    Fq c;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (q & 2) ? ((q & 1) ? d.v[i] : c.v[i]) : ((q & 1) ? b.v[i] : a.v[i]);
-  return r;
+    for (int i = 0; i < 8; i++) c.v[i] = P29::C261[i];
+    return f29_pack(fp_mul(x, c).v);  // X 2^256 -> X 2^261, canonical
+  }
+  static ZK_DEV Fq to_fq(const T& x) {
+    Fq r, k = fp_zero<FqP>();
+    f29_unpack(r.v, x);
+    k.v[7] = 1u << 27;  // 2^251: X 2^261 -> X 2^256
+    return fp_mul(r, k);
+  }
+};
+
+template <class QF>
+struct QPoint {
+  typename QF::T X, Y, ZZ, ZZZ;
+};
+template <class QF>
+ZK_DEV bool qp_is_inf(const QPoint<QF>& p) { return QF::is_zero(p.ZZ); }
+template <class QF>
+ZK_DEV QPoint<QF> qp_inf() { return {QF::one(), QF::one(), QF::zero(), QF::zero()}; }
+using G1Q = QPoint<Q29>;
+ZK_DEV G1Q g1q_from(const G1P& p) {
+  return {Q29::from_fq(p.X), Q29::from_fq(p.Y), Q29::from_fq(p.ZZ), Q29::from_fq(p.ZZZ)};
+}
+ZK_DEV G1P g1q_to(const G1Q& p) {
+  return {Q29::to_fq(p.X), Q29::to_fq(p.Y), Q29::to_fq(p.ZZ), Q29::to_fq(p.ZZZ)};
 }
 
 // dbl-2008-s-1 by levels: {U^2, X^2} -> {U V, X V, V ZZ, M^2} -> {M (S - X3), W Y, W ZZZ}
-ZK_DEV G1P quad_dbl(const G1P& p, int q) {
-  if (xyzz_is_inf<FqOps>(p)) return p;
-  const Fq U = fp_dbl(p.Y);
-  const Fq a1 = pick4(q & 1, U, p.X, U, p.X);
-  Fq t = fp_mul(a1, a1);
-  const Fq V = quad_bcast<0>(t), X2 = quad_bcast<1>(t);
-  const Fq M = fp_add(fp_dbl(X2), X2);
-  t = fp_mul(pick4(q, U, p.X, p.ZZ, M), pick4(q, V, V, V, M));
-  const Fq W = quad_bcast<0>(t), S = quad_bcast<1>(t), ZZ3 = quad_bcast<2>(t), M2 = quad_bcast<3>(t);
-  G1P r;
-  r.X = fp_sub(M2, fp_dbl(S));
-  t = fp_mul(pick4(q, M, W, W, W), pick4(q, fp_sub(S, r.X), p.Y, p.ZZZ, p.ZZZ));
-  r.Y = fp_sub(quad_bcast<0>(t), quad_bcast<1>(t));
+template <class QF>
+ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
+  using T = typename QF::T;
+  if (qp_is_inf(p)) return p;
+  const T U = QF::dbl(p.Y);
+  const T a1 = QF::pick4(q & 1, U, p.X, U, p.X);
+  T t = QF::mul(a1, a1);
+  const T V = QF::template bcast<0>(t), X2 = QF::template bcast<1>(t);
+  const T M = QF::add(QF::dbl(X2), X2);
+  t = QF::mul(QF::pick4(q, U, p.X, p.ZZ, M), QF::pick4(q, V, V, V, M));
+  const T W = QF::template bcast<0>(t), S = QF::template bcast<1>(t), ZZ3 = QF::template bcast<2>(t),
+          M2 = QF::template bcast<3>(t);
+  QPoint<QF> r;
+  r.X = QF::sub(M2, QF::dbl(S));
+  t = QF::mul(QF::pick4(q, M, W, W, W), QF::pick4(q, QF::sub(S, r.X), p.Y, p.ZZZ, p.ZZZ));
+  r.Y = QF::sub(QF::template bcast<0>(t), QF::template bcast<1>(t));
   r.ZZ = ZZ3;
-  r.ZZZ = quad_bcast<2>(t);
+  r.ZZZ = QF::template bcast<2>(t);
   return r;
 }
 
 // add-2008-s by levels: {U1, U2, S1, S2} -> {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2} -> {P PP, U1 PP, ZZ PP}
 // -> {R (Q - X3), S1 PPP, ZZZ PPP}
-ZK_DEV G1P quad_add(const G1P& p, const G1P& o, int q) {
-  if (xyzz_is_inf<FqOps>(o)) return p;
-  if (xyzz_is_inf<FqOps>(p)) return o;
-  Fq t = fp_mul(pick4(q, p.X, o.X, p.Y, o.Y), pick4(q, o.ZZ, p.ZZ, o.ZZZ, p.ZZZ));
-  const Fq U1 = quad_bcast<0>(t), U2 = quad_bcast<1>(t), S1 = quad_bcast<2>(t), S2 = quad_bcast<3>(t);
-  const Fq P = fp_sub(U2, U1), R = fp_sub(S2, S1);
-  if (fp_is_zero(P)) {
-    if (fp_is_zero(R)) return quad_dbl(p, q);
-    return xyzz_inf<FqOps>();
+template <class QF>
+ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
+  using T = typename QF::T;
+  if (qp_is_inf(o)) return p;
+  if (qp_is_inf(p)) return o;
+  T t = QF::mul(QF::pick4(q, p.X, o.X, p.Y, o.Y), QF::pick4(q, o.ZZ, p.ZZ, o.ZZZ, p.ZZZ));
+  const T U1 = QF::template bcast<0>(t), U2 = QF::template bcast<1>(t), S1 = QF::template bcast<2>(t),
+          S2 = QF::template bcast<3>(t);
+  const T P = QF::sub(U2, U1), R = QF::sub(S2, S1);
+  if (QF::is_zero(P)) {
+    if (QF::is_zero(R)) return quad_dbl<QF>(p, q);
+    return qp_inf<QF>();
   }
-  t = fp_mul(pick4(q, P, R, p.ZZ, p.ZZZ), pick4(q, P, R, o.ZZ, o.ZZZ));
-  const Fq PP = quad_bcast<0>(t), R2 = quad_bcast<1>(t), Z12 = quad_bcast<2>(t),
-           ZZZ12 = quad_bcast<3>(t);
-  t = fp_mul(pick4(q, P, U1, Z12, P), PP);
-  const Fq PPP = quad_bcast<0>(t), Q = quad_bcast<1>(t);
-  G1P r;
-  r.ZZ = quad_bcast<2>(t);
-  r.X = fp_sub(fp_sub(R2, PPP), fp_dbl(Q));
-  const Fq QX = fp_sub(Q, r.X);
-  t = fp_mul(pick4(q, R, S1, ZZZ12, R), pick4(q, QX, PPP, PPP, QX));
-  r.Y = fp_sub(quad_bcast<0>(t), quad_bcast<1>(t));
-  r.ZZZ = quad_bcast<2>(t);
+  t = QF::mul(QF::pick4(q, P, R, p.ZZ, p.ZZZ), QF::pick4(q, P, R, o.ZZ, o.ZZZ));
+  const T PP = QF::template bcast<0>(t), R2 = QF::template bcast<1>(t), Z12 = QF::template bcast<2>(t),
+          ZZZ12 = QF::template bcast<3>(t);
+  t = QF::mul(QF::pick4(q, P, U1, Z12, P), PP);
+  const T PPP = QF::template bcast<0>(t), Q = QF::template bcast<1>(t);
+  QPoint<QF> r;
+  r.ZZ = QF::template bcast<2>(t);
+  r.X = QF::sub(QF::sub(R2, PPP), QF::dbl(Q));
+  const T QX = QF::sub(Q, r.X);
+  t = QF::mul(QF::pick4(q, R, S1, ZZZ12, R), QF::pick4(q, QX, PPP, PPP, QX));
+  r.Y = QF::sub(QF::template bcast<0>(t), QF::template bcast<1>(t));
+  r.ZZZ = QF::template bcast<2>(t);
   return r;
 }
 
@@ -348,6 +412,16 @@ ZK_DEV Affine<FqOps> g1_to_affine_bgcd(const G1P& p) {
   return {fp_mul(p.X, fp_mul(iZ, iZ)), fp_mul(p.Y, iZZZ)};
 }
 
+// G2 likewise: (a0 + a1 u)^-1 = (a0 - a1 u) / (a0^2 + a1^2), one Fq inverse
+ZK_DEV Affine<Fq2Ops> g2_to_affine_bgcd(const G2P& p) {
+  if (xyzz_is_inf<Fq2Ops>(p)) return {f2_zero(), f2_zero()};
+  const Fq2& z = p.ZZZ;
+  const Fq ni = fq_inv_bgcd(fp_add(fp_sqr(z.c0), fp_sqr(z.c1)));
+  const Fq2 iZZZ = {fp_mul(z.c0, ni), fp_neg(fp_mul(z.c1, ni))};
+  const Fq2 iZ = f2_mul(p.ZZ, iZZZ);
+  return {f2_mul(p.X, f2_sqr(iZ)), f2_mul(p.Y, iZZZ)};
+}
+
 // Proof assembly, one block of three waves (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
 //   wave 0, quads 0..3 (lanes 0..15): k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)),
@@ -356,7 +430,8 @@ ZK_DEV Affine<FqOps> g1_to_affine_bgcd(const G1P& p) {
 //     quad 4: C' + H meanwhile; then quads 0, 1 sum the parts and quad 0 adds C' + H and writes
 //     pi_c (one inversion) -> proof[48..63]
 //   wave 1, lane 0: pi_a affine -> proof[0..15];  wave 2, lane 0: pi_b affine -> proof[16..47]
-// The critical path is 132 quad doublings + 33 quad additions + 2 additions + one inversion.
+// The critical path is 132 quad doublings + 33 quad additions + 2 additions + one inversion; the
+// quad operations run in the 29-bit engine (Q29, canonical values), every inversion is a binary GCD.
 __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                   const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
   // one block per proof: block b reads res[5b..], resB2[b], ks[4b..] and writes proof[64b..]
@@ -364,8 +439,8 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   resB2 += blockIdx.x;
   ks += 4 * blockIdx.x;
   proof += 64 * blockIdx.x;
-  __shared__ G1P tab[4][8];
-  __shared__ G1P part[6];  // the four products, C' + H, then the sum of parts 2 + 3
+  __shared__ G1Q tab[4][8];
+  __shared__ G1Q part[6];  // the four products, C' + H, then the sum of parts 2 + 3
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 2, q = lane & 3;
   if (wave == 0 && g < 4) {
@@ -378,12 +453,13 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
     }
     const GlvScalar k = ks[g];
     if (k.neg) P = xyzz_neg<FqOps>(P);
-    if (q == 0) tab[g][0] = P;
-    G1P Q = quad_dbl(P, q);
+    const G1Q P29 = g1q_from(P);
+    if (q == 0) tab[g][0] = P29;
+    G1Q Q = quad_dbl<Q29>(P29, q);
     if (q == 0) tab[g][1] = Q;
 #pragma unroll 1
     for (int j = 2; j < 8; j++) {
-      Q = quad_add(Q, P, q);
+      Q = quad_add<Q29>(Q, P29, q);
       if (q == 0) tab[g][j] = Q;
     }
     // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
@@ -396,43 +472,43 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
       dg[w >> 3] |= (carry ? (v - 16) & 15u : v) << (4 * (w & 7));
     }
     dg[4] = carry;
-    G1P acc = xyzz_inf<FqOps>();
+    G1Q acc = qp_inf<Q29>();
 #pragma unroll 1
     for (int w = 32; w >= 0; w--) {
       if (w < 32)
-        for (int j = 0; j < 4; j++) acc = quad_dbl(acc, q);
+        for (int j = 0; j < 4; j++) acc = quad_dbl<Q29>(acc, q);
       const int wi = w >> 3;
       const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
       const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
       if (nib) {
         const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
-        G1P t = tab[g][(d < 0 ? -d : d) - 1];
-        const Fq ny = fp_neg(t.Y);
+        G1Q t = tab[g][(d < 0 ? -d : d) - 1];
+        const F29 ny = Q29::sub(Q29::zero(), t.Y);
 #pragma unroll
-        for (int i = 0; i < 8; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
-        acc = quad_add(acc, t, q);
+        for (int i = 0; i < 9; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
+        acc = quad_add<Q29>(acc, t, q);
       }
     }
     if (q == 0) part[g] = acc;
   } else if (wave == 0 && g == 4) {  // C' + H, off the critical path
-    const G1P c = quad_add(res[2], res[3], q);
+    const G1Q c = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
     if (q == 0) part[4] = c;
   } else if (wave == 1 && lane == 0) {
-    store_affine_std<FqOps>(xyzz_to_affine<FqOps>(res[0]), proof);
+    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
   } else if (wave == 2 && lane == 0) {
-    store_affine_std<Fq2Ops>(xyzz_to_affine<Fq2Ops>(resB2[0]), proof + 16);
+    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
   }
   __syncthreads();
   if (wave == 0 && g == 1) {
-    const G1P t = quad_add(part[2], part[3], q);
+    const G1Q t = quad_add<Q29>(part[2], part[3], q);
     if (q == 0) part[5] = t;
   }
-  G1P t01 = xyzz_inf<FqOps>();
-  if (wave == 0 && g == 0) t01 = quad_add(part[0], part[1], q);
+  G1Q t01 = qp_inf<Q29>();
+  if (wave == 0 && g == 0) t01 = quad_add<Q29>(part[0], part[1], q);
   __syncthreads();
   if (wave == 0 && g == 0) {
-    const G1P C = quad_add(quad_add(t01, part[5], q), part[4], q);
-    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(C), proof + 48);
+    const G1Q C = quad_add<Q29>(quad_add<Q29>(t01, part[5], q), part[4], q);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
   }
 }
 
