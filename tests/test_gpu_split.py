@@ -158,3 +158,29 @@ def test_split_prover_two_ranks_one_device(tmp_path, gpu_ctx, small):
         w.close()
     full.close()
     assert got == b"".join(want)
+
+
+@pytest.mark.parametrize("world", [4, 7])
+def test_many_shards_small_circuit(gpu_ctx, world):
+    """More shards than some queries have points: shards with few or no bases of a query (empty
+    MSMs) still give parts whose sum assembles to the unsplit proof (config 1's PoseidonHash2)."""
+    from oracle import witness as ow
+    from zkfl import circuits, native, zkey
+    b = circuits.build("poseidon_hash2")
+    zk = zkey.groth16_setup(b, gpu_ctx, zkey.Toxic(**TOXIC))
+    wt = zkey.wtns_bytes(ow.evaluate(b, {"left": 3, "right": 4}))
+    rs = _le(0x99) + _le(0x77)
+    full = native.ProvingKey(gpu_ctx, zk)
+    keys = [native.ProvingKey(gpu_ctx, zk, shard=k, n_shards=world) for k in range(world)]
+    try:
+        parts = []
+        for key in keys:
+            w = key.upload(wt)
+            parts.append(key.prove_part_batch([w], rs)[0])
+            w.close()
+        proof = gpu_ctx.assemble(b"".join(parts), world, rs)[0]
+        assert proof == full.prove(wt, rs)[0]
+    finally:
+        for key in keys:
+            key.close()
+        full.close()
