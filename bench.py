@@ -668,14 +668,12 @@ def main():
         e2e = end_to_end_leg(key, wp, wprog.compile_program(b), [json.dumps(x) for x in input_objs], args.slots,
                              args.e2e_steps, ctx, dist, zk, pubs)
         log(f"[bench r{rank}] end to end: {e2e}")
-    split_res = None
+    split_wts = None
     if args.split_proofs:
         # every shard of a split proof needs the SAME witness: rank 0's first two clients on all ranks
         common = [wprog.input_bytes(b, clients.Client(c + 1, batch, dim, depth, clients.JsLcg(12345 + c))
                                     .training_input(batch, precision, 100000000)[0]) for c in range(2)]
         split_wts = wp.compute(common) if world > 1 else wts[:2]
-        split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
-        log(f"[bench r{rank}] split proof: {split_res}")
     for r_ in res:
         r_.close()
     wp.close()
@@ -686,14 +684,16 @@ def main():
         log(f"[bench r{rank}] config 5: {c5}; weak: {c5w}")
     extra = None
     if args.extra_circuit and args.extra_circuit != "none" and args.extra_circuit != args.circuit:
-        key.close()
-        key = None
         extra = extra_circuit_leg(ctx, rank, world, args.extra_circuit, args.extra_steps, args.slots, dist)
         log(f"[bench r{rank}] {args.extra_circuit}: {extra}")
     merkle = None
     if args.merkle_log2n:
         merkle = merkle_leg(ctx, rank, args.merkle_log2n)
         log(f"[bench r{rank}] dataset commitment: {merkle}")
+    split_res = None
+    if args.split_proofs:  # last: the other legs never run beside a second (shard) key
+        split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
+        log(f"[bench r{rank}] split proof: {split_res}")
     if rank == 0:
         cpu, oracle_match = None, None
         if world == 1 and not args.no_cpu_baseline:
