@@ -57,6 +57,8 @@ struct PairHost {
   static V one() { return {f29_const(P29::ONE), f29_zero()}; }
   static V swap(const V& a) { return {a.l[1], a.l[0]}; }
   static V sel(const V& v1, const V& v0) { return {v0.l[0], v1.l[1]}; }
+  static V even(const V& a) { return {a.l[0], a.l[0]}; }
+  static V odd(const V& a) { return {a.l[1], a.l[1]}; }
   static bool is_zero(const V& a) { return f29_is_zero(a.l[0]) && f29_is_zero(a.l[1]); }
   static bool is_zero3(const V& a) { return f29_is_zero3(a.l[0]) && f29_is_zero3(a.l[1]); }
   static V mul(const V& a, const V& b) { return {f29_mul(a.l[0], b.l[0]), f29_mul(a.l[1], b.l[1])}; }

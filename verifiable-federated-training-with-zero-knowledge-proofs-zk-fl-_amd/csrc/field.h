@@ -548,6 +548,14 @@ ZK_DEV uint32_t pair_swap_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
+// the even / odd lane of each pair to both lanes: DPP quad_perm [0,0,2,2] / [1,1,3,3]
+ZK_DEV uint32_t pair_even_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);
+}
+ZK_DEV uint32_t pair_odd_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);
+}
+
 ZK_DEV Fq pair_swap(const Fq& a) {
   Fq r;
 #pragma unroll

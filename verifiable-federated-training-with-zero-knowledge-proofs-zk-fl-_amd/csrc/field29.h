@@ -641,9 +641,10 @@ struct G2P29 {
 template <class L>
 ZK_HD typename L::V f2_mul(const typename L::V& a, const typename L::V& b, const uint32_t (&k)[9]) {
   using V = typename L::V;
-  const V pa = L::swap(a), pb = L::swap(b);
+  const V pa = L::swap(a);
   const V zero = L::zero();
-  return L::mulsum2(a, L::sel(pb, b), L::sel(pa, L::ksub(k, zero, pa)), L::sel(b, pb));
+  // b0 and b1 to both lanes by one broadcast each (was: swap(b) and two selects)
+  return L::mulsum2(a, L::even(b), L::sel(pa, L::ksub(k, zero, pa)), L::odd(b));
 }
 
 // a^2 over Fq2 (a normalized, a < A p, K >= A p): one Montgomery product per lane
@@ -667,10 +668,10 @@ template <class L>
 ZK_HD typename L::V f2_mulsub(const typename L::V& A, const typename L::V& B, const uint32_t (&kA)[9],
                               const typename L::V& Y, const typename L::V& D, const uint32_t (&kY)[9]) {
   using V = typename L::V;
-  const V pA = L::swap(A), pB = L::swap(B), pY = L::swap(Y), pD = L::swap(D);
+  const V pA = L::swap(A), pY = L::swap(Y);
   const V zero = L::zero();
   const V x[4] = {A, L::sel(pA, L::ksub(kA, zero, pA)), L::ksub(kY, zero, Y), L::sel(L::ksub(kY, zero, pY), pY)};
-  const V y[4] = {L::sel(pB, B), L::sel(B, pB), L::sel(pD, D), L::sel(D, pD)};
+  const V y[4] = {L::even(B), L::odd(B), L::even(D), L::odd(D)};
   return L::mulsum4(x, y);
 }
 
@@ -797,6 +798,18 @@ struct Pair29Dev {
     V r;
 #pragma unroll
     for (int i = 0; i < 9; i++) r.v[i] = h ? v1.v[i] : v0.v[i];
+    return r;
+  }
+  static ZK_DEV V even(const V& a) {  // component 0 of the pair in both lanes
+    V r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = pair_even_u32(a.v[i]);
+    return r;
+  }
+  static ZK_DEV V odd(const V& a) {  // component 1 of the pair in both lanes
+    V r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = pair_odd_u32(a.v[i]);
     return r;
   }
   static ZK_DEV bool is_zero(const V& a) {
