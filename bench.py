@@ -591,6 +591,7 @@ def main():
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     ap.add_argument("--extra-circuit", default="M19", help="second training-circuit size leg ('' or none: skip)")
     ap.add_argument("--extra-steps", type=int, default=4, help="timed steps of the extra-circuit leg")
+    ap.add_argument("--c5-slots", type=int, default=8, help="proof slots per key in the config-5 legs")
     ap.add_argument("--split-proofs", type=int, default=8,
                     help="split-proof leg: proofs, one at a time, each split over all ranks (0: skip)")
     args = ap.parse_args()
@@ -680,7 +681,7 @@ def main():
     key.set_slots(1)
     c5 = c5w = None
     if args.c5_rounds:
-        c5, c5w = c5_leg(ctx, rank, world, args.c5_rounds, min(args.slots, 8), dist, args.c5_weak_rounds)
+        c5, c5w = c5_leg(ctx, rank, world, args.c5_rounds, args.c5_slots, dist, args.c5_weak_rounds)
         log(f"[bench r{rank}] config 5: {c5}; weak: {c5w}")
     extra = None
     if args.extra_circuit and args.extra_circuit != "none" and args.extra_circuit != args.circuit:
