@@ -115,6 +115,9 @@ def test_inverse_canon_and_affine_add(f29):
     got = f29(["invb " + limbs(v) for v in lifted])          # binary extended Euclid, canonical out
     for v, (r,) in zip(vals, got):
         assert r == pow(v * RINV, -1, P) * R % P
+    # 0 and p (both 0 mod p) have no inverse: 0 comes back at once (it used to halve u = 0 forever,
+    # a malformed split-proof part reached it through k_assemble)
+    assert [list(x) for x in f29(["invb " + limbs(0), "invb " + limbs(P)])] == [[0], [0]]
     cv = [rng.randrange(4 * P) for _ in range(200)] + [0, P, 2 * P, 3 * P, 4 * P - 1, P - 1]
     got = f29(["canon " + limbs(v) for v in cv])
     for v, (r,) in zip(cv, got):

@@ -217,6 +217,31 @@ def test_msm_g2_small_scalars(gpu_ctx):
     assert _g2_std(out) == bn.mul(bn.G2_GEN, want)
 
 
+@pytest.mark.parametrize("target", [1, 7, 64, 1000])
+@pytest.mark.parametrize("case", ["random", "ones", "small"])
+def test_msm_long_chunks(gpu_ctx, monkeypatch, target, case):
+    """Adaptive chunk length (csrc/msm_api.h msm_chunk_len): with the resident-lane target forced
+    small (ZKFL_MSM_TARGET), small MSMs run chunks of up to all their entries in one lane, with
+    chunk edges anywhere in a bucket, and the stitching's liveness flags skip dead levels."""
+    monkeypatch.setenv("ZKFL_MSM_TARGET", str(target))
+    rnd = random.Random(zlib.crc32(f"{case}{target}".encode()))
+    for g2, n in ((False, 2500), (True, 900)):
+        ks = [rnd.randrange(1, R) for _ in range(n)]
+        if case == "random":
+            ss = [rnd.randrange(R) for _ in range(n)]
+        elif case == "ones":
+            ss = [1] * n
+        else:
+            ss = [rnd.choice([0, 1, 2, 3, 100, 1 << 15, (1 << 15) + 1, R - 1]) for _ in range(n)]
+        want = _expect(ks, ss)
+        if g2:
+            out = _g2_std(gpu_ctx.msm_g2(_bases_g2(gpu_ctx, ks), _scal(ss)))
+            assert out == (bn.mul(bn.G2_GEN, want) if want else None)
+        else:
+            out = _g1_std(gpu_ctx.msm_g1(_bases_g1(gpu_ctx, ks), _scal(ss)))
+            assert out == (bn.mul(bn.G1_GEN, want) if want else None)
+
+
 # ---------------------------------------------------------------------------
 # Full Groth16 proofs
 # ---------------------------------------------------------------------------

@@ -128,6 +128,59 @@ def test_assemble_rejects_bad_coordinates(gpu_ctx):
     assert out == [bytes(256)]
 
 
+# word offsets of a part's points (csrc/zkfl.hip PART_OFF): A' 0, B1' 32, B2' 64 (G2), C' 128, H 160;
+# a G1 point is X | Y | ZZ | ZZZ, 8 words each, standard form
+@pytest.mark.parametrize("case", ["zz_without_zzz", "zzz_without_zz", "off_curve", "zz3_ne_zzz2", "g2_off_curve"])
+def test_assemble_rejects_malformed_points(gpu_ctx, case):
+    """canonical but malformed parts used to reach the assembly's binary-GCD inversion
+    (ZZ = 1, ZZZ = 0 -> inverse of 0, an endless loop).  k_parts_sum now checks every point
+    (infinity, or ZZ^3 = ZZZ^2 and Y^2 = X^3 + b ZZ^3) and the call fails with ZKFL_E_ARG."""
+    from zkfl import native
+    bad = bytearray(768)
+    w = lambda word, v: bad.__setitem__(slice(4 * word, 4 * word + 32), _le(v))  # noqa: E731
+    if case == "zz_without_zzz":
+        w(0 + 16, 1)                                   # A': ZZ = 1, ZZZ = 0
+    elif case == "zzz_without_zz":
+        w(32 + 24, 1)                                  # B1': ZZ = 0, ZZZ = 1
+    elif case == "off_curve":                          # C' = (1, 1, 1, 1): 1 != 1 + 3
+        for k in range(4):
+            w(128 + 8 * k, 1)
+    elif case == "zz3_ne_zzz2":                        # H: the generator (1, 2) with ZZ = 4, ZZZ = 9
+        w(160, 4), w(160 + 8, 18), w(160 + 16, 4), w(160 + 24, 9)
+    else:                                              # B2': x = 0, y = 1 is no point of the twist
+        w(64 + 8, 0), w(64 + 16, 1), w(64 + 32, 1), w(64 + 48, 1)
+    with pytest.raises(native.ZkflError) as e:
+        gpu_ctx.assemble(bytes(bad), 1, _le(1) + _le(2))
+    assert e.value.code == -1
+    # the generator as a scaled XYZZ point (X = 4, Y = 16, ZZ = 4, ZZZ = 8: lambda = 2) is accepted
+    good = bytearray(768)
+    for k, v in enumerate((4, 16, 4, 8)):
+        good[4 * (0 + 8 * k):4 * (0 + 8 * k) + 32] = _le(v)
+    proof = gpu_ctx.assemble(bytes(good), 1, _le(1) + _le(2))[0]
+    assert bn.g1_from_bytes_std(proof[:64]) == bn.G1_GEN
+
+
+def test_sharded_key_refuses_whole_proofs(gpu_ctx, small):
+    """a key loaded as one shard of a split proof holds only its share of every MSM (and
+    shards > 0 no alpha/beta/delta terms): proving a whole proof with it is ZKFL_E_ARG, not a
+    256-byte proof that does not verify."""
+    from zkfl import native
+    _, zk, wts = small
+    for k in range(2):
+        key = native.ProvingKey(gpu_ctx, zk, shard=k, n_shards=2)
+        try:
+            with pytest.raises(native.ZkflError) as e:
+                key.prove(wts[0], _le(3) + _le(4))
+            assert e.value.code == -1
+            ws = [key.upload(wts[0])]
+            with pytest.raises(native.ZkflError):
+                key.prove_batch(ws, _le(3) + _le(4))
+            assert len(key.prove_part_batch(ws, _le(3) + _le(4))[0]) == 768  # parts still work
+            ws[0].close()
+        finally:
+            key.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -1,0 +1,59 @@
+"""gfx950 ISA of the built libzkfl.so, checked on the CPU (tools/isa_check.py; no GPU needed).
+
+Guards the LDS-DMA ordering of the MSM accumulation kernels (csrc/msm.h k_msm_accumulate): every
+ds_read_b128 of the prefetch buffer must be preceded, on every control-flow path, by an
+`s_waitcnt vmcnt(0)` after the global_load_lds_dwordx4 that fills it.  In round 3 the compiler
+dropped that wait on the loop's first iteration once the buffer became a native vector type
+(commit 5a57083): 25 GPU proof tests failed while the MSM primitive tests passed by timing, so
+the ordering is now checked statically on the shipped code object instead of by luck on the GPU.
+"""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import isa_check  # noqa: E402
+
+SO = os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd", "libzkfl.so")
+
+
+@pytest.fixture(scope="module")
+def acc():
+    if not os.path.exists(SO):
+        pytest.skip("libzkfl.so not built (__graft_entry__.build())")
+    if not shutil.which(os.path.join(isa_check.LLVM, "llvm-objdump")):
+        pytest.skip("llvm-objdump not available")
+    ks = isa_check.disassemble(SO, r"k_msm_accumulate")
+    return ks
+
+
+def test_both_accumulation_kernels_present(acc):
+    names = list(acc)
+    assert any("FqOps29" in n for n in names) and any("Fq2Pair29" in n for n in names), names
+
+
+def test_lds_dma_waited_before_every_read(acc):
+    for name, lines in acc.items():
+        assert sum("global_load_lds_dwordx4" in ln for ln in lines) >= 4, name   # the prefetch exists
+        assert sum("ds_read_b128" in ln for ln in lines) >= 4, name
+        bad = isa_check.lds_dma_hazards(lines)
+        assert not bad, f"{name}: LDS reads with a DMA possibly in flight: {bad}"
+
+
+def test_checker_finds_a_dropped_wait(acc):
+    """The checker itself: the same kernels with their vmcnt(0) waits deleted must be flagged
+    (the round-3 failure mode)."""
+    for name, lines in acc.items():
+        stripped = [ln for ln in lines if not ln.startswith("s_waitcnt") or "vmcnt(0)" not in ln]
+        assert isa_check.lds_dma_hazards(stripped), name
+
+
+def test_accumulation_kernels_do_not_spill(acc):
+    res = isa_check.resources(SO, r"k_msm_accumulate")
+    assert len(res) == 2
+    for name, r in res.items():
+        assert r.get("vgpr_spill_count", 0) == 0 and r.get("private_segment_fixed_size", 0) == 0, (name, r)
+        assert r["group_segment_fixed_size"] == 8192, (name, r)  # two 4 KB LDS-DMA buffers per wave

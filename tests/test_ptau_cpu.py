@@ -192,3 +192,16 @@ def test_secret_derivation(monkeypatch):
     assert a != ptau.derive_secret("entropy", "alpha")
     monkeypatch.delenv("ZKFL_DETERMINISTIC_SETUP")
     assert ptau.derive_secret("entropy", "tau") != ptau.derive_secret("entropy", "tau")
+
+
+def test_prepare_phase2_refuses_too_large_power_before_group_work(monkeypatch):
+    """a power-28 transcript (MAX_POWER) is valid phase 1, but its phase-2 tauG1 block
+    is 2^29 points, past the GPU group FFT's 2^28: prepare phase2 must refuse it up front, not after
+    the earlier blocks' work.  (A real power-28 file is 34 GB; the bound is lowered to test it.)"""
+    class NoGroupWork:
+        def __getattr__(self, name):
+            raise AssertionError(f"group work ({name}) before the power check")
+    monkeypatch.setattr(ptau, "MAX_PHASE2_POWER", 3)
+    with pytest.raises(ValueError, match="power 4 > 3"):
+        ptau.prepare_phase2(ptau.new(4), NoGroupWork())
+    assert ptau.MAX_POWER == 28 and ptau.MAX_PHASE2_POWER + 1 <= 28

@@ -520,8 +520,17 @@ ZK_HD bool f29_sub_plain(const F29& a, const F29& b, F29& r) {
   r.v[8] = (uint32_t)top;
   return top >= 0;
 }
+// a == 0 (mod p) has no inverse: it returns 0, as the Fermat inverse does (0^(p-2) = 0), instead
+// of halving u = 0 forever.  Every step below removes at least one bit from u or v (both < 2^254),
+// so a valid input takes at most 2 x 254 outer iterations; the bound only guards the kernel.
 ZK_HD F29 f29_inv_bgcd(const F29& a_in) {
   F29 u = f29_canon_sub<1>(a_in), v = f29_const(P29::P), x1 = f29_zero(), x2 = f29_zero();
+  {
+    uint32_t z = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) z |= u.v[i];
+    if (z == 0) return f29_zero();
+  }
   x1.v[0] = 1;
   const F29 P = f29_const(P29::P);
   auto half = [&](F29& x) {  // x / 2 mod p for canonical x
@@ -531,8 +540,9 @@ ZK_HD F29 f29_inv_bgcd(const F29& a_in) {
     }
     x = f29_shr1(x);
   };
+  int guard = 0;
 #pragma unroll 1
-  while (!f29_is_one_plain(u) && !f29_is_one_plain(v)) {
+  while (!f29_is_one_plain(u) && !f29_is_one_plain(v) && guard++ < 2 * 261) {
 #pragma unroll 1
     while (f29_even(u)) {
       u = f29_shr1(u);

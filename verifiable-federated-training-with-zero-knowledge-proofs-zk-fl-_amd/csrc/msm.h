@@ -559,26 +559,33 @@ ZK_DEV void msm_emit_run(uint32_t k, const XYZZ<F>& acc, bool real, bool open_le
   }
 }
 
+// Marks stitching level `level` live when any lane of the wave emitted a real open run.
+ZK_DEV void msm_mark_live(uint32_t* __restrict__ live, int level, bool open) {
+  const uint64_t b = __ballot(open);
+  if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)b) - 1)) live[level] = 1u;
+}
+
 // Level 0: lane c adds the sorted entries [c*L, min(c*L+L, nnz)) (fixed-size chunks, independent
-// of bucket boundaries, so every lane does the same work).  Software-pipelined: the key/index of
-// entry p+1 and its base are in flight while entry p is added.  MINW: minimum waves per SIMD
-// the register allocator must allow (chosen per curve).
+// of bucket boundaries, so every lane does the same work; L = msm_chunk_len(nnz, target)).
+// Software-pipelined: the key/index of entry p+1 and its base are in flight while entry p is
+// added.  MINW: minimum waves per SIMD the register allocator must allow (chosen per curve,
+// DESIGN.md §5).
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<S>* __restrict__ bases,
     const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
-    XYZZ<S>* __restrict__ buckets) {
+    XYZZ<S>* __restrict__ buckets, uint32_t target, uint32_t* __restrict__ live) {
   using IO = MsmIO<F>;
   constexpr bool PF = sizeof(typename S::T) == 32 ? MSM_G1_PREFETCH : MSM_G2_PREFETCH;
   const size_t c = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
   const uint32_t nnz = *nnz_ptr;
-  constexpr uint32_t L = MsmChunk<S>::L;
+  const uint32_t L = msm_chunk_len<S>(nnz, target);
   const size_t p0 = c * L;
   if (p0 >= nnz) return;
   const uint32_t p1 = (uint32_t)(p0 + L < nnz ? p0 + L : nnz);
   // the neighbouring chunks' keys and the item slots are only read at a run's end (registers are
   // the G1 kernel's limit at 4 waves/SIMD)
-  bool slot0 = false, slot1 = false, first_run = true;
+  bool slot0 = false, slot1 = false, first_run = true, open = false;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t cur = keys[p0];
   uint32_t v0 = vals[p0], k1 = 0, v1 = 0;
@@ -635,6 +642,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
       const bool open_right = last && p1 < nnz && keys[p1] == cur;
       msm_emit_run<F>(cur, acc, true, open_left, open_right, buckets, item_key + 2 * c, item_val + 2 * c, slot0,
                       slot1);
+      open = open || open_left || open_right;
       acc = xyzz_inf<F>();
       cur = k1;
       first_run = false;
@@ -649,6 +657,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   }
   if (!slot0) item_key[2 * c] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
   if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
+  msm_mark_live(live, 0, open);
 }
 
 }  // namespace zkfl
@@ -657,8 +666,8 @@ namespace zkfl {
 
 // Item count of stitching level `level` (>= 1), derived on the device from nnz.
 template <class S>
-ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level) {
-  constexpr uint32_t L = MsmChunk<S>::L;
+ZK_DEV uint32_t msm_items_at(uint32_t nnz, int level, uint32_t target) {
+  const uint32_t L = msm_chunk_len<S>(nnz, target);
   uint32_t n = 2 * ((nnz + L - 1) / L);
   for (int l = 1; l < level; l++) n = 2 * ((n + MSM_SG - 1) / MSM_SG);
   return n;
@@ -676,6 +685,8 @@ struct MsmTailArgs {
   XYZZ<S>* red_s[MSM_TAIL_MAX];
   const uint32_t* nnz[MSM_TAIL_MAX];
   XYZZ<S>* out[MSM_TAIL_MAX];
+  uint32_t* live[MSM_TAIL_MAX];
+  uint32_t target[MSM_TAIL_MAX];
 };
 
 // Zero the buckets (ZZ = 0: infinity) and the nnz counter of every tail in the batch: one launch
@@ -688,6 +699,7 @@ __global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta)
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
     b[i] = make_uint4(0, 0, 0, 0);
   if (blockIdx.x == 0 && threadIdx.x == 0) *const_cast<uint32_t*>(ta.nnz[y]) = 0;
+  if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ta.live[y][threadIdx.x] = 0;
 }
 
 template <class F, int MINW, class S = typename MsmIO<F>::S>
@@ -700,8 +712,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   uint32_t* __restrict__ out_key = ta.key[y][src ^ 1];
   XYZZ<S>* __restrict__ out_val = ta.val[y][src ^ 1];
   XYZZ<S>* __restrict__ buckets = ta.buckets[y];
+  // the level before emitted no real open run: every bucket is final already
+  if (ta.live[y][level - 1] == 0u) return;
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
-  const uint32_t N = msm_items_at<S>(*ta.nnz[y], level);
+  const uint32_t N = msm_items_at<S>(*ta.nnz[y], level, ta.target[y]);
   const uint32_t q0 = g * MSM_SG;
   if (q0 >= N) return;
   const uint32_t q1 = q0 + MSM_SG < N ? q0 + MSM_SG : N;
@@ -710,7 +724,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   const uint32_t knext = q1 < N ? (in_key[q1] & KM) : 0xFFFFFFFFu;
   uint32_t* okey = out_key + 2 * g;
   XYZZ<S>* oval = out_val + 2 * g;
-  bool slot0 = false, slot1 = false, real = false;
+  bool slot0 = false, slot1 = false, real = false, open = false;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t kq = in_key[q0];
   uint32_t cur = kq & KM, run_start = q0;
@@ -722,8 +736,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
     const bool last = q + 1 == q1;
     if (last || (kn & KM) != cur) {
-      msm_emit_run<F>(cur, acc, real, run_start == q0 && kprev == cur, last && knext == cur, buckets, okey, oval,
-                      slot0, slot1);
+      const bool ol = run_start == q0 && kprev == cur, orr = last && knext == cur;
+      msm_emit_run<F>(cur, acc, real, ol, orr, buckets, okey, oval, slot0, slot1);
+      open = open || (real && (ol || orr));
       acc = xyzz_inf<F>();
       real = false;
       cur = kn & KM;
@@ -733,6 +748,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   }
   if (!slot0) okey[0] = (in_key[q0] & KM) | MSM_ITEM_DUMMY;
   if (!slot1) okey[1] = (in_key[q1 - 1] & KM) | MSM_ITEM_DUMMY;
+  if (level < MSM_LIVE_LEVELS) msm_mark_live(ta.live[y], level, open);
 }
 
 // Weighted bucket reduction sum_b (b+1) S_b.  An item i stands for a group of g = 2^log2g
@@ -892,10 +908,34 @@ void msm_scratch_free(MsmScratch<F>& s) {
   s = MsmScratch<F>();
 }
 
+// Accumulation lanes (chunks) the device holds at once for this curve's k_msm_accumulate: the
+// occupancy of its 64-thread blocks x the CUs x chunks per block (0 when unknown: fixed L).
+template <class F>
+uint32_t msm_resident_chunks() {
+#if !MSM_ADAPTIVE_L
+  return 0;
+#else
+  if constexpr (std::is_same<F, FqOps>::value)
+    if (MSM_G1_AFFINE) return 0;  // the batch-affine rounds use the fixed L
+  // tests: ZKFL_MSM_TARGET=<chunks> forces a small target, so small MSMs run long chunks too
+  if (const char* e = getenv("ZKFL_MSM_TARGET")) return (uint32_t)strtoul(e, nullptr, 10);
+  using FC = typename MsmCompute<F>::type;
+  constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
+  int dev = 0, ncu = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_msm_accumulate<FC, AW>, 64, 0) != hipSuccess) return 0;
+  if (ncu <= 0 || nb <= 0) return 0;
+  return (uint32_t)ncu * (uint32_t)nb * (64u / MsmIO<FC>::LANES);
+#endif
+}
+
 template <class F>
 hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
   const size_t m = cap * MSM_W;
+  t.target = msm_resident_chunks<F>();
   t.max_chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  if (t.target) t.max_chunks = std::min<size_t>(t.max_chunks, t.target);  // msm_chunk_len bounds the lanes
   t.item_cap[0] = 2 * t.max_chunks;
   t.item_cap[1] = 2 * ((t.item_cap[0] + MSM_SG - 1) / MSM_SG);
   for (int k = 0; k < 2; k++) {
@@ -906,12 +946,14 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
   ZK_CHECK(hipMalloc(&t.red_a, 2 * MSM_RB * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.red_s, 2 * MSM_RB * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.nnz, sizeof(uint32_t)));
+  ZK_CHECK(hipMalloc(&t.live, MSM_LIVE_LEVELS * sizeof(uint32_t)));
   return hipSuccess;
 }
 
 template <class F>
 void msm_tail_free(MsmTail<F>& t) {
-  void* ptrs[] = {t.item_key[0], t.item_key[1], t.item_val[0], t.item_val[1], t.buckets, t.red_a, t.red_s, t.nnz};
+  void* ptrs[] = {t.item_key[0], t.item_key[1], t.item_val[0], t.item_val[1], t.buckets, t.red_a, t.red_s, t.nnz,
+                  t.live};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   t = MsmTail<F>();
@@ -930,6 +972,8 @@ MsmTailArgs<F> msm_tail_args(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n) 
     ta.red_s[i] = t[i]->red_s;
     ta.nnz[i] = t[i]->nnz;
     ta.out[i] = outs ? outs[i] : nullptr;
+    ta.live[i] = t[i]->live;
+    ta.target[i] = t[i]->target;
   }
   return ta;
 }
@@ -991,7 +1035,8 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
                                  hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
   if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
-  const size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  if (t.target) chunks = std::min<size_t>(chunks, t.target);  // lanes of msm_chunk_len(nnz, target)
   if (chunks > t.max_chunks) return hipErrorInvalidValue;
   const int pidx = prof ? prof->begin(tag, st) : -1;
   using FC = typename MsmCompute<F>::type;
@@ -1001,12 +1046,13 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
   if constexpr (std::is_same<F, FqOps>::value) {
     if (MSM_G1_AFFINE && t.aff && t.aff->lanes && !(ZK_KNOCKOUT & 64)) {  // batch-affine rounds
       ZK_CHECK(msm_aff_accumulate<MSM_G1_AFF_WAVES>(b, keys, vals, t, *t.aff, st));
+      ZK_CHECK(hipMemsetAsync(t.live, 1, 1, st));  // it does not track open runs: stitch every level
       done = true;
     }
   }
   if (!done && !((ZK_KNOCKOUT & 64) && LN == 1))
     hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, keys, vals,
-                       b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets);
+                       b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, t.target, t.live);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
   return hipGetLastError();
 }
@@ -1039,6 +1085,7 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   N = std::max<size_t>(N, 2);
   int cur = 0;
   for (int level = 1; !(ZK_KNOCKOUT & 8); level++) {
+    if (level >= MSM_LIVE_LEVELS) return hipErrorInvalidValue;  // liveness flags per level
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
     hipLaunchKernelGGL((k_msm_stitch<FC, SW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
     if (N <= (size_t)MSM_SG) break;

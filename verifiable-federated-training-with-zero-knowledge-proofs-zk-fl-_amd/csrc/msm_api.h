@@ -72,6 +72,25 @@ template <>
 struct MsmChunk<Fq2Ops> {
   static constexpr int L = MSM_G2_L;
 };
+// 1 (default): the chunk length grows with the MSM so that one accumulation launch is ONE full
+// round of resident lanes (msm_chunk_len); 0: every MSM uses MsmChunk<S>::L (A/B builds).
+#ifndef MSM_ADAPTIVE_L
+#define MSM_ADAPTIVE_L 1
+#endif
+// Entries per accumulation lane for an MSM with nnz sorted non-zero digits: the minimum
+// MsmChunk<S>::L, or the fewest that keep the lanes within `target` = the lanes the device holds
+// at once for the accumulation kernel (0: always the minimum).  A longer chunk leaves fewer chunk
+// edges inside a bucket, and every such edge costs one full point addition in the stitching;
+// the launch stays one full round of lanes, so the accumulation's own duration does not change.
+// The accumulation and the stitching levels derive the same value from nnz on the device.
+template <class S>
+__host__ __device__ inline uint32_t msm_chunk_len(uint32_t nnz, uint32_t target) {
+  constexpr uint32_t L0 = MsmChunk<S>::L;
+  if (target == 0) return L0;
+  const uint32_t l = (uint32_t)(((uint64_t)nnz + target - 1) / target);
+  return l > L0 ? l : L0;
+}
+constexpr int MSM_LIVE_LEVELS = 32;  // stitching levels with a liveness flag (level 0 = accumulation)
 
 
 // Read-only, per proving key: every base expanded into its W window copies.
@@ -129,6 +148,10 @@ struct MsmTail {
   XYZZ<F>* red_a = nullptr;     // weighted-reduction block outputs
   XYZZ<F>* red_s = nullptr;
   uint32_t* nnz = nullptr;      // number of non-zero digits of the last run (device)
+  // live[l] != 0: level l (0 = the accumulation) emitted a real open run, so level l + 1 has
+  // something to stitch; a level whose predecessor emitted none returns at once (device)
+  uint32_t* live = nullptr;
+  uint32_t target = 0;          // accumulation lanes resident at once (msm_chunk_len; 0: fixed L)
   const MsmAffScratch* aff = nullptr;  // G1: batch-affine scratch to accumulate with (not owned)
 };
 

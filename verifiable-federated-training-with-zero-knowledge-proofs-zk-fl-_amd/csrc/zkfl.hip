@@ -39,6 +39,7 @@
 #include "merkle.h"
 #include "msm_api.h"
 #include "ntt.h"
+#include "pairing.h"
 #include "prof.h"
 #include "setup.h"
 #include "verify.h"
@@ -562,21 +563,46 @@ __global__ void __launch_bounds__(64) k_part_out(const G1P* __restrict__ res, co
   else if (lane == 4) st_xyzz_std<Fq2Ops>(resB2[0], out + PART_OFF[4]);
 }
 
+// A part's point crossed a process boundary: it must be infinity (ZZ = ZZZ = 0) or a well-formed
+// XYZZ point of the curve y^2 = x^3 + b: ZZ, ZZZ != 0, ZZ^3 = ZZZ^2 and (with x = X/ZZ, y = Y/ZZZ,
+// multiplied through by ZZ^3 = ZZZ^2) Y^2 = X^3 + b ZZ^3.  A malformed one (say ZZ = 1, ZZZ = 0)
+// would otherwise reach the assembly's inversions.
+template <class F>
+ZK_DEV bool xyzz_part_ok(const XYZZ<F>& p, const typename F::T& b) {
+  const bool zz0 = F::is_zero(p.ZZ), zzz0 = F::is_zero(p.ZZZ);
+  if (zz0 || zzz0) return zz0 && zzz0;
+  const typename F::T zz3 = F::mul(F::sqr(p.ZZ), p.ZZ);
+  if (!F::eq(zz3, F::sqr(p.ZZZ))) return false;
+  return F::eq(F::sqr(p.Y), F::add(F::mul(F::sqr(p.X), p.X), F::mul(b, zz3)));
+}
+
 // block b sums the n_parts parts of proof b (parts[b][j]) into res[5b + {0, 1, 2, 3}] (A', B1', C',
-// H) and resB2[b]: lanes 0..3 the G1 points, lane 4 the G2 point, a serial sum over the world size
+// H) and resB2[b]: lanes 0..3 the G1 points, lane 4 the G2 point, a serial sum over the world size.
+// A point that is not on its curve sets *bad (and is left out).
 __global__ void __launch_bounds__(64) k_parts_sum(const uint32_t* __restrict__ parts, int n_parts,
-                                                  G1P* __restrict__ res, G2P* __restrict__ resB2) {
+                                                  G1P* __restrict__ res, G2P* __restrict__ resB2,
+                                                  uint32_t* __restrict__ bad) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const uint32_t* p = parts + (size_t)b * n_parts * PART_WORDS;
   if (lane < 4) {
+    Fq b3;
+#pragma unroll
+    for (int i = 0; i < 8; i++) b3.v[i] = FQ_THREE[i];
     G1P acc = xyzz_inf<FqOps>();
-    for (int j = 0; j < n_parts; j++)
-      acc = xyzz_add<FqOps>(acc, ld_xyzz_std<FqOps>(p + j * PART_WORDS + PART_OFF[lane]));
+    for (int j = 0; j < n_parts; j++) {
+      const G1P q = ld_xyzz_std<FqOps>(p + j * PART_WORDS + PART_OFF[lane]);
+      if (xyzz_part_ok<FqOps>(q, b3)) acc = xyzz_add<FqOps>(acc, q);
+      else *bad = 1u;
+    }
     res[5 * b + lane] = acc;
   } else if (lane == 4) {
+    const Fq2 bt = load_fq2(TWIST_B);
     G2P acc = xyzz_inf<Fq2Ops>();
-    for (int j = 0; j < n_parts; j++)
-      acc = xyzz_add<Fq2Ops>(acc, ld_xyzz_std<Fq2Ops>(p + j * PART_WORDS + PART_OFF[4]));
+    for (int j = 0; j < n_parts; j++) {
+      const G2P q = ld_xyzz_std<Fq2Ops>(p + j * PART_WORDS + PART_OFF[4]);
+      if (xyzz_part_ok<Fq2Ops>(q, bt)) acc = xyzz_add<Fq2Ops>(acc, q);
+      else *bad = 1u;
+    }
     resB2[b] = acc;
   }
 }
@@ -705,6 +731,10 @@ struct zkfl_key {
   // the extra pointer = the slot's h vector, whose extra slots 1, r, s, -rs follow it).  bC / bH
   // stay for the parity hook (zkfl_debug_prove_parts returns C and H apart).
   MsmBases<FqOps> bCH;
+  // the parity hook's zeros (zkfl_debug_prove_parts, first call): with C and H merged it runs the
+  // C + H MSM twice, once with a zero h (C alone) and once with a zero witness (H alone), so the key
+  // holds no separate C and H bases (they were ~0.5 GB of expanded bases per key at 2^18)
+  Fr* dbg_zero = nullptr;
   bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
@@ -773,7 +803,8 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * MSM_W * sizeof(uint32_t), st));
   }
 #endif
-  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), k->bH.n};
+  // tail 3 is H's; with C and H merged only the parity hook uses it, for the C + H MSM
+  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), std::max(k->bH.n, k->bCH.n)};
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
@@ -887,6 +918,7 @@ void key_release(zkfl_key* k) {
   msm_bases_free_g1(k->bH);
   msm_bases_free_g1(k->bCH);
   msm_bases_free_g2(k->bB2);
+  if (k->dbg_zero) (void)hipFree(k->dbg_zero);
   ntt_plan_free(k->ntt);
   void* ptrs[] = {k->rows, k->cols, k->coefs};
   for (void* p : ptrs)
@@ -942,7 +974,11 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
   // C + H as one MSM into tail 2 (res[2] = C' + H, res[3] = infinity); the parity hook (plain)
   // keeps them apart
-  const bool merge = MSM_MERGE_CH && plain != 1 && k->bCH.n > 0;
+  const bool merge = MSM_MERGE_CH && plain != 1;
+  // the parity hook on merged bases: C = the C + H MSM over (witness, zero h), H = over (zero witness, h)
+  const bool split_ch = MSM_MERGE_CH && plain == 1;
+  if (split_ch && !k->dbg_zero) return fail(ZKFL_E_ARG, "parity hook: zeros not allocated");
+  const uint32_t* Z = (const uint32_t*)k->dbg_zero;
   const int ntails = merge ? 3 : 4;
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
@@ -976,7 +1012,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   } else {
     HIP_TRY(msm_accumulate_g1(k->bB1, sB, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   }
-  if (!merge) HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
+  if (split_ch)
+    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, Z, st, prof, "msm_accumulate_g1"), "msm C");
+  else if (!merge)
+    HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
   int pi = prof->begin("abc", st);
   if (k->K) {
     const uint32_t K = (uint32_t)k->K;
@@ -999,6 +1038,9 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(msm_accumulate_g1(k->bCH, sCH, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
     HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
+  } else if (split_ch) {
+    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[3], Z, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+            "msm H");
   } else {
     HIP_TRY(msm_accumulate_g1(k->bH, s->g1s, s->g1t[3], (const uint32_t*)s->h, nullptr, st, prof, "msm_accumulate_g1"),
             "msm H");
@@ -1057,6 +1099,12 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     Job J;
     rc = job(i, J);
     if (rc) break;
+    if (J.key->nshards != 1 && !J.part_out) {  // its MSMs are one shard's share: no whole proof
+      rc = fail(ZKFL_E_ARG, "this key is shard " + std::to_string(J.key->shard) + " of " +
+                                std::to_string(J.key->nshards) +
+                                " of a split proof: prove parts (zkfl_groth16_prove_part_batch) and assemble them");
+      break;
+    }
     uint32_t rsl[16];
     rc = get_rs(J.rs, rsl);
     if (rc) break;
@@ -1474,8 +1522,8 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
     // B_i(tau) G1 and B_i(tau) G2 vanish together in an honest zkey; the sort is shared only when
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
-    if (e == hipSuccess) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
-    if (e == hipSuccess) e = build(k->bH, 64, z.secH, dom, 0, {}, h_identity);
+    if (e == hipSuccess && !MSM_MERGE_CH) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
+    if (e == hipSuccess && !MSM_MERGE_CH) e = build(k->bH, 64, z.secH, dom, 0, {}, h_identity);
     if (e == hipSuccess && MSM_MERGE_CH) {
       // C (private wires -> the witness) then H (h_j -> extra[j], the slot's h vector), then
       // delta1 with -rs (extra[dom + 3]: the extra slots sit behind h)
@@ -1653,10 +1701,11 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
   }
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   hipStream_t st = ctx->st;
-  // one device buffer, carved: parts | res (5 G1P per proof) | resB2 | GLV halves | proofs
+  // one device buffer, carved: parts | res (5 G1P per proof) | resB2 | GLV halves | proofs | bad flag
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_res = up(n * n_parts * PART_WORDS * 4), o_b2 = o_res + up(n * 5 * sizeof(G1P)),
-               o_ks = o_b2 + up(n * sizeof(G2P)), o_pf = o_ks + up(ks.size()), total = o_pf + n * 256;
+               o_ks = o_b2 + up(n * sizeof(G2P)), o_pf = o_ks + up(ks.size()), o_bad = o_pf + up(n * 256),
+               total = o_bad + 4;
   if (total > ctx->asm_cap) {
     if (ctx->asm_buf) (void)hipFree(ctx->asm_buf);
     ctx->asm_buf = nullptr;
@@ -1666,15 +1715,23 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
   }
   uint8_t* base = static_cast<uint8_t*>(ctx->asm_buf);
   void *d_parts = base, *d_res = base + o_res, *d_b2 = base + o_b2, *d_ks = base + o_ks, *d_proof = base + o_pf;
+  uint32_t* d_bad = reinterpret_cast<uint32_t*>(base + o_bad);
+  uint32_t bad = 0;
   hipError_t e = hipMemcpyAsync(d_parts, parts, n * n_parts * PART_WORDS * 4, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(d_ks, ks.data(), ks.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, st);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_parts_sum, dim3((uint32_t)n), dim3(64), 0, st, (const uint32_t*)d_parts, (int)n_parts,
-                       (G1P*)d_res, (G2P*)d_b2);
-    hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n), dim3(192), 0, st, (const G1P*)d_res, (const G2P*)d_b2,
-                       (const GlvScalar*)d_ks, (uint32_t*)d_proof);
+                       (G1P*)d_res, (G2P*)d_b2, d_bad);
     e = hipGetLastError();
   }
+  if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "assemble");
+  if (bad) return fail(ZKFL_E_ARG, "assemble: a part holds a point that is not on its curve");
+  hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n), dim3(192), 0, st, (const G1P*)d_res, (const G2P*)d_b2,
+                     (const GlvScalar*)d_ks, (uint32_t*)d_proof);
+  e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(proofs_out, d_proof, n * 256, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "assemble");
@@ -1991,6 +2048,12 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   ProofSlot* s = nullptr;
   rc = get_slot(key, 0, &s);
   uint32_t zeros[16] = {0};
+  if (rc == ZKFL_OK && MSM_MERGE_CH && !key->dbg_zero) {  // see zkfl_key::dbg_zero
+    const size_t bytes = std::max<size_t>(key->nVars, (size_t)key->n + 4) * 32;
+    hipError_t e = hipMalloc(&key->dbg_zero, bytes);
+    if (e == hipSuccess) e = hipMemset(key->dbg_zero, 0, bytes);
+    if (e != hipSuccess) rc = hip_fail(e, "parity hook zeros");
+  }
   if (rc == ZKFL_OK && s->busy) rc = wait_slot(s);
   if (rc == ZKFL_OK) {
     s->out_proof = nullptr;

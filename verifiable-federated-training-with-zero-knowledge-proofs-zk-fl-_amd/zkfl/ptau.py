@@ -44,6 +44,9 @@ N8 = 32
 G1_SIZE = 64
 G2_SIZE = 128
 MAX_POWER = 28
+# prepare phase2 needs a 2^(power + 1) Lagrange block of tauG1 and the GPU group iFFT stops at 2^28
+# (zkfl_setup_g1_lagrange): a power-28 file is a valid phase-1 transcript but cannot be prepared
+MAX_PHASE2_POWER = 27
 
 # generators, standard form (ffjavascript bn128 G1.g / G2.g)
 G1_GEN = (1, 2)
@@ -227,6 +230,9 @@ def prepare_phase2(buf, ctx) -> bytes:
     of every 2^p prefix of sections 2..5 (p = 0..power, and p = power + 1 for tauG1 with its last,
     absent power replaced by the point at infinity)."""
     pt = Ptau(buf)
+    if pt.power > MAX_PHASE2_POWER:  # before any GPU work (ADVICE r3)
+        raise ValueError(f"prepare phase2: power {pt.power} > {MAX_PHASE2_POWER}: its 2^{pt.power + 1} tauG1 "
+                         f"Lagrange block exceeds the GPU group FFT's 2^28")
     secs = [(t, pt.section(t)) for t in range(1, 8)]
     for src, dst, g2 in ((2, 12, False), (3, 13, True), (4, 14, False), (5, 15, False)):
         lag = ctx.g2_lagrange if g2 else ctx.g1_lagrange
