@@ -57,3 +57,28 @@ def test_accumulation_kernels_do_not_spill(acc):
     for name, r in res.items():
         assert r.get("vgpr_spill_count", 0) == 0 and r.get("private_segment_fixed_size", 0) == 0, (name, r)
         assert r["group_segment_fixed_size"] == 8192, (name, r)  # two 4 KB LDS-DMA buffers per wave
+
+
+def test_no_function_clobbers_its_return_address():
+    """Round-3 G2 ceremony hang (commit 68f6c67), root cause found on the CPU from the pre-fix code
+    object: the outlined smul_xyzz<Fq2Ops> / smul_aff<Fq2Ops> (333 / 276 KB, past the +-128 KB
+    reach of s_branch) got long branches `s_getpc_b64 s[30:31]; s_add_u32 s30 ..; s_setpc_b64
+    s[30:31]` that used the return-address pair as scratch, so the final `s_setpc_b64 s[30:31]`
+    jumped back into the loop and the waves never finished.  No non-kernel function of the shipped
+    library may write s[30:31]."""
+    if not os.path.exists(SO):
+        pytest.skip("libzkfl.so not built")
+    fns = isa_check.functions(SO)
+    assert fns, "the pairing helpers are outlined (csrc/pairing.h ZK_NOINLINE): expected functions"
+    bad = {n: isa_check.return_address_clobbers(ls) for n, ls in fns.items()}
+    assert not {n: b for n, b in bad.items() if b}, bad
+
+
+def test_return_address_checker_flags_the_r03_code():
+    """The checker on an excerpt of the round-3 smul_xyzz<Fq2Ops> disassembly (its entry up to the
+    first long branch, and its end): the long branch writes s[30:31], then the 'return' uses it."""
+    path = os.path.join(ROOT, "tests", "golden", "isa_r03_smul_xyzz_g2_excerpt.s")
+    lines = [ln.strip() for ln in open(path) if ln.strip() and ln.strip() != "..."]
+    got = isa_check.return_address_clobbers(lines)
+    assert any(g.startswith("s_getpc_b64 s[30:31]") for g in got)
+    assert lines[-1].startswith("s_setpc_b64 s[30:31]")

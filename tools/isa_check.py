@@ -19,6 +19,9 @@ writes and dropped the vmcnt wait of the accumulation loop's first iteration (cs
 k_msm_accumulate); the MSM primitive tests passed by timing.  tests/test_isa.py runs this on
 both accumulation kernels.
 
+  * functions(so) / return_address_clobbers(lines): non-kernel functions that write s[30:31], the
+    return address (the round-3 G2 ceremony hang, commit 68f6c67; see return_address_clobbers).
+
     python3 tools/isa_check.py [path/to/libzkfl.so]
 """
 from __future__ import annotations
@@ -114,13 +117,14 @@ def lds_dma_hazards(lines: list[str]) -> list[str]:
         base = a if base is None else base
         ins.append((a - base, ln.split("//")[0].strip()))
     index = {off: i for i, (off, _) in enumerate(ins)}
+    src = [ln for ln in lines if _ADDR.search(ln)]  # ins[i] is src[i] (its branch-target annotation)
     # basic-block leaders: the entry, branch targets, instructions after a branch
     succ_of: dict[int, list[int]] = {}
     leaders = {0}
     for i, (off, text) in enumerate(ins):
         op = text.split()[0] if text else ""
         if op.startswith("s_cbranch") or op == "s_branch":
-            t = _TARGET.search(lines[[j for j, ln in enumerate(lines) if _ADDR.search(ln)][i]])
+            t = _TARGET.search(src[i])
             tgt = index.get(int(t.group(1), 16)) if t else None
             succ_of[i] = ([tgt] if tgt is not None else []) + ([i + 1] if op != "s_branch" else [])
             if tgt is not None:
@@ -166,6 +170,44 @@ def lds_dma_hazards(lines: list[str]) -> list[str]:
     return bad
 
 
+def functions(so: str) -> dict[str, list[str]]:
+    """Non-kernel functions (called by s_swappc) of every gfx950 code object: {symbol: lines}."""
+    out: dict[str, list[str]] = {}
+    for co in code_objects(so):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f.name], check=True,
+                                   capture_output=True, text=True).stdout
+        kernels = set(re.findall(r"\.name:\s+(\S+)", notes))
+        cur = None
+        for ln in _objdump(co, "-d", "--mcpu=gfx950").splitlines():
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:$", ln)
+            if m:
+                cur = None if m.group(1) in kernels else m.group(1)
+                if cur:
+                    out[cur] = []
+                continue
+            if cur and ln.strip():
+                out[cur].append(ln.strip())
+    return out
+
+
+_RA_WRITE = re.compile(r"^(s_getpc_b64|s_mov_b64|s_add_u32|s_addc_u32|s_mov_b32|s_load_dwordx2)\s+s(\[30:31\]|30\b|31\b)")
+
+
+def return_address_clobbers(lines: list[str]) -> list[str]:
+    """Writes of s[30:31] -- the return address of the AMDGPU calling convention -- inside a
+    non-kernel function.  The round-3 G2 ceremony hang (commit 68f6c67): the outlined 215 KB
+    smul_xyzz<Fq2Ops> / smul_aff<Fq2Ops> were past the +-128 KB reach of s_branch, and the long
+    branches the compiler expanded them into (s_getpc_b64 s[30:31]; s_add_u32 s30 ...;
+    s_setpc_b64 s[30:31]) took s[30:31] as their scratch pair without saving it, so the function's
+    final `s_setpc_b64 s[30:31]` "returned" to the last long-branch target inside the loop: the
+    waves never left.  A function here may restore s[30:31] from a save before it returns; this
+    flags every write so such a case is looked at, and there is none in the current library."""
+    return [ln.split("//")[0].strip() for ln in lines if _RA_WRITE.match(ln)]
+
+
 def main() -> int:
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     so = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
@@ -183,6 +225,13 @@ def main() -> int:
         rc |= bool(bad)
     for name, r in resources(so, r"k_msm_(accumulate|stitch|wsum)|k_assemble").items():
         print(name[:60], r)
+    for name, lines in functions(so).items():
+        bad = return_address_clobbers(lines)
+        addrs = [int(m.group(1), 16) for m in map(_ADDR.search, lines) if m]
+        size = (addrs[-1] - addrs[0] + 8) if addrs else 0
+        print(f"function {name[:70]}: {len(lines)} instructions, {size // 1024} KB "
+              f"(s_branch reaches +-128 KB), {len(bad)} writes of the return address s[30:31]")
+        rc |= bool(bad)
     return rc
 
 

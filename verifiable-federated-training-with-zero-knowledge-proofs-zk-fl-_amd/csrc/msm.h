@@ -32,6 +32,7 @@
 
 #include "field29.h"
 #include "msm_api.h"
+#include "wtrace.h"
 
 namespace zkfl {
 
@@ -399,6 +400,8 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint3
                                                                    const uint32_t* __restrict__ sidx,
                                                                    uint32_t extra_start, size_t n, size_t per_blk,
                                                                    uint32_t* __restrict__ cnt) {
+  ZK_WT(WT_SORT_COUNT);
+  ZK_LIGHT();
   __shared__ uint32_t h[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
   __syncthreads();
@@ -418,6 +421,8 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint3
 static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* __restrict__ cnt, uint32_t nblk,
                                                                    uint32_t* __restrict__ bin_start,
                                                                    uint32_t* __restrict__ nnz) {
+  ZK_WT(WT_SORT_SCAN);
+  ZK_LIGHT();
   __shared__ uint32_t c[MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_BT];  // +1 word per 32: no bank conflicts
   __shared__ uint32_t part[MSM_SORT_BT];
   const uint32_t total = MSM_SORT_HB * nblk, t = threadIdx.x;
@@ -461,6 +466,8 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
     const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra, const uint32_t* __restrict__ sidx,
     uint32_t extra_start, size_t n, size_t per_blk, const uint32_t* __restrict__ cnt, uint16_t* __restrict__ keys,
     uint32_t* __restrict__ vals) {
+  ZK_WT(WT_SORT_SCATTER);
+  ZK_LIGHT();
   __shared__ uint32_t cur[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
@@ -479,6 +486,8 @@ static __global__ void __launch_bounds__(MSM_SORT_BINT) k_msm_bin_sort(const uin
                                                                    const uint32_t* __restrict__ tv,
                                                                    uint16_t* __restrict__ ko,
                                                                    uint32_t* __restrict__ vo) {
+  ZK_WT(WT_SORT_BINS);
+  ZK_LIGHT();
   __shared__ uint32_t c[MSM_SORT_NL];
   const uint32_t b0 = bin_start[blockIdx.x], b1 = bin_start[blockIdx.x + 1], t = threadIdx.x;
   if (b0 == b1) return;
@@ -575,6 +584,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<S>* __restrict__ bases,
     const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
     XYZZ<S>* __restrict__ buckets, uint32_t target, uint32_t* __restrict__ live) {
+  ZK_WT(WT_ACC | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
   using IO = MsmIO<F>;
   constexpr bool PF = sizeof(typename S::T) == 32 ? MSM_G1_PREFETCH : MSM_G2_PREFETCH;
   const size_t c = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
@@ -693,6 +703,8 @@ struct MsmTailArgs {
 // for all MSMs of a proof instead of two memsets each.
 template <class S>
 __global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta) {
+  ZK_WT(WT_TAIL_RESET | (sizeof(typename S::T) == 32 ? 0u : WT_G2));
+  ZK_LIGHT();
   const int y = blockIdx.y;
   uint4* b = reinterpret_cast<uint4*>(ta.buckets[y]);
   constexpr size_t nv = MSM_NB * sizeof(XYZZ<S>) / sizeof(uint4);
@@ -705,6 +717,8 @@ __global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta)
 template <class F, int MINW, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
     const MsmTailArgs<S> ta, int level, int src) {
+  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
   using IO = MsmIO<F>;
   const int y = blockIdx.y;
   const uint32_t* __restrict__ in_key = ta.key[y][src];
@@ -777,6 +791,8 @@ static_assert(MSM_NB % (MSM_RB * MSM_G1_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G
 template <class F, int MINW, bool L0, class S = typename MsmIO<F>::S>
 __global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
 k_msm_wsum(const MsmTailArgs<S> ta) {
+  ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
   // One kernel per level (template L0): level 0 keeps only the running sums R, W live through its
   // fold, level 1 has no fold at all, so neither carries the other's registers.
   const int yb = blockIdx.y;
@@ -1111,6 +1127,7 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
 
 // Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
 #define ZKFL_MSM_DEFINE(SUF, F)                                                                          \
+  hipError_t zk_wtrace_bind_##SUF(const WtBuf& b) { return zk_wtrace_bind_tu(b); }                      \
   hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n) { return msm_bases_alloc(b, n); }           \
   hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,          \
                                  uint32_t extra_start, hipStream_t st) {                                 \

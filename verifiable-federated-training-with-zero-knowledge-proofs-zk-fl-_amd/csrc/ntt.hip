@@ -1,6 +1,7 @@
 // NTT kernels (see ntt.h for the algorithm and the reference behaviour it replaces).
 #include "ntt.h"
 #include "fr_consts.h"
+#include "wtrace.h"
 
 namespace zkfl {
 
@@ -128,6 +129,8 @@ __global__ void __launch_bounds__(512) k_ntt_lds(Fr* __restrict__ a, size_t n, i
 __global__ void __launch_bounds__(512) k_ntt_lds_pair(Fr* __restrict__ a, size_t n, int logt,
                                                       const Fr* __restrict__ tw_inv, const Fr* __restrict__ tw_fwd,
                                                       int nvec, size_t vstride, const Fr* __restrict__ scale) {
+  ZK_WT(WT_NTT_LDS);
+  ZK_LIGHT();
   __shared__ Fr tile[NTT_LDS_N];
   const size_t T = (size_t)1 << logt;
   const size_t tiles_per_vec = n >> logt;
@@ -254,6 +257,8 @@ constexpr int NTT_COL_TILE = 1 << NTT_COL_TILE_LOG;
 template <bool DIF>
 __global__ void __launch_bounds__(256) k_ntt_cols(Fr* __restrict__ a, int logn, int k, const Fr* __restrict__ tw,
                                                   int nvec, size_t vstride) {
+  ZK_WT(DIF ? WT_NTT_COLS_INV : WT_NTT_COLS_FWD);
+  ZK_LIGHT();
   __shared__ Fr tile[NTT_COL_TILE];
   const size_t n = (size_t)1 << logn;
   const int lowlog = logn - k;                 // column stride 2^lowlog
@@ -433,5 +438,7 @@ __global__ void k_bitrev_copy(const Fr* __restrict__ in, Fr* __restrict__ out, s
   size_t q = logn ? (__brevll((unsigned long long)p) >> (64 - logn)) : 0;
   out[q] = in[p];
 }
+
+hipError_t zk_wtrace_bind_ntt(const WtBuf& b) { return zk_wtrace_bind_tu(b); }
 
 }  // namespace zkfl

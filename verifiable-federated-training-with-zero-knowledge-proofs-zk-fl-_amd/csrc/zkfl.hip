@@ -44,6 +44,7 @@
 #include "setup.h"
 #include "verify.h"
 #include "witness.h"
+#include "wtrace.h"
 #include "zkfl.h"
 
 using namespace zkfl;
@@ -118,6 +119,8 @@ template <bool PACKED>
 __global__ void __launch_bounds__(64) k_abc_chunks(const uint32_t* __restrict__ rp, uint32_t nrows, AbcTerms T,
                                                    const Fr* __restrict__ w, uint32_t K, Fr* __restrict__ head,
                                                    Fr* __restrict__ tail, Fr* __restrict__ abc) {
+  ZK_WT(WT_ABC);
+  ZK_LIGHT();
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t p0 = c * ABC_L;
   if (p0 >= K) return;
@@ -196,6 +199,8 @@ __device__ __forceinline__ Fr abc_row(const uint32_t* __restrict__ rp, uint32_t 
 __global__ void __launch_bounds__(256) k_abc_rows(const uint32_t* __restrict__ rp, size_t n, uint32_t K,
                                                   const Fr* __restrict__ head, const Fr* __restrict__ tail,
                                                   Fr* __restrict__ abc) {
+  ZK_WT(WT_ABC_ROWS);
+  ZK_LIGHT();
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const Fr a = abc_row(rp, (uint32_t)j, K, head, tail, abc);
@@ -207,6 +212,8 @@ __global__ void __launch_bounds__(256) k_abc_rows(const uint32_t* __restrict__ r
 
 // h = a*b - c (coset evaluations), to standard form for the H MSM.
 __global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h) {
+  ZK_WT(WT_JOIN);
+  ZK_LIGHT();
   size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
 #if ZK_KNOCKOUT & 4
@@ -222,6 +229,8 @@ __global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h)
 // Blinding scalar slots referenced by the compacted bases' index maps (std form):
 // extra = [1, r, s, -r*s].  plain -> all zero (parity hook: pure MSMs).
 __global__ void k_set_extra(const Fr* __restrict__ rs, Fr* __restrict__ extra, int plain) {
+  ZK_WT(WT_SET_EXTRA);
+  ZK_LIGHT();
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Fr one = fp_zero<FrP>();
   one.v[0] = plain ? 0u : 1u;
@@ -435,6 +444,8 @@ ZK_DEV Affine<Fq2Ops> g2_to_affine_bgcd(const G2P& p) {
 // quad operations run in the 29-bit engine (Q29, canonical values), every inversion is a binary GCD.
 __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                   const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
+  ZK_WT(WT_ASSEMBLE);
+  ZK_LIGHT();
   // one block per proof: block b reads res[5b..], resB2[b], ks[4b..] and writes proof[64b..]
   res += 5 * blockIdx.x;
   resB2 += blockIdx.x;
@@ -678,6 +689,7 @@ struct zkfl_ctx {
   PosTables* pos = nullptr;  // Poseidon constants of every width (first hashing call)
   void* asm_buf = nullptr;   // zkfl_groth16_assemble's device buffers (grown on demand, reused)
   size_t asm_cap = 0;
+  WtBuf wt;                  // wave-timeline records (ZK_WTRACE builds, zkfl_debug_wtrace)
 };
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
@@ -1364,6 +1376,9 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
   vk_free(ctx->vk);
   pos_tables_free(ctx->pos);
   if (ctx->asm_buf) (void)hipFree(ctx->asm_buf);
+  if (ctx->wt.rec) {  // a wave trace still bound: unbind before its buffer goes
+    (void)zkfl_debug_wtrace(ctx, 0, 0, nullptr, nullptr);
+  }
   (void)hipStreamDestroy(ctx->st);
   delete ctx;
   return ZKFL_OK;
@@ -2038,6 +2053,51 @@ int zkfl_groth16_prove(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t
   }
   zkfl_witness_free(w);
   return rc;
+}
+
+int zkfl_debug_wtrace(zkfl_ctx* ctx, int op, uint32_t cap, void* out, uint32_t* count) {
+#if !ZK_WTRACE
+  (void)ctx;
+  (void)op;
+  (void)cap;
+  (void)out;
+  (void)count;
+  return fail(ZKFL_E_ARG, "wave trace: this library was built without -DZK_WTRACE=1");
+#else
+  if (!ctx || op < 0 || op > 2) return fail(ZKFL_E_ARG, "wave trace: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  auto bind_all = [](const WtBuf& b) {
+    hipError_t e = zk_wtrace_bind_tu(b);
+    if (e == hipSuccess) e = zk_wtrace_bind_g1(b);
+    if (e == hipSuccess) e = zk_wtrace_bind_g2(b);
+    if (e == hipSuccess) e = zk_wtrace_bind_ntt(b);
+    return e;
+  };
+  HIP_TRY(hipDeviceSynchronize(), "wave trace: sync");
+  if (op == 2) {
+    if (!ctx->wt.rec) return fail(ZKFL_E_ARG, "wave trace: not started");
+    uint32_t n = 0;
+    HIP_TRY(hipMemcpy(&n, ctx->wt.cnt, 4, hipMemcpyDeviceToHost), "wave trace: count");
+    HIP_TRY(bind_all(WtBuf()), "wave trace: unbind");
+    const uint32_t m = std::min(n, std::min(cap, ctx->wt.cap));
+    if (out && m) HIP_TRY(hipMemcpy(out, ctx->wt.rec, (size_t)m * sizeof(WtRec), hipMemcpyDeviceToHost), "wave trace: read");
+    if (count) *count = n;
+    return ZKFL_OK;
+  }
+  HIP_TRY(bind_all(WtBuf()), "wave trace: unbind");
+  if (ctx->wt.rec) (void)hipFree(ctx->wt.rec);
+  if (ctx->wt.cnt) (void)hipFree(ctx->wt.cnt);
+  ctx->wt = WtBuf();
+  if (op == 0) return ZKFL_OK;
+  if (cap == 0) return fail(ZKFL_E_ARG, "wave trace: cap must be > 0");
+  HIP_TRY(hipMalloc(&ctx->wt.rec, (size_t)cap * sizeof(WtRec)), "wave trace: alloc");
+  HIP_TRY(hipMalloc(&ctx->wt.cnt, 4), "wave trace: alloc");
+  HIP_TRY(hipMemset(ctx->wt.cnt, 0, 4), "wave trace: reset");
+  ctx->wt.cap = cap;
+  HIP_TRY(bind_all(ctx->wt), "wave trace: bind");
+  HIP_TRY(hipDeviceSynchronize(), "wave trace: sync");
+  return ZKFL_OK;
+#endif
 }
 
 int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, size_t wtns_len, uint8_t* h_out,

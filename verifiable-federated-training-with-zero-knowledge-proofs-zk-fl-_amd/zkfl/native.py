@@ -55,6 +55,7 @@ SIGNATURES = {
     "zkfl_groth16_prove_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_debug_prove_parts": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, _U8P, _U8P]),
     "zkfl_debug_glv_split": (C.c_int, [C.c_char_p, _U8P]),
+    "zkfl_debug_wtrace": (C.c_int, [_P, C.c_int, C.c_uint32, _P, C.POINTER(C.c_uint32)]),
     "zkfl_msm_g1": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_msm_g2": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_ntt_coset": (C.c_int, [_P, _U8P, C.c_uint32]),
@@ -226,6 +227,20 @@ class Context:
 
     def synchronize(self):
         check(lib().zkfl_ctx_synchronize(self.h))
+
+    # wave timeline (libraries built with -DZK_WTRACE=1; tools/wtrace.py)
+    def wtrace_start(self, cap: int):
+        check(lib().zkfl_debug_wtrace(self.h, 1, cap, None, None))
+
+    def wtrace_stop(self, cap: int) -> tuple[bytes, int]:
+        """-> (min(count, cap) records of 24 B, count recorded)"""
+        buf = C.create_string_buffer(24 * cap)
+        n = C.c_uint32(0)
+        check(lib().zkfl_debug_wtrace(self.h, 2, cap, buf, C.byref(n)))
+        return buf.raw[:24 * min(n.value, cap)], n.value
+
+    def wtrace_free(self):
+        check(lib().zkfl_debug_wtrace(self.h, 0, 0, None, None))
 
     # primitives
     def msm_g1(self, bases: bytes, scalars: bytes) -> bytes:
