@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -120,6 +121,89 @@ def verify_all(ctx, zk, proofs, pubs_of):
     npub = len(pubs_of(0)) // 32
     ok = ctx.verify_batch(vk, pubs, b"".join(proofs), npub)
     return sum(ok)
+
+
+def cli_leg(ctx, runs, names=("C2", "M")):
+    """Like-for-like with how the reference proves (Report Table 3's 6.8 s is one
+    `snarkjs groth16 prove` CLI invocation): the harness's exact command
+    `npx snarkjs groth16 prove <c>_final.zkey <w>.wtns <proof>.json <public>.json`
+    (tests/full_system_simulation.mjs:773-776, one child process per proof, cwd = the circuit dir),
+    resolved offline by npm to this package's shim (node/snarkjs_shim.js -> N-API -> C ABI), run
+    `runs` times per circuit; the witness comes from the harness's generate_witness.cjs string
+    (:758-763).  Per circuit: median wall clock of the command and the median of each stage
+    (npx and node start, libzkfl + HIP runtime load, HIP context, zkey read, key load -- parse,
+    QAP upload, base upload + 16x window expansion per query, first proof slot --, wtns read, GPU
+    prove, JSON write) from the shim's and the library's timing marks (ZKFL_CLI_TIMING,
+    ZKFL_LOAD_TIMING).  Every CLI proof is checked by the GPU batch verifier."""
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    from zkfl import clients, groth16
+    if not shutil.which("node") or not shutil.which("npm"):
+        return {"skipped": "node / npm not found"}
+    med = statistics.median
+    tmp = tempfile.mkdtemp(prefix="zkfl_cli_")
+    env = dict(os.environ, PYTHONPATH=PKG_DIR + os.pathsep + os.environ.get("PYTHONPATH", ""))
+
+    def run(cmd, cwd, extra=None):
+        p = subprocess.run(cmd, cwd=cwd, shell=True, capture_output=True, text=True, timeout=300,
+                           env=dict(env, **(extra or {})))
+        if p.returncode != 0:
+            raise RuntimeError(f"{cmd}: {p.stderr[-400:]}")
+        return p
+    try:
+        with open(os.path.join(tmp, "package.json"), "w") as f:
+            json.dump({"name": "harness", "version": "1.0.0", "private": True,
+                       "dependencies": {"zkfl-snarkjs": "file:" + PKG_DIR}}, f)
+        run("npm install --offline --no-audit --no-fund", tmp)
+        out = {"command": "npx snarkjs groth16 prove <c>_final.zkey <w>.wtns <proof>.json <public>.json",
+               "reference": "tests/full_system_simulation.mjs:773-776", "runs": runs}
+        for cname in names:
+            name, params = CIRCUITS[cname]
+            circ = os.path.join(tmp, cname)
+            os.makedirs(circ)
+            ps = " ".join(str(x) for x in params)
+            py = sys.executable
+            run(f"{py} -m zkfl compile {name} {ps} --name {name} --circom-layout -o .", circ)
+            run(f"{py} -m zkfl setup {name} {ps} --name {name} -o .", circ)
+            batch, dim, depth, precision = params
+            inp = clients.Client(1, batch, dim, depth, clients.JsLcg(12345)).training_input(batch, precision,
+                                                                                             100000000)[0]
+            with open(os.path.join(circ, "input.json"), "w") as f:
+                json.dump(inp, f)
+            t = time.perf_counter()
+            run(f'node "{name}_js/generate_witness.cjs" "{name}_js/{name}.wasm" "input.json" "w.wtns"', circ)
+            wit_ms = (time.perf_counter() - t) * 1e3
+            cli_t, load_t = os.path.join(circ, "cli.jsonl"), os.path.join(circ, "load.jsonl")
+            walls = []
+            for i in range(runs):
+                t = time.perf_counter()
+                run(f"npx snarkjs groth16 prove {name}_final.zkey w.wtns proof{i}.json public{i}.json", circ,
+                    {"ZKFL_CLI_TIMING": cli_t, "ZKFL_LOAD_TIMING": load_t})
+                walls.append((time.perf_counter() - t) * 1e3)
+            zk = open(os.path.join(circ, name + "_final.zkey"), "rb").read()
+            proofs = [groth16.proof_from_json(json.load(open(os.path.join(circ, f"proof{i}.json"))))
+                      for i in range(runs)]
+            pubs = [b"".join(int(x).to_bytes(32, "little") for x in json.load(open(os.path.join(circ, f"public{i}.json"))))
+                    for i in range(runs)]
+            verified = verify_all(ctx, zk, proofs, lambda i: pubs[i])
+            marks = [dict(json.loads(ln)["marks"]) for ln in open(cli_t)]
+            loads = [json.loads(ln) for ln in open(load_t)]
+            seq = ["entry", "addon", "context", "zkey_read", "key_load", "wtns_read", "prove", "json_write", "exit"]
+            stages = {"npx_and_node_start": med(w - m["exit"] + m["entry"] for w, m in zip(walls, marks))}
+            for a, b_ in zip(seq, seq[1:]):
+                stages[{"addon": "libzkfl_and_hip_runtime_load", "context": "hip_context"}.get(b_, b_)] = \
+                    med(m[b_] - m[a] for m in marks)
+            key_load = {k[:-3]: round(med(ld[k] for ld in loads), 2) for k in loads[0] if k.endswith("_ms")}
+            out[cname] = {"circuit": f"{name}{params}", "zkey_MB": round(len(zk) / 1e6, 1),
+                          "median_ms": round(med(walls), 1), "min_ms": round(min(walls), 1),
+                          "verified": verified, "witness_cli_ms": round(wit_ms, 1),
+                          "stages_ms": {k: round(v, 1) for k, v in stages.items()},
+                          "key_load_stages_ms": key_load}
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist, zk, expect_pubs):
@@ -229,7 +313,9 @@ def roofline(prof, key, traffic=True, nprof=1):
     fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
     clk, clk_src = _measured_clock(dom) if collect else (None, "not collected for this leg")
     peak_clk = FQMUL_PEAK_GPS * clk / 2.4 if clk else None
-    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+    # "bound" stays the roofline of record (north_star: HBM bandwidth fraction); "binding" names the
+    # one that limits this kernel: the integer VALU issue rate (the "valu" object below)
+    return {"bound": "hbm", "binding": "valu", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes": round(algo), "query_length": round(q),
             "impl_bytes": round(impl), "impl_GBps": round(impl / avg_s / 1e9, 1) if avg_s > 0 else 0.0,
@@ -285,12 +371,22 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
                 ok += sum(ctx.verify_batch(vks[nm], pubs, b"".join(p for p, _ in sel), keys[nm].n_public))
         return _sum_over_ranks(ok, dist)
 
-    def timed(js):
+    cpu = {}
+
+    def timed(js, tag):
+        # host CPU time of this process (every thread: the C parse workers, the launching thread,
+        # the HIP runtime's) over the timed region, per proof proved here
         _barrier(ctx, dist)
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t_start = time.perf_counter()
         out = run(js)
         _barrier(ctx, dist)
-        return _max_over_ranks(time.perf_counter() - t_start, dist), out
+        dt = time.perf_counter() - t_start
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        busy = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        cpu[tag] = {"host_cpu_ms_per_proof": round(busy * 1e3 / max(1, len(js)), 3),
+                    "host_cpu_cores_busy": round(busy / dt, 2)}
+        return _max_over_ranks(dt, dist), out
 
     all_jobs = jobs_of(rounds + 1, 1)                  # round 0 = warm-up
     mine = [j for k, j in enumerate([j for j in all_jobs if j[0] > 0]) if k % world == rank]
@@ -298,7 +394,7 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
     log(f"[bench r{rank}] c5: keys for {[(nm, b.n_constraints) for nm, b in circ.items()]}, "
         f"{len(mine)} of {rounds * 16} proofs on this rank ({time.perf_counter() - t0:.1f} s)")
     run(warm)
-    elapsed, out = timed(mine)
+    elapsed, out = timed(mine, "strong")
     ok = verified(mine, out)
     if ok != rounds * 16:
         raise SystemExit(f"[bench r{rank}] c5: {rounds * 16 - ok} proofs do not verify")
@@ -308,18 +404,18 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
     strong = {"value": round(rounds * 16 / elapsed, 3), "unit": "proofs/s", "proofs": rounds * 16, "verified": ok,
               "rounds": rounds, "ms_per_round": round(elapsed / rounds * 1e3, 3), "scaling": "strong",
               "workload": workload + "; proof k -> GPU k mod G",
-              "constraints": {nm: b.n_constraints for nm, b in circ.items()}}
+              "constraints": {nm: b.n_constraints for nm, b in circ.items()}, **cpu["strong"]}
     weak = None
     if weak_rounds:
         mine_w = jobs_of(weak_rounds, 1 + 8 * rank)     # this GPU's own 8 clients, every round
-        elapsed_w, out_w = timed(mine_w)
+        elapsed_w, out_w = timed(mine_w, "weak")
         ok_w = verified(mine_w, out_w)
         total = world * weak_rounds * 16
         if ok_w != total:
             raise SystemExit(f"[bench r{rank}] c5 weak: {total - ok_w} proofs do not verify")
         weak = {"value": round(total / elapsed_w, 3), "unit": "proofs/s", "proofs": total, "verified": ok_w,
                 "rounds_per_gpu": weak_rounds, "clients_per_gpu": 8, "scaling": "weak",
-                "ms_per_round": round(elapsed_w / weak_rounds * 1e3, 3),
+                "ms_per_round": round(elapsed_w / weak_rounds * 1e3, 3), **cpu["weak"],
                 "workload": workload + "; 8 clients per GPU (ids 8 x rank + 1..8), every GPU proves its own rounds"}
     for x in list(progs.values()) + list(keys.values()):
         x.close()
@@ -572,6 +668,18 @@ def report(args, world, elapsed, n_timed_all, verified_all, prof, nprof, key, co
         "stage_ms_isolated_per_proof": stage_ms,
     }
     line.update(extra)
+    # whole-proof VALU efficiency: every accumulated MSM entry of a proof (G1: 10 Fq products, G2:
+    # 30) at the timed throughput, against the same ISA ceiling -- the accumulations' share of the
+    # chip's multiply issue, with every other stage (sort, stitching, reduction, NTT, ABC, assembly)
+    # counted as overhead
+    if line.get("roofline") and nprof:
+        fq = sum(prof[k][2] / nprof * FQMUL_PER_ENTRY[k] for k in FQMUL_PER_ENTRY if k in prof)
+        achieved = fq * line["value"] / 1e9
+        clk = line["roofline"]["valu"].get("measured_clock_GHz")
+        line["roofline"]["whole_proof_valu"] = {
+            "fq_mul_equivalents_per_proof": round(fq), "achieved": round(achieved, 2), "unit": "G Fq-mul/s",
+            "frac": round(achieved / FQMUL_PEAK_GPS, 4),
+            "frac_at_measured_clock": round(achieved / (FQMUL_PEAK_GPS * clk / 2.4), 4) if clk else None}
     return line
 
 
@@ -590,10 +698,13 @@ def main():
                     help="config-5 weak-scaling leg: federated rounds of 8 own clients per GPU (0: skip)")
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     ap.add_argument("--extra-circuit", default="M19", help="second training-circuit size leg ('' or none: skip)")
-    ap.add_argument("--extra-steps", type=int, default=4, help="timed steps of the extra-circuit leg")
+    ap.add_argument("--extra-steps", type=int, default=16,
+                    help="timed steps of the extra-circuit leg (16 x 20 proofs: over 1 s, VERDICT r3)")
     ap.add_argument("--c5-slots", type=int, default=8, help="proof slots per key in the config-5 legs")
     ap.add_argument("--split-proofs", type=int, default=8,
                     help="split-proof leg: proofs, one at a time, each split over all ranks (0: skip)")
+    ap.add_argument("--cli-runs", type=int, default=5,
+                    help="cli_prove leg: `npx snarkjs groth16 prove` invocations per circuit (0: skip; 1 GPU only)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -695,6 +806,13 @@ def main():
     if args.split_proofs:  # last: the other legs never run beside a second (shard) key
         split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
         log(f"[bench r{rank}] split proof: {split_res}")
+    cli = None
+    if args.cli_runs and world == 1:
+        try:
+            cli = cli_leg(ctx, args.cli_runs)
+        except Exception as e:  # noqa: BLE001
+            cli = {"error": str(e)[-300:]}
+        log(f"[bench r{rank}] cli prove: {cli}")
     if rank == 0:
         cpu, oracle_match = None, None
         if world == 1 and not args.no_cpu_baseline:
@@ -714,7 +832,7 @@ def main():
                       {"n_gpus": devices_used, "ranks": world, "build_id": build_id,
                        "build_matches_sources": build_id == source_id, "oracle_match": oracle_match,
                        "end_to_end": e2e, "c5": c5, "c5_weak": c5w, "extra_circuit": extra,
-                       "dataset_commit": merkle, "split_proof": split_res, "cpu_baseline": cpu})
+                       "dataset_commit": merkle, "split_proof": split_res, "cli_prove": cli, "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")

@@ -2,8 +2,9 @@
 # Same-box throughput A/B of library variants (GPU box).  Variants alternate round by round, so a
 # drift of the box's clock hits every variant alike; each run is one tools/ko_probe.py line.
 #   bash tools/ab.sh TAG ROUNDS VARIANT... [-- PROBE_ARGS...]
-# VARIANT: "cur" = the in-tree libzkfl.so, otherwise build_ab/<VARIANT>/libzkfl.so
-# (tools/build_ab.sh NAME "-DKNOB=..." builds one on the CPU first).
+# VARIANT: LIB[+VAR=VALUE...]; LIB "cur" = the in-tree libzkfl.so, otherwise build_ab/<LIB>/libzkfl.so
+# (tools/build_ab.sh NAME "-DKNOB=..." builds one on the CPU first); +VAR=VALUE sets an environment
+# knob for that variant's runs (e.g. cur+ZKFL_STAGGER=1).
 # Output: gpurun_out/TAG/ab.log (every line) and a per-variant summary (mean, min, max, spread).
 # A run that fails, times out or crashes ends the script (nothing is retried).
 set -o pipefail
@@ -19,8 +20,11 @@ mkdir -p "$OUT"
 cd "$R"
 for r in $(seq 1 "$ROUNDS"); do
   for v in "${VARS[@]}"; do
-    if [ "$v" = cur ]; then lib=""; else lib=build_ab/$v/libzkfl.so; fi
-    line=$(ZKFL_LIB=$lib timeout -k 10 180 python -u tools/ko_probe.py "${PROBE[@]}" 2>>"$OUT/stderr.log" | tail -n 1)
+    IFS=+ read -r -a parts <<< "$v"
+    base=${parts[0]}
+    if [ "$base" = cur ]; then lib=""; else lib=build_ab/$base/libzkfl.so; fi
+    line=$(env ZKFL_LIB="$lib" "${parts[@]:1}" timeout -k 10 180 python -u tools/ko_probe.py "${PROBE[@]}" \
+           2>>"$OUT/stderr.log" | tail -n 1)
     rc=$?
     [ $rc -ne 0 ] && { echo "$v round $r failed (rc $rc)"; exit $rc; }
     echo "$v $line" | tee -a "$OUT/ab.log"

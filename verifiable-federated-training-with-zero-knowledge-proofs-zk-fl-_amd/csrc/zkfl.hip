@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -715,6 +716,7 @@ struct ProofSlot {
   uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
   uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (768 at 512)
   bool busy = false;
+  int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
   uint8_t* out_proof = nullptr;   // where its 256 proof bytes go (nullable)
   uint8_t* out_part = nullptr;    // split proofs: where the 768 part bytes go (nullable)
@@ -845,6 +847,7 @@ int get_slot(zkfl_key* k, size_t idx, ProofSlot** out) {
       slot_release(s);
       return hip_fail(e, "proof slot allocation");
     }
+    s->index = (int)k->slots.size();
     k->slots.push_back(s);
   }
   *out = k->slots[want];
@@ -992,6 +995,13 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   if (split_ch && !k->dbg_zero) return fail(ZKFL_E_ARG, "parity hook: zeros not allocated");
   const uint32_t* Z = (const uint32_t*)k->dbg_zero;
   const int ntails = merge ? 3 : 4;
+  // Stage order.  Every slot runs the same chain, so under load the slots move as a convoy: the
+  // accumulations fill the GPU one at a time, and the slots that leave them together reach ABC +
+  // NTT together -- the wave timeline (tools/wtrace.py) showed stretches of ~4 ms with no
+  // accumulation resident at all.  ZKFL_STAGGER=1: odd slots run ABC + NTT before their
+  // witness-scalar MSMs instead of after, so their light phase falls beside the others' heavy one.
+  static const int stagger = getenv("ZKFL_STAGGER") ? atoi(getenv("ZKFL_STAGGER")) : 0;
+  const bool light_first = stagger && (s->index & 1) && !prof->serialize;
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
   const bool share = k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32);
@@ -1001,6 +1011,28 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
       HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
     HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   }
+  // ABC (a, b, c on the domain), the coset NTT of all three and h = a b - c (std form, the H MSM scalars)
+  auto abc_ntt = [&]() -> int {
+    int pi = prof->begin("abc", st);
+    if (k->K) {
+      const uint32_t K = (uint32_t)k->K;
+      const AbcTerms T = {k->cols, k->coefs, k->cshift};
+      if (k->cshift)
+        hipLaunchKernelGGL(k_abc_chunks<true>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                           (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+      else
+        hipLaunchKernelGGL(k_abc_chunks<false>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                           (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+    }
+    hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
+                       s->abc_tail, s->abc);
+    prof->end(pi, st, (double)k->K);
+    pi = prof->begin("ntt", st);
+    if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
+    prof->end(pi, st, 3.0 * (double)n);
+    hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
+    return ZKFL_OK;
+  };
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   HIP_TRY(msm_tails_reset_g1(tails, ntails, st), "msm reset");
 #if ZK_KNOCKOUT & 2
@@ -1008,6 +1040,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
 #else
   MsmScratch<FqOps>&sA = s->g1s, &sB = s->g1s, &sCH = s->g1s;
 #endif
+  if (light_first) {
+    const int rc = abc_ntt();
+    if (rc) return rc;
+  }
   HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   if (share) {
     MsmTail<Fq2Ops>* t2 = &s->g2t;
@@ -1028,24 +1064,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, Z, st, prof, "msm_accumulate_g1"), "msm C");
   else if (!merge)
     HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
-  int pi = prof->begin("abc", st);
-  if (k->K) {
-    const uint32_t K = (uint32_t)k->K;
-    const AbcTerms T = {k->cols, k->coefs, k->cshift};
-    if (k->cshift)
-      hipLaunchKernelGGL(k_abc_chunks<true>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
-                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
-    else
-      hipLaunchKernelGGL(k_abc_chunks<false>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
-                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+  if (!light_first) {
+    const int rc = abc_ntt();
+    if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
-                     s->abc_tail, s->abc);
-  prof->end(pi, st, (double)k->K);
-  pi = prof->begin("ntt", st);
-  if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
-  prof->end(pi, st, 3.0 * (double)n);
-  hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
   if (merge) {
     HIP_TRY(msm_accumulate_g1(k->bCH, sCH, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
@@ -1419,12 +1441,23 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
                    zkfl_key** out) {
   if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
   if (nshards < 1 || nshards > 1024 || shard >= nshards) return fail(ZKFL_E_ARG, "shard must be < n_shards <= 1024");
+  // ZKFL_LOAD_TIMING=<file>: one JSON line per load with the host-side stages (bench.py cli_prove)
+  const char* timing_path = getenv("ZKFL_LOAD_TIMING");
+  std::vector<std::pair<std::string, double>> marks;
+  auto t_last = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!timing_path) return;
+    const auto t = std::chrono::steady_clock::now();
+    marks.emplace_back(what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   ZkeyHost z;
   {
     std::string err;
     int rc = zkey_parse(buf, len, z, err);  // csrc/host_parse.cc: header, sections, CSR + dictionary
     if (rc) return fail(rc, err);
   }
+  mark("parse");
   const uint32_t nVars = z.nVars, nPub = z.nPub, dom = z.dom;
   const int logn = z.logn;
   const size_t nC = z.nC;
@@ -1468,6 +1501,8 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
     KTRY(hipMemcpyAsync(k->cols, cols.data(), (size_t)ncoef * 4, hipMemcpyHostToDevice, st), "upload");
     KTRY(hipMemcpyAsync(k->coefs, coefs.data(), ncoefs_dev * 32, hipMemcpyHostToDevice, st), "upload");
   }
+  if (timing_path) KTRY(hipStreamSynchronize(st), "sync");
+  mark("qap_upload");
   // MSM bases: infinity points dropped (e.g. ~1/3 of B1/B2 for Poseidon-heavy circuits: x^4
   // wires never appear in B), plus augmentation slots alpha1/delta1 (A), beta1/delta1 (B1),
   // beta2/delta2 (B2), delta1 (C) whose scalars are the proof's extra = [1, r, s, -rs]
@@ -1530,10 +1565,13 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
       return e;
     };
     hipError_t e = build(k->bA, 64, z.secA, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
+    mark("bases_A");
     if (e == hipSuccess)
       e = build(k->bB1, 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false, &sidx_b1);
+    mark("bases_B1");
     if (e == hipSuccess)
       e = build(k->bB2, 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false, &sidx_b2);
+    mark("bases_B2");
     // B_i(tau) G1 and B_i(tau) G2 vanish together in an honest zkey; the sort is shared only when
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
@@ -1570,15 +1608,31 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (d_img) (void)hipFree(d_img);
     }
+    mark("bases_CH");
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
+  if (timing_path) KTRY(hipStreamSynchronize(st), "sync");
+  mark("ntt_plan");
   {
     ProofSlot* s0 = nullptr;
     int rc0 = get_slot(k, 0, &s0);  // first slot eagerly: surfaces OOM at load time
     if (rc0) return cleanup(rc0);
   }
   KTRY(hipStreamSynchronize(st), "sync");
+  mark("first_slot");
+  if (timing_path) {
+    if (FILE* f = fopen(timing_path, "a")) {
+      double total = 0;
+      fprintf(f, "{\"bytes\": %zu", len);
+      for (auto& m : marks) {
+        fprintf(f, ", \"%s_ms\": %.3f", m.first.c_str(), m.second);
+        total += m.second;
+      }
+      fprintf(f, ", \"total_ms\": %.3f}\n", total);
+      fclose(f);
+    }
+  }
 #undef KTRY
   *out = k;
   return ZKFL_OK;

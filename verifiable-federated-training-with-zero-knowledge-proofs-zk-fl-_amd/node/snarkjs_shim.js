@@ -23,10 +23,23 @@
 //   const vKey = await zKey.exportVerificationKey('c_final.zkey');
 //   const info = await r1cs.info('c.r1cs');
 'use strict';
+// ZKFL_CLI_TIMING=<file>: one JSON line per invocation with the stages of the CLI (ms since this
+// node process started): bench.py's cli_prove leg breaks `npx snarkjs groth16 prove` down with it.
+const T_ENTRY = process.uptime() * 1000;
+const TIMING = process.env.ZKFL_CLI_TIMING || null;
+const marks = [['entry', T_ENTRY]];
+function mark(name) { if (TIMING) marks.push([name, process.uptime() * 1000]); }
 const fs = require('fs');
 const path = require('path');
 
 const addon = require(path.join(__dirname, 'zkfl.node'));
+mark('addon');
+if (TIMING) {
+  process.on('exit', () => {
+    mark('exit');
+    fs.appendFileSync(TIMING, JSON.stringify({ argv: process.argv.slice(2), marks }) + '\n');
+  });
+}
 
 const Q = BigInt('21888242871839275222246405745257275088696311157297823662689037894645226208583');
 let ctx = null;
@@ -70,7 +83,12 @@ function key(zkey) {
   const id = Buffer.isBuffer(zkey) ? zkey : path.resolve(zkey);
   let k = keys.get(id);
   if (!k) {
-    k = addon.loadKey(context(), read(zkey));
+    const c = context();
+    mark('context');
+    const buf = read(zkey);
+    mark('zkey_read');
+    k = addon.loadKey(c, buf);
+    mark('key_load');
     keys.set(id, k);
   }
   return k;
@@ -106,7 +124,11 @@ function inputText(input) {
 }
 
 async function prove(zkey, wtnsFile) {
-  const r = await addon.prove(context(), key(zkey), read(wtnsFile));
+  const k = key(zkey);
+  const wtns = read(wtnsFile);
+  mark('wtns_read');
+  const r = await addon.prove(context(), k, wtns);
+  mark('prove');
   return { proof: proofToJson(r.proof), publicSignals: publicToJson(r.publicSignals) };
 }
 
@@ -269,7 +291,11 @@ if (require.main === module && isCeremony(process.argv.slice(2))) {
   const [cmd, sub] = a;
   const w = (f, o) => fs.writeFileSync(f, JSON.stringify(o, null, 1));
   if (cmd === 'groth16' && sub === 'prove' && a.length >= 6) {
-    done(prove(a[2], a[3]).then(({ proof, publicSignals }) => { w(a[4], proof); w(a[5], publicSignals); }));
+    done(prove(a[2], a[3]).then(({ proof, publicSignals }) => {
+      w(a[4], proof);
+      w(a[5], publicSignals);
+      mark('json_write');
+    }));
   } else if (cmd === 'groth16' && sub === 'fullprove' && a.length >= 7) {
     done(fullProve(fs.readFileSync(a[2], 'utf8'), a[3], a[4]).then(({ proof, publicSignals }) => {
       w(a[5], proof);
