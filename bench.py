@@ -237,6 +237,25 @@ def end_to_end_leg(key, wp, image, json_inputs, slots, steps, ctx, dist, zk, exp
                     "at a time, one group ahead -> GPU proofs (zkfl_groth16_full_prove_json_batch)"}
 
 
+def latency_leg(key, ws, n=24):
+    """One proof alone, as the CLI's `groth16 prove` and the API's prove run it: a batch of one takes
+    the low-latency schedule (csrc/zkfl.hip enqueue_proof_lowlat: B2 and the A/B1 tails + the
+    s pi_A + r B1 multiplications on side streams beside ABC / NTT / C + H).  Host wall clock of
+    prove_batch([w]) -- witness resident, from the call to the proof bytes in host memory --, n
+    times after a warm-up call: median, spread and the verdict's <= 4.5 ms target."""
+    import statistics
+    key.prove_batch(ws[:1])
+    ts = []
+    for i in range(n):
+        t = time.perf_counter()
+        key.prove_batch([ws[i % len(ws)]])
+        ts.append((time.perf_counter() - t) * 1e3)
+    med = statistics.median(ts)
+    return {"median_ms": round(med, 3), "min_ms": round(min(ts), 3), "max_ms": round(max(ts), 3),
+            "p90_ms": round(sorted(ts)[int(0.9 * (n - 1))], 3), "proofs": n,
+            "path": "prove_batch of one resident witness -> low-latency schedule (3 streams), host wall clock"}
+
+
 def roofline_pass(key, ctx, ws, slots, n=6):
     """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's
     streams serialized onto one), after the timed region: the roofline's average launch time."""
@@ -773,6 +792,8 @@ def main():
     verified_all = _sum_over_ranks(verified, dist)
     if verified_all != n_timed * world:
         raise SystemExit(f"[bench r{rank}] {n_timed * world - verified_all} timed proofs do not verify")
+    lat = latency_leg(key, res)
+    log(f"[bench r{rank}] one proof alone: {lat}")
     prof, nprof = roofline_pass(key, ctx, res, args.slots)
     kinfo = KeyInfo(key.n_vars, key.n_public, key.domain_size)
     e2e = None
@@ -832,7 +853,8 @@ def main():
                       {"n_gpus": devices_used, "ranks": world, "build_id": build_id,
                        "build_matches_sources": build_id == source_id, "oracle_match": oracle_match,
                        "end_to_end": e2e, "c5": c5, "c5_weak": c5w, "extra_circuit": extra,
-                       "dataset_commit": merkle, "split_proof": split_res, "cli_prove": cli, "cpu_baseline": cpu})
+                       "latency_single_proof": lat, "dataset_commit": merkle, "split_proof": split_res,
+                       "cli_prove": cli, "cpu_baseline": cpu})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")

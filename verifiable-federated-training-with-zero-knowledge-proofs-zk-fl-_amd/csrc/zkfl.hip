@@ -433,11 +433,62 @@ ZK_DEV Affine<Fq2Ops> g2_to_affine_bgcd(const G2P& p) {
   return {f2_mul(p.X, f2_sqr(iZ)), f2_mul(p.Y, iZZZ)};
 }
 
+// One quad's GLV half of the assembly's scalar multiplications: quad g < 4 of wave 0 computes
+// k_g * P_g for (s1, A'), (s2, phi(A')), (r1, B1'), (r2, phi(B1')) (res[0] = A', res[1] = B1'),
+// the GLV halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over the quad's
+// table of 1P..8P in LDS (tab: its row), each point operation evaluated by the quad.
+ZK_DEV G1Q glv_quad_mul(const G1P* __restrict__ res, const GlvScalar* __restrict__ ks, G1Q* tab, int g, int q) {
+  G1P P = res[g >> 1];
+  if (g & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
+    Fq beta;
+#pragma unroll
+    for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
+    P.X = fp_mul(P.X, fp_to_mont(beta));
+  }
+  const GlvScalar k = ks[g];
+  if (k.neg) P = xyzz_neg<FqOps>(P);
+  const G1Q P29 = g1q_from(P);
+  if (q == 0) tab[0] = P29;
+  G1Q Q = quad_dbl<Q29>(P29, q);
+  if (q == 0) tab[1] = Q;
+#pragma unroll 1
+  for (int j = 2; j < 8; j++) {
+    Q = quad_add<Q29>(Q, P29, q);
+    if (q == 0) tab[j] = Q;
+  }
+  // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
+  // d_8i .. d_8i+7, word 4 holds d_32 (the final carry)
+  uint32_t dg[5] = {0, 0, 0, 0, 0};
+  uint32_t carry = 0;
+  for (int w = 0; w < 32; w++) {
+    const uint32_t v = ((k.mag[w >> 3] >> (4 * (w & 7))) & 15u) + carry;
+    carry = v > 8 ? 1u : 0u;
+    dg[w >> 3] |= (carry ? (v - 16) & 15u : v) << (4 * (w & 7));
+  }
+  dg[4] = carry;
+  G1Q acc = qp_inf<Q29>();
+#pragma unroll 1
+  for (int w = 32; w >= 0; w--) {
+    if (w < 32)
+      for (int j = 0; j < 4; j++) acc = quad_dbl<Q29>(acc, q);
+    const int wi = w >> 3;
+    const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
+    const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
+    if (nib) {
+      const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
+      G1Q t = tab[(d < 0 ? -d : d) - 1];
+      const F29 ny = Q29::sub(Q29::zero(), t.Y);
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
+      acc = quad_add<Q29>(acc, t, q);
+    }
+  }
+  return acc;
+}
+
 // Proof assembly, one block of three waves (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
-//   wave 0, quads 0..3 (lanes 0..15): k_i * P_i for (s1, A), (s2, phi(A)), (r1, B1), (r2, phi(B1)),
-//     the GLV halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over a per-quad
-//     table of 1P..8P in LDS, each point operation evaluated by the quad (quad_dbl / quad_add);
+//   wave 0, quads 0..3 (lanes 0..15): the four GLV halves (glv_quad_mul);
 //     quad 4: C' + H meanwhile; then quads 0, 1 sum the parts and quad 0 adds C' + H and writes
 //     pi_c (one inversion) -> proof[48..63]
 //   wave 1, lane 0: pi_a affine -> proof[0..15];  wave 2, lane 0: pi_b affine -> proof[16..47]
@@ -457,51 +508,7 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 2, q = lane & 3;
   if (wave == 0 && g < 4) {
-    G1P P = res[g >> 1];
-    if (g & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
-      Fq beta;
-#pragma unroll
-      for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
-      P.X = fp_mul(P.X, fp_to_mont(beta));
-    }
-    const GlvScalar k = ks[g];
-    if (k.neg) P = xyzz_neg<FqOps>(P);
-    const G1Q P29 = g1q_from(P);
-    if (q == 0) tab[g][0] = P29;
-    G1Q Q = quad_dbl<Q29>(P29, q);
-    if (q == 0) tab[g][1] = Q;
-#pragma unroll 1
-    for (int j = 2; j < 8; j++) {
-      Q = quad_add<Q29>(Q, P29, q);
-      if (q == 0) tab[g][j] = Q;
-    }
-    // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
-    // d_8i .. d_8i+7, word 4 holds d_32 (the final carry)
-    uint32_t dg[5] = {0, 0, 0, 0, 0};
-    uint32_t carry = 0;
-    for (int w = 0; w < 32; w++) {
-      const uint32_t v = ((k.mag[w >> 3] >> (4 * (w & 7))) & 15u) + carry;
-      carry = v > 8 ? 1u : 0u;
-      dg[w >> 3] |= (carry ? (v - 16) & 15u : v) << (4 * (w & 7));
-    }
-    dg[4] = carry;
-    G1Q acc = qp_inf<Q29>();
-#pragma unroll 1
-    for (int w = 32; w >= 0; w--) {
-      if (w < 32)
-        for (int j = 0; j < 4; j++) acc = quad_dbl<Q29>(acc, q);
-      const int wi = w >> 3;
-      const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
-      const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
-      if (nib) {
-        const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
-        G1Q t = tab[g][(d < 0 ? -d : d) - 1];
-        const F29 ny = Q29::sub(Q29::zero(), t.Y);
-#pragma unroll
-        for (int i = 0; i < 9; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
-        acc = quad_add<Q29>(acc, t, q);
-      }
-    }
+    const G1Q acc = glv_quad_mul(res, ks, tab[g], g, q);
     if (q == 0) part[g] = acc;
   } else if (wave == 0 && g == 4) {  // C' + H, off the critical path
     const G1Q c = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
@@ -522,6 +529,54 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   if (wave == 0 && g == 0) {
     const G1Q C = quad_add<Q29>(quad_add<Q29>(t01, part[5], q), part[4], q);
     if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
+  }
+}
+
+// The same assembly in two launches for the low-latency schedule (enqueue_proof, one proof alone):
+// k_assemble_t runs as soon as A' and B1' are final, beside the ABC / NTT / C + H chain:
+// T = s pi_A + r B1 -> res[4] (XYZZ, Montgomery 2^256) and pi_a -> proof[0..15];
+// k_assemble_c at the end: pi_c = (C' + H) + T -> proof[48..63] and pi_b -> proof[16..47].
+// pi_c is the same point as k_assemble's (the group sum does not depend on the order), so the
+// proof bytes are identical.
+__global__ void __launch_bounds__(128) k_assemble_t(G1P* __restrict__ res, const GlvScalar* __restrict__ ks,
+                                                    uint32_t* __restrict__ proof) {
+  ZK_WT(WT_ASSEMBLE);
+  ZK_LIGHT();
+  __shared__ G1Q tab[4][8];
+  __shared__ G1Q part[6];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 2, q = lane & 3;
+  if (wave == 0 && g < 4) {
+    const G1Q acc = glv_quad_mul(res, ks, tab[g], g, q);
+    if (q == 0) part[g] = acc;
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
+  }
+  __syncthreads();
+  if (wave == 0 && g == 1) {
+    const G1Q t = quad_add<Q29>(part[2], part[3], q);
+    if (q == 0) part[5] = t;
+  }
+  G1Q t01 = qp_inf<Q29>();
+  if (wave == 0 && g == 0) t01 = quad_add<Q29>(part[0], part[1], q);
+  __syncthreads();
+  if (wave == 0 && g == 0) {
+    const G1Q T = quad_add<Q29>(t01, part[5], q);
+    if (q == 0) res[4] = g1q_to(T);
+  }
+}
+
+__global__ void __launch_bounds__(128) k_assemble_c(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                    uint32_t* __restrict__ proof) {
+  ZK_WT(WT_ASSEMBLE);
+  ZK_LIGHT();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 2, q = lane & 3;
+  if (wave == 0 && g == 0) {
+    const G1Q C = quad_add<Q29>(quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q), g1q_from(res[4]), q);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
   }
 }
 
@@ -715,6 +770,12 @@ struct ProofSlot {
   uint32_t* d_proof = nullptr;  // [64]
   uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
   uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (768 at 512)
+  // the low-latency schedule (enqueue_proof_lowlat, one proof alone): two side streams, their
+  // events (B sorted and B1 accumulated | B2 final | T = s pi_A + r B1 final) and B's own sort
+  // scratch, so C + H can sort on the main stream while B2 still reads B's pairs; made on first use
+  hipStream_t st_lat[2] = {nullptr, nullptr};
+  hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
+  MsmScratch<FqOps> g1s_b;
   bool busy = false;
   int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
@@ -788,9 +849,12 @@ void slot_release(ProofSlot* s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
-  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done})
+  for (hipStream_t st : s->st_lat)
+    if (st) (void)hipStreamSynchronize(st);
+  msm_scratch_free_g1(s->g1s_b);
+  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t st : {s->st_main, s->st_g2})
+  for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
     if (st) (void)hipStreamDestroy(st);
   delete s;
 }
@@ -970,7 +1034,101 @@ int get_rs(const uint8_t* rs, uint32_t out[16]) {
 // plain = 1 (parity hook): alpha/beta/delta/r/s terms zeroed, nothing assembled.
 // plain = 2 (split proof): the full augmentation (on shard 0's bases), no assembly; the part
 // A' | B1' | B2' | C' + H | infinity goes to pinned + 512 (zkfl_groth16_prove_part_batch).
-int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain) {
+// ABC (a, b, c on the domain), the coset NTT of all three and h = a b - c (std form: the H MSM's
+// scalars) for one proof on stream st.
+int enqueue_abc_ntt(zkfl_key* k, ProofSlot* s, const Fr* d_w, hipStream_t st, Profiler* prof) {
+  const size_t n = k->n;
+  int pi = prof->begin("abc", st);
+  if (k->K) {
+    const uint32_t K = (uint32_t)k->K;
+    const AbcTerms T = {k->cols, k->coefs, k->cshift};
+    if (k->cshift)
+      hipLaunchKernelGGL(k_abc_chunks<true>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+    else
+      hipLaunchKernelGGL(k_abc_chunks<false>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
+                         (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
+  }
+  hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
+                     s->abc_tail, s->abc);
+  prof->end(pi, st, (double)k->K);
+  pi = prof->begin("ntt", st);
+  if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
+  prof->end(pi, st, 3.0 * (double)n);
+  hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
+  return ZKFL_OK;
+}
+
+// One proof alone (a batch of one: the CLI's `groth16 prove`, the API's prove): its latency is
+// the metric, and the GPU is mostly idle along the one-stream chain, so independent stages run on
+// side streams:
+//   main : r, s, tails reset, A (sort + accumulate), B (sort into its own scratch + B1) [ev B],
+//          ABC, coset NTT, join, C + H (sort + accumulate), its tail, wait(B2, T), k_assemble_c,
+//          proof D2H [ev_done]
+//   lat0 : wait(ev B) B2 (from B's pairs) + its tail [ev B2]
+//   lat1 : wait(ev B) the tails of A and B1, k_assemble_t (T = s pi_A + r B1, pi_a) [ev T]
+// Same proof bytes as the one-stream schedule (k_assemble_t / _c form the same points).
+int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w) {
+  Profiler* prof = &ctx->prof;
+  hipStream_t st = s->st_main;
+  for (int i = 0; i < 2; i++)
+    if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
+  for (int i = 0; i < 3; i++)
+    if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
+  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
+  hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
+  hipEvent_t ev_b = s->ev_lat[0], ev_b2 = s->ev_lat[1], ev_t = s->ev_lat[2];
+  const uint32_t* W = (const uint32_t*)d_w;
+  const uint32_t* E = (const uint32_t*)s->extra;
+  MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
+  MsmTail<Fq2Ops>* t2 = &s->g2t;
+  G2P* o2 = s->resB2;
+  HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
+  HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
+  HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+  HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
+  HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
+                                   "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+  HIP_TRY(hipEventRecord(ev_b, st), "event");
+  // lat0: B2 and its tail
+  HIP_TRY(hipStreamWaitEvent(sb, ev_b, 0), "wait");
+  HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
+                                   "msm_accumulate_g2"), "msm B2");
+  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb), "msm B2 tail");
+  HIP_TRY(hipEventRecord(ev_b2, sb), "event");
+  // lat1: the tails of A and B1, then T = s pi_A + r B1 and pi_a
+  HIP_TRY(hipStreamWaitEvent(sa, ev_b, 0), "wait");
+  {
+    G1P* outs[2] = {s->res + 0, s->res + 1};
+    HIP_TRY(msm_tails_g1(tails, outs, 2, sa), "msm tails A, B1");
+  }
+  hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
+                     reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+  HIP_TRY(hipEventRecord(ev_t, sa), "event");
+  // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
+  {
+    const int rc = enqueue_abc_ntt(k, s, d_w, st, prof);
+    if (rc) return rc;
+  }
+  HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+          "msm C+H");
+  HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
+  {
+    G1P* out2 = s->res + 2;
+    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st), "msm tail C+H");
+  }
+  HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
+  HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
+  const int pa = prof->begin("assemble", st);
+  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, s->d_proof);
+  prof->end(pa, st, 1.0);
+  HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
+  return ZKFL_OK;
+}
+
+int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain,
+                  bool lowlat = false) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
@@ -983,6 +1141,14 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
           "upload r,s");
   hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain == 1);
+  if (lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT) {
+    const int rc = enqueue_proof_lowlat(ctx, k, s, d_w);
+    if (rc) return rc;
+    prof->end(pp, st, 1.0);
+    HIP_TRY(hipEventRecord(s->ev_done, st), "event");
+    HIP_TRY(hipGetLastError(), "launch");
+    return ZKFL_OK;
+  }
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
   HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
@@ -1011,28 +1177,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
       HIP_TRY(msm_run_g2(k->bB2, s->g2s, s->g2t, W, E, s->resB2, st_g2, prof, "msm_accumulate_g2"), "msm B2");
     HIP_TRY(hipEventRecord(s->ev_b2, st_g2), "event");
   }
-  // ABC (a, b, c on the domain), the coset NTT of all three and h = a b - c (std form, the H MSM scalars)
-  auto abc_ntt = [&]() -> int {
-    int pi = prof->begin("abc", st);
-    if (k->K) {
-      const uint32_t K = (uint32_t)k->K;
-      const AbcTerms T = {k->cols, k->coefs, k->cshift};
-      if (k->cshift)
-        hipLaunchKernelGGL(k_abc_chunks<true>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
-                           (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
-      else
-        hipLaunchKernelGGL(k_abc_chunks<false>, dim3(zk_grid((K + ABC_L - 1) / ABC_L, 64)), dim3(64), 0, st, k->rows,
-                           (uint32_t)(2 * n), T, d_w, K, s->abc_head, s->abc_tail, s->abc);
-    }
-    hipLaunchKernelGGL(k_abc_rows, dim3(zk_grid(n, 256)), dim3(256), 0, st, k->rows, n, (uint32_t)k->K, s->abc_head,
-                       s->abc_tail, s->abc);
-    prof->end(pi, st, (double)k->K);
-    pi = prof->begin("ntt", st);
-    if (!(ZK_KNOCKOUT & 4)) HIP_TRY(ntt_coset_shift(k->ntt, s->abc, 3, n, st), "ntt");
-    prof->end(pi, st, 3.0 * (double)n);
-    hipLaunchKernelGGL(k_join, dim3(zk_grid(n, 256)), dim3(256), 0, st, s->abc, n, s->h);
-    return ZKFL_OK;
-  };
+  auto abc_ntt = [&]() { return enqueue_abc_ntt(k, s, d_w, st, prof); };
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
   HIP_TRY(msm_tails_reset_g1(tails, ntails, st), "msm reset");
 #if ZK_KNOCKOUT & 2
@@ -1159,7 +1304,9 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
       hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
       if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
     }
-    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0);
+    // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain)
+    static const bool lowlat = !getenv("ZKFL_LOWLAT") || atoi(getenv("ZKFL_LOWLAT")) != 0;
+    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, lowlat && n == 1);
     if (rc) break;
     s->busy = true;
   }
