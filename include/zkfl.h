@@ -162,8 +162,9 @@ int zkfl_debug_glv_split(const uint8_t k[32], uint8_t out[40]);
 /* Wave-level kernel timeline (measurement only; libraries built with -DZK_WTRACE=1, otherwise every
  * op returns ZKFL_E_ARG).  op 1: start recording into a fresh device buffer of `cap` records (any
  * earlier one is freed); op 2: wait for the device, stop recording, copy min(count, cap) records of
- * 24 B {u32 kind, u32 HW_ID, u64 start, u64 end (s_memrealtime, 100 MHz)} to out (may be NULL) and
- * the number recorded (possibly > cap) to *count; op 0: free.  tools/wtrace.py reads them. */
+ * 40 B {u32 kind, u32 HW_ID, u64 start, u64 end (s_memrealtime, 100 MHz), u64 start, u64 end
+ * (s_memtime, shader clock cycles)} to out (may be NULL) and the number recorded (possibly > cap) to
+ * *count; op 0: free.  tools/wtrace.py reads them. */
 int zkfl_debug_wtrace(zkfl_ctx* ctx, int op, uint32_t cap, void* out, uint32_t* count);
 
 /* Stand-alone primitives (parity tests).  bases: mont affine; scalars: std, n x 32 B. */

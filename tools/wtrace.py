@@ -87,6 +87,12 @@ def analyse(rec, n_proofs, shares):
             "simd_share_per_wave": round(sh, 3),
             "mean_simd_share": round(float(d.sum()) * sh / (span * ticks_us) / 1024.0, 4),  # of the 1024 SIMDs
         }
+        if "c0" in rec.dtype.names:  # the shader clock the waves ran at: cycles / real time
+            cyc = (rec["c1"][m].astype(np.int64) - rec["c0"][m].astype(np.int64)).astype(np.float64)
+            real = (t1[m] - t0[m]).astype(np.float64) * 1e-8  # seconds
+            ok = real > 2e-6
+            if ok.any():
+                out["kinds"][name]["clock_GHz"] = round(float(cyc[ok].sum() / real[ok].sum() / 1e9), 3)
     # share of the window with >= 1 accumulation wave resident (G1 or G2)
     acc = (kind & 31) == 1
     ev = np.concatenate([np.stack([t0[acc], np.ones(acc.sum(), np.int64)], 1),
@@ -125,7 +131,7 @@ def main():
     key.prove_batch([res[i % 4] for i in range(2 * args.slots)])
     ctx.synchronize()
     shares = vgpr_share(native.LIB_PATH)
-    dt = np.dtype([("kind", "<u4"), ("hwid", "<u4"), ("t0", "<u8"), ("t1", "<u8")])
+    dt = np.dtype([("kind", "<u4"), ("hwid", "<u4"), ("t0", "<u8"), ("t1", "<u8"), ("c0", "<u8"), ("c1", "<u8")])
     summary = {"library": native.LIB_PATH, "slots": args.slots, "simd_share_per_wave": shares}
     cap = 80000 * (args.proofs + 4)
     # under load
@@ -165,7 +171,7 @@ def main():
         for k, v in sorted(s["kinds"].items(), key=lambda kv: -kv[1]["mean_simd_share"]):
             print(f"   {k:14s} waves/proof {v['waves_per_proof']:9.1f}  wave-ms/proof {v['wave_ms_per_proof']:9.3f}  "
                   f"mean wave {v['mean_wave_us']:8.1f} us  resident {v['mean_resident_waves']:7.1f}  "
-                  f"SIMD share {v['mean_simd_share']:.4f}")
+                  f"SIMD share {v['mean_simd_share']:.4f}  clock {v.get('clock_GHz', 0):.2f} GHz")
 
 
 if __name__ == "__main__":

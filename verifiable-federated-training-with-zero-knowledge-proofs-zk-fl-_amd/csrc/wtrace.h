@@ -1,7 +1,8 @@
 // Wave-level timeline of the prover's kernels (build flag ZK_WTRACE=1; 0, the default, compiles
-// it out).  Every instrumented kernel's waves append one record {kind, HW_ID, start, end}: the
-// start when the wave begins, the end when its last lane leaves (64-bit atomicMax), both from
-// s_memrealtime (100 MHz).  rocprofv3's kernel trace cost the 20-slot bench a third of its
+// it out).  Every instrumented kernel's waves append one record {kind, HW_ID, start, end, start
+// cycle, end cycle}: the start when the wave begins, the end when its last lane leaves (64-bit
+// atomicMax), from s_memrealtime (100 MHz) and s_memtime (shader clock) -- so each wave also gives
+// the clock it ran at.  rocprofv3's kernel trace cost the 20-slot bench a third of its
 // throughput (275 vs 420 proofs/s); these records cost one atomic and one store per wave, so the
 // timeline they give is the unperturbed one: which kernels share the GPU, how many waves each
 // keeps resident, how long a wave of each takes under load.  Records go to a device buffer that
@@ -18,7 +19,8 @@ namespace zkfl {
 
 struct WtRec {
   uint32_t kind, hwid;
-  unsigned long long t0, t1;
+  unsigned long long t0, t1;  // s_memrealtime (100 MHz)
+  unsigned long long c0, c1;  // s_memtime (shader clock cycles): (c1 - c0) / (t1 - t0) = the clock
 };
 struct WtBuf {
   WtRec* rec = nullptr;
@@ -51,13 +53,19 @@ struct WtScope {
         const unsigned long long t = wall_clock64();
         r->kind = kind;
         r->hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID: wave, SIMD, CU, SH, SE
+        const unsigned long long c = clock64();
         r->t0 = t;
         r->t1 = t;
+        r->c0 = c;
+        r->c1 = c;
       }
     }
   }
   __device__ ~WtScope() {
-    if (r) atomicMax(&r->t1, (unsigned long long)wall_clock64());
+    if (r) {
+      atomicMax(&r->t1, (unsigned long long)wall_clock64());
+      atomicMax(&r->c1, (unsigned long long)clock64());
+    }
   }
 };
 #define ZK_WT(kind) ::zkfl::WtScope zk_wt_scope_(kind)

@@ -233,11 +233,11 @@ class Context:
         check(lib().zkfl_debug_wtrace(self.h, 1, cap, None, None))
 
     def wtrace_stop(self, cap: int) -> tuple[bytes, int]:
-        """-> (min(count, cap) records of 24 B, count recorded)"""
-        buf = C.create_string_buffer(24 * cap)
+        """-> (min(count, cap) records of 40 B, count recorded)"""
+        buf = C.create_string_buffer(40 * cap)
         n = C.c_uint32(0)
         check(lib().zkfl_debug_wtrace(self.h, 2, cap, buf, C.byref(n)))
-        return buf.raw[:24 * min(n.value, cap)], n.value
+        return buf.raw[:40 * min(n.value, cap)], n.value
 
     def wtrace_free(self):
         check(lib().zkfl_debug_wtrace(self.h, 0, 0, None, None))
