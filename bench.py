@@ -131,7 +131,8 @@ def cli_leg(ctx, runs, names=("C2", "M")):
     resolved offline by npm to this package's shim (node/snarkjs_shim.js -> N-API -> C ABI), run
     `runs` times per circuit; the witness comes from the harness's generate_witness.cjs string
     (:758-763).  Per circuit: median wall clock of the command and the median of each stage
-    (npx and node start, libzkfl + HIP runtime load, HIP context, zkey read, key load -- parse,
+    (npx and node start, libzkfl + HIP runtime load, HIP context, zkey map + parse, wait for the
+    context, key load -- parse,
     QAP upload, base upload + 16x window expansion per query, first proof slot --, wtns read, GPU
     prove, JSON write) from the shim's and the library's timing marks (ZKFL_CLI_TIMING,
     ZKFL_LOAD_TIMING).  Every CLI proof is checked by the GPU batch verifier."""
@@ -190,10 +191,14 @@ def cli_leg(ctx, runs, names=("C2", "M")):
             verified = verify_all(ctx, zk, proofs, lambda i: pubs[i])
             marks = [dict(json.loads(ln)["marks"]) for ln in open(cli_t)]
             loads = [json.loads(ln) for ln in open(load_t)]
-            seq = ["entry", "addon", "context", "zkey_read", "key_load", "wtns_read", "prove", "json_write", "exit"]
+            # the shim creates the HIP context on a thread of its own while it maps + parses the key
+            # file (zkey_read); context_wait = what was left of the context's creation after that
+            seq = ["entry", "addon", "context", "zkey_read", "context_wait", "key_load", "wtns_read", "prove",
+                   "json_write", "exit"]
+            seq = [x for x in seq if all(x in m for m in marks)]
             stages = {"npx_and_node_start": med(w - m["exit"] + m["entry"] for w, m in zip(walls, marks))}
             for a, b_ in zip(seq, seq[1:]):
-                stages[{"addon": "libzkfl_and_hip_runtime_load", "context": "hip_context"}.get(b_, b_)] = \
+                stages[{"addon": "libzkfl_and_hip_runtime_load", "context": "hip_context_call"}.get(b_, b_)] = \
                     med(m[b_] - m[a] for m in marks)
             key_load = {k[:-3]: round(med(ld[k] for ld in loads), 2) for k in loads[0] if k.endswith("_ms")}
             out[cname] = {"circuit": f"{name}{params}", "zkey_MB": round(len(zk) / 1e6, 1),

@@ -81,6 +81,16 @@ int zkfl_ctx_synchronize(zkfl_ctx* ctx);
 /* Parse a snarkjs groth16 .zkey and make it device-resident (bases expanded per window).
  * The caller keeps ownership of buf. */
 int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out);
+/* The same key by path, in two steps so a host can overlap them with creating its context:
+ * zkfl_zkey_file_open maps the file (read-only) and parses it on host threads -- no device work --,
+ * zkfl_zkey_load_file makes it device-resident (= zkfl_zkey_load on the file's bytes),
+ * zkfl_zkey_file_close unmaps it (any time after the load).  snarkjs reads the key by file name:
+ * `snarkjs groth16 prove <zkey> ...` (tests/full_system_simulation.mjs:773-776); node/snarkjs_shim.js
+ * maps it while its HIP context comes up.  Errors: ZKFL_E_ARG (open / map failed), as zkfl_zkey_load. */
+typedef struct zkfl_zkey_file zkfl_zkey_file;
+int zkfl_zkey_file_open(const char* path, zkfl_zkey_file** out);
+int zkfl_zkey_load_file(zkfl_ctx* ctx, const zkfl_zkey_file* f, zkfl_key** out);
+int zkfl_zkey_file_close(zkfl_zkey_file* f);
 int zkfl_key_free(zkfl_key* key);
 int zkfl_key_info(const zkfl_key* key, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
 /* Number of proofs kept in flight by zkfl_groth16_prove_batch (1..32, default 3).  Each slot

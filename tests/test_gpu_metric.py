@@ -64,6 +64,22 @@ def test_metric_proof_and_parts_bit_exact_vs_c_oracle(metric):
         assert len(pub) == 6 and pub[0] == i + 1
 
 
+def test_metric_key_by_path_equals_key_by_bytes(metric, gpu_ctx, tmp_path):
+    """zkfl_zkey_file_open + zkfl_zkey_load_file (the CLI's path: the key file mapped and parsed
+    on host threads) make the same key as zkfl_zkey_load on its bytes: same proofs."""
+    from zkfl import native
+    _, zk, key, _, wts = metric
+    p = tmp_path / "m_final.zkey"
+    p.write_bytes(zk)
+    k2 = native.ProvingKey(gpu_ctx, str(p))
+    try:
+        assert (k2.n_vars, k2.n_public, k2.domain_size) == (key.n_vars, key.n_public, key.domain_size)
+        rs = _le(0xABCDEF) + _le(0x123457)
+        assert k2.prove(wts[0], rs) == key.prove(wts[0], rs)
+    finally:
+        k2.close()
+
+
 def test_metric_concurrent_slots_equal_single_slot(metric):
     """bench.py's concurrency (20 slots x 1 stream each over 28 HW queues): 40 proofs with
     distinct fixed (r, s) from the batch prover equal one-at-a-time proofs; 2 vs the oracle."""

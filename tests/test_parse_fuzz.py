@@ -70,3 +70,21 @@ def test_library_rejects_hostile_inputs_without_device(tmp_path):
     for doc in (b"[" * 5000, b'{"left": 1', b'{"left": 1.5, "right": 2}', b'{"left": [1], "right": 2}', b""):
         assert L.zkfl_wprog_parse_inputs(img, len(img), doc, out, 4, ctypes.byref(n)) == -1
     assert L.zkfl_wprog_parse_inputs(img, len(img), files["json"], out, 1, ctypes.byref(n)) < 0   # cap too small
+
+
+def test_zkey_file_open_parses_on_host_without_device(tmp_path):
+    """zkfl_zkey_file_open maps and parses a key by path with no device work: a good key opens
+    (and closes), a missing path is ZKFL_E_ARG, truncations and a flipped magic are format errors."""
+    from zkfl import native
+    files, paths = _corpus(tmp_path)
+    L = native.lib()
+    f = ctypes.c_void_p()
+    assert L.zkfl_zkey_file_open(paths["zkey"].encode(), ctypes.byref(f)) == 0 and f.value
+    assert L.zkfl_zkey_file_close(f) == 0
+    assert L.zkfl_zkey_file_open(str(tmp_path / "missing.zkey").encode(), ctypes.byref(f)) == -1
+    zk = files["zkey"]
+    for k, data in enumerate((zk[:len(zk) // 2], zk[:11], b"", b"zkez" + zk[4:])):
+        p = tmp_path / f"bad{k}.zkey"
+        p.write_bytes(data)
+        assert L.zkfl_zkey_file_open(str(p).encode(), ctypes.byref(f)) < -1
+    assert L.zkfl_zkey_file_close(None) == 0

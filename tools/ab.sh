@@ -34,11 +34,13 @@ python3 - "$OUT/ab.log" <<'EOF'
 import re, sys, collections
 runs = collections.defaultdict(list)
 for ln in open(sys.argv[1]):
-    m = re.match(r"(\S+) .*: ([0-9.]+) proofs/s", ln)
+    m = re.match(r"(\S+) .*: ([0-9.]+) (proofs/s|ms median)", ln)
     if m:
-        runs[m.group(1)].append(float(m.group(2)))
+        runs[m.group(1)].append((float(m.group(2)), m.group(3)))
 for v, xs in runs.items():
+    u = xs[0][1]
+    xs = [x for x, _ in xs]
     mean = sum(xs) / len(xs)
-    print(f"{v}: mean {mean:.1f} proofs/s over {len(xs)} runs, min {min(xs):.1f}, max {max(xs):.1f}, "
+    print(f"{v}: mean {mean:.3f} {u} over {len(xs)} runs, min {min(xs):.3f}, max {max(xs):.3f}, "
           f"spread {100 * (max(xs) - min(xs)) / mean:.1f}%")
 EOF

@@ -7,6 +7,8 @@ Never a benchmark of record: the proofs of a knocked-out build are wrong.
 
     ZKFL_LIB=build_ab/ko1/libzkfl.so python3 tools/ko_probe.py [--steps 48 --warmup 8 --slots 20]
     --e2e: time the input.json -> proof path (zkfl_groth16_full_prove_json_batch) instead
+    --latency N: N proofs one at a time (prove_batch of one -> the low-latency schedule); prints
+    the median host wall clock per proof
 """
 import argparse
 import os
@@ -24,6 +26,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--slots", type=int, default=20)
     ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--latency", type=int, default=0)
     args = ap.parse_args()
     from zkfl import circuits, clients, native, wprog, zkey
     b = circuits.build("sgd_verified", 128, 4, 7, 1000)
@@ -35,6 +38,19 @@ def main():
     key.set_slots(args.slots)
     wp = native.WitnessProgram(ctx, wprog.compile_program(b))
     n = args.steps * args.slots
+    if args.latency:
+        import statistics
+        res = wp.compute_resident(key, [wprog.input_bytes(b, o) for o in objs])
+        for i in range(args.warmup):
+            key.prove_batch([res[i % 4]])
+        ts = []
+        for i in range(args.latency):
+            t0 = time.perf_counter()
+            key.prove_batch([res[i % 4]])
+            ts.append((time.perf_counter() - t0) * 1e3)
+        print(f"{os.environ.get('ZKFL_LIB', 'in-tree')}: latency min {min(ts):.3f} max {max(ts):.3f}: "
+              f"{statistics.median(ts):.3f} ms median")
+        return
     if args.e2e:
         import json
         texts = [json.dumps(o) for o in objs]

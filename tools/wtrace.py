@@ -10,9 +10,10 @@ slots) and reports, over the timed window:
     duration, the mean number of its waves resident;
   * the share of the window with an accumulation kernel resident, and the mean SIMD share held by
     each kind (a wave's VGPR allocation / 512 per SIMD, from the code object: tools/isa_check.py);
-  * the same for proofs run one at a time (--isolated).
-Writes <out>/summary.json, and <out>/waves.npz (kind, t0, t1 in 10-ns ticks) for the first
---keep proofs' window.
+  * the same for proofs run one at a time (--isolated), with the last one's kernel timeline (per
+    kernel kind, the stretches in which its waves ran back to back: start, end, waves, clock).
+Writes <out>/summary.json, <out>/waves.npz (kind, t0, t1 in 10-ns ticks) for the first --keep
+proofs' window and <out>/waves_isolated.npz (every record of the isolated proofs).
 
     ZKFL_LIB=build_ab/wtrace/libzkfl.so python3 tools/wtrace.py --proofs 120 --out gpurun_out/wt
 """
@@ -109,6 +110,39 @@ def analyse(rec, n_proofs, shares):
     return out
 
 
+def proofs_of(rec, gap_us=150.0):
+    """Split a one-proof-at-a-time trace into proofs: a proof ends where no wave is resident for
+    more than gap_us (the host's turn between prove calls)."""
+    o = np.argsort(rec["t0"], kind="stable")
+    r = rec[o]
+    t0, t1 = r["t0"].astype(np.int64), r["t1"].astype(np.int64)
+    run_end = np.maximum.accumulate(t1)
+    cut = np.nonzero(t0[1:] > run_end[:-1] + int(gap_us * 100))[0] + 1
+    return np.split(r, cut)
+
+
+def gantt(rec):
+    """One proof's kernel timeline: per kind, the stretches in which its waves follow each other
+    without a gap (one launch, or launches of that kind back to back), times from the proof's start."""
+    lo = int(rec["t0"].min())
+    segs = []
+    for k in sorted(set(rec["kind"].tolist())):
+        r = rec[rec["kind"] == k]
+        r = r[np.argsort(r["t0"], kind="stable")]
+        t0, t1 = r["t0"].astype(np.int64), r["t1"].astype(np.int64)
+        run_end = np.maximum.accumulate(t1)
+        cut = np.nonzero(t0[1:] > run_end[:-1])[0] + 1
+        for part in np.split(np.arange(len(r)), cut):
+            a, b = int(t0[part].min()), int(t1[part].max())
+            cyc = float((r["c1"][part].astype(np.int64) - r["c0"][part].astype(np.int64)).sum())
+            real = float((t1[part] - t0[part]).sum()) * 1e-8
+            segs.append({"kind": kind_name(k), "start_us": round((a - lo) / 100, 1), "end_us": round((b - lo) / 100, 1),
+                         "waves": int(len(part)), "mean_wave_us": round(float((t1[part] - t0[part]).mean()) / 100, 1),
+                         "clock_GHz": round(cyc / real / 1e9, 3) if real > 0 else None})
+    segs.sort(key=lambda s: s["start_us"])
+    return segs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--proofs", type=int, default=120)
@@ -158,7 +192,12 @@ def main():
             key.prove_batch([res[i % 4]])
         ctx.synchronize()
         raw, n = ctx.wtrace_stop(80000 * (args.isolated + 1))
-        summary["isolated"] = analyse(np.frombuffer(raw, dtype=dt), args.isolated, shares)
+        rec = np.frombuffer(raw, dtype=dt)
+        summary["isolated"] = analyse(rec, args.isolated, shares)
+        np.savez_compressed(os.path.join(args.out, "waves_isolated.npz"), rec=rec)
+        ps = proofs_of(rec)
+        summary["isolated"]["proof_spans_us"] = [round((int(p["t1"].max()) - int(p["t0"].min())) / 100, 1) for p in ps]
+        summary["isolated"]["gantt_last"] = gantt(ps[-1])
     ctx.wtrace_free()
     with open(os.path.join(args.out, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
@@ -172,6 +211,11 @@ def main():
             print(f"   {k:14s} waves/proof {v['waves_per_proof']:9.1f}  wave-ms/proof {v['wave_ms_per_proof']:9.3f}  "
                   f"mean wave {v['mean_wave_us']:8.1f} us  resident {v['mean_resident_waves']:7.1f}  "
                   f"SIMD share {v['mean_simd_share']:.4f}  clock {v.get('clock_GHz', 0):.2f} GHz")
+    if "gantt_last" in summary.get("isolated", {}):
+        print("== isolated proof spans (us):", summary["isolated"]["proof_spans_us"])
+        for g in summary["isolated"]["gantt_last"]:
+            print(f"   {g['kind']:14s} {g['start_us']:8.1f} .. {g['end_us']:8.1f} us  waves {g['waves']:6d}  "
+                  f"mean wave {g['mean_wave_us']:7.1f} us  clock {g['clock_GHz']} GHz")
 
 
 if __name__ == "__main__":

@@ -3,10 +3,12 @@
 // zkfl/wprog.py's witness-program image, and circom's input.json (generate_witness.cjs, :758-767).
 #include "host_parse.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <cctype>
-#include <unordered_map>
+#include <algorithm>
+#include <thread>
 
 #include "zkfl.h"
 
@@ -320,6 +322,154 @@ int wtns_parse(const uint8_t* buf, size_t len, WtnsView& out, std::string& err) 
   return ZKFL_OK;
 }
 
+// Coefficient dictionary: open addressing over the 32-byte values (a circuit's coefficients take
+// few distinct values -- 1971 over the metric circuit's 7.0 M terms).
+struct CoefDict {
+  std::vector<uint32_t> slot;  // id + 1, 0 = empty
+  std::vector<uint32_t> vals;  // 8 u32 per id
+  uint32_t mask = 0;
+  CoefDict() { rehash(1024); }
+  uint32_t size() const { return (uint32_t)(vals.size() / 8); }
+  static uint32_t hash(const uint32_t* v) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int i = 0; i < 8; i++) h = (h ^ v[i]) * 0x100000001B3ull;
+    return (uint32_t)(h ^ (h >> 31));
+  }
+  void rehash(uint32_t cap) {
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    for (uint32_t id = 0; id < size(); id++) {
+      uint32_t i = hash(&vals[(size_t)id * 8]) & mask;
+      while (slot[i]) i = (i + 1) & mask;
+      slot[i] = id + 1;
+    }
+  }
+  uint32_t intern(const uint8_t* p) {
+    uint32_t v[8];
+    memcpy(v, p, 32);
+    uint32_t i = hash(v) & mask;
+    for (;; i = (i + 1) & mask) {
+      const uint32_t e = slot[i];
+      if (!e) break;
+      if (memcmp(&vals[(size_t)(e - 1) * 8], v, 32) == 0) return e - 1;
+    }
+    const uint32_t id = size();
+    vals.insert(vals.end(), v, v + 8);
+    slot[i] = id + 1;
+    if (2 * (size_t)size() > slot.size()) rehash((uint32_t)slot.size() * 2);
+    return id;
+  }
+};
+
+// Section 4 (ncoef x {matrix, constraint, signal, value}) -> CSR rows (A rows, then B rows over one
+// term array), terms in file order within each row.  Contiguous ranges of the entries go to
+// threads: each validates its range, counts its terms per row and interns the values in its own
+// dictionary; the dictionaries merge in range order, thread t's terms of row j start after the
+// earlier ranges' terms of row j, and the scatter runs in parallel again.  Terms pack col | value
+// id << cshift when both fit a u32 (otherwise every term keeps its 32-byte value: cshift = 0).
+int coef_csr(const uint8_t* ent, uint32_t ncoef, ZkeyHost& z, std::string& err) {
+  const size_t dom = z.dom, rows = 2 * (dom + 1);
+  uint32_t colbits = 1;
+  while (colbits < 32 && (1ull << colbits) < z.nVars) colbits++;
+#ifndef ZK_COEF_DICT_MAX
+#define ZK_COEF_DICT_MAX 0xFFFFFFFFull  // tests build a smaller cap to reach the wide path
+#endif
+  const uint64_t id_limit = colbits < 32 ? std::min<uint64_t>(1ull << (32 - colbits), ZK_COEF_DICT_MAX) : 0;
+  unsigned T = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  T = (unsigned)std::min<size_t>(T, std::max<size_t>(1, ncoef / 65536));
+  if (const char* e = getenv("ZKFL_PARSE_THREADS")) T = (unsigned)std::max(1, std::min(64, atoi(e)));
+  T = (unsigned)std::min<size_t>(T, std::max<size_t>(1, ((size_t)256 << 20) / (rows * 4)));  // histograms
+  std::vector<std::vector<uint32_t>> hist(T);
+  std::vector<CoefDict> dicts(T);
+  std::vector<uint32_t> lid(ncoef);
+  std::vector<int> badr(T, 0);
+  auto range = [&](unsigned t, size_t& a, size_t& b) {
+    a = (size_t)ncoef * t / T;
+    b = (size_t)ncoef * (t + 1) / T;
+  };
+  auto par = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(fn, t);
+    fn(0u);
+    for (auto& x : th) x.join();
+  };
+  par([&](unsigned t) {
+    size_t a, b;
+    range(t, a, b);
+    std::vector<uint32_t>& h = hist[t];
+    h.assign(rows, 0);
+    CoefDict& d = dicts[t];
+    for (size_t i = a; i < b; i++) {
+      const uint8_t* e = ent + i * 44;
+      uint32_t mcs[3];
+      memcpy(mcs, e, 12);
+      if (mcs[0] > 1 || mcs[1] >= dom || mcs[2] >= z.nVars) {
+        badr[t] = 1;
+        return;
+      }
+      h[mcs[0] * (dom + 1) + mcs[1]]++;
+      if (id_limit) lid[i] = d.intern(e + 12);
+    }
+  });
+  for (int x : badr)
+    if (x) return bad(err, ZKFL_E_FORMAT, "zkey: coefficient out of range");
+  // merged dictionary (range order) and each range's local -> merged id map
+  CoefDict g;
+  std::vector<std::vector<uint32_t>> gmap(T);
+  bool packed = id_limit != 0 && ncoef != 0;
+  for (unsigned t = 0; t < T && packed; t++) {
+    const CoefDict& d = dicts[t];
+    gmap[t].resize(d.size());
+    for (uint32_t j = 0; j < d.size() && packed; j++) {
+      gmap[t][j] = g.intern(reinterpret_cast<const uint8_t*>(&d.vals[(size_t)j * 8]));
+      packed = g.size() <= id_limit;
+    }
+  }
+  // row pointers: per row, the ranges' counts in order; hist[t][row] becomes range t's first slot
+  std::vector<uint32_t>& rowptr = z.rowptr;
+  rowptr.assign(rows, 0);
+  size_t run = 0;
+  for (size_t m = 0; m < 2; m++)
+    for (size_t j = 0; j < dom; j++) {
+      const size_t r = m * (dom + 1) + j;
+      rowptr[r] = (uint32_t)run;
+      for (unsigned t = 0; t < T; t++) {
+        const uint32_t c = hist[t][r];
+        hist[t][r] = (uint32_t)run;
+        run += c;
+      }
+      if (j + 1 == dom) rowptr[r + 1] = (uint32_t)run;
+    }
+  // rowptr[m (dom + 1) + j] = first term of row j of matrix m; rowptr[dom] = nA = rowptr[dom + 1]
+  std::vector<uint32_t> cols(ncoef);
+  std::vector<uint32_t> coefs(packed ? 0 : (size_t)ncoef * 8);
+  par([&](unsigned t) {
+    size_t a, b;
+    range(t, a, b);
+    std::vector<uint32_t>& h = hist[t];
+    const uint32_t* gm = packed ? gmap[t].data() : nullptr;
+    for (size_t i = a; i < b; i++) {
+      const uint8_t* e = ent + i * 44;
+      uint32_t mcs[3];
+      memcpy(mcs, e, 12);
+      const uint32_t pos = h[mcs[0] * (dom + 1) + mcs[1]]++;
+      if (packed) {
+        cols[pos] = mcs[2] | (gm[lid[i]] << colbits);
+      } else {
+        cols[pos] = mcs[2];
+        memcpy(&coefs[(size_t)pos * 8], e + 12, 32);
+      }
+    }
+  });
+  z.cshift = packed ? colbits : 0;
+  z.cols.swap(cols);
+  if (packed)
+    z.coefs.swap(g.vals);
+  else
+    z.coefs.swap(coefs);
+  return ZKFL_OK;
+}
+
 int zkey_parse(const uint8_t* buf, size_t len, ZkeyHost& z, std::string& err) {
   std::vector<Section> s;
   int rc = binfile_sections(buf, len, "zkey", s, err);
@@ -357,79 +507,7 @@ int zkey_parse(const uint8_t* buf, size_t len, ZkeyHost& z, std::string& err) {
   const uint32_t ncoef = rd32(cs);
   if (s[4].size != 4 + (size_t)ncoef * 44) return bad(err, ZKFL_E_FORMAT, "zkey: coefficient section size");
   z.ncoef = ncoef;
-  const size_t dom = z.dom;
-  std::vector<uint32_t>& rowptr = z.rowptr;
-  rowptr.assign(2 * (dom + 1), 0);
-  for (uint32_t i = 0; i < ncoef; i++) {
-    uint32_t mcs[3];
-    memcpy(mcs, cs + 4 + (size_t)i * 44, 12);
-    if (mcs[0] > 1 || mcs[1] >= dom || mcs[2] >= z.nVars)
-      return bad(err, ZKFL_E_FORMAT, "zkey: coefficient out of range");
-    rowptr[mcs[0] * (dom + 1) + mcs[1] + 1]++;
-  }
-  for (int m = 0; m < 2; m++) {
-    uint32_t* rp = rowptr.data() + m * (dom + 1);
-    for (size_t j = 0; j < dom; j++) rp[j + 1] += rp[j];
-  }
-  const uint32_t nA = rowptr[dom];  // B rows follow A rows in one term array
-  for (size_t j = 0; j <= dom; j++) rowptr[dom + 1 + j] += nA;
-  std::vector<uint32_t> fill(rowptr.begin(), rowptr.end());
-  std::vector<uint32_t> cols(ncoef);
-  std::vector<uint32_t> coefs((size_t)ncoef * 8);
-  for (uint32_t i = 0; i < ncoef; i++) {
-    const uint8_t* e = cs + 4 + (size_t)i * 44;
-    uint32_t mcs[3];
-    memcpy(mcs, e, 12);
-    const uint32_t pos = fill[mcs[0] * (dom + 1) + mcs[1]]++;
-    cols[pos] = mcs[2];
-    memcpy(&coefs[(size_t)pos * 8], e + 12, 32);
-  }
-  // coefficient dictionary: pack col | index << cshift when both fit one u32
-  z.cshift = 0;
-  uint32_t colbits = 1;
-  while (colbits < 32 && (1ull << colbits) < z.nVars) colbits++;
-  struct K32 {
-    uint32_t v[8];
-    bool operator==(const K32& o) const { return memcmp(v, o.v, 32) == 0; }
-  };
-  struct H32 {
-    size_t operator()(const K32& k) const {
-      uint64_t hsh = 0x9E3779B97F4A7C15ull;
-      for (uint32_t x : k.v) hsh = (hsh ^ x) * 0x100000001B3ull;
-      return (size_t)(hsh ^ (hsh >> 29));
-    }
-  };
-  std::unordered_map<K32, uint32_t, H32> idx;
-  std::vector<uint32_t> dict;
-  std::vector<uint32_t> packed(ncoef);
-  bool ok = colbits < 32;
-  for (uint32_t p = 0; p < ncoef && ok; p++) {
-    K32 key;
-    memcpy(key.v, &coefs[(size_t)p * 8], 32);
-    auto it = idx.find(key);
-    uint32_t id;
-    if (it == idx.end()) {
-      id = (uint32_t)idx.size();
-      if ((uint64_t)id >= (1ull << (32 - colbits))) {
-        ok = false;
-        break;
-      }
-      idx.emplace(key, id);
-      dict.insert(dict.end(), &coefs[(size_t)p * 8], &coefs[(size_t)p * 8] + 8);
-    } else {
-      id = it->second;
-    }
-    packed[p] = cols[p] | (id << colbits);
-  }
-  if (ok && ncoef) {
-    z.cshift = colbits;
-    z.cols.swap(packed);
-    z.coefs.swap(dict);
-  } else {
-    z.cols.swap(cols);
-    z.coefs.swap(coefs);
-  }
-  return ZKFL_OK;
+  return coef_csr(cs + 4, ncoef, z, err);
 }
 
 int wprog_signals(const uint8_t* img, size_t len, std::vector<WSignal>& sigs, std::string& err) {

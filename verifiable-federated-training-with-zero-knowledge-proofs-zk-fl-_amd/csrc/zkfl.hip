@@ -18,7 +18,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/random.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -776,6 +780,7 @@ struct ProofSlot {
   hipStream_t st_lat[2] = {nullptr, nullptr};
   hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
   MsmScratch<FqOps> g1s_b;
+  MsmScratch<FqOps> g1s_a;  // A's sort scratch in the overlapped schedule (A beside C + H)
   bool busy = false;
   int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
@@ -852,6 +857,7 @@ void slot_release(ProofSlot* s) {
   for (hipStream_t st : s->st_lat)
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s_b);
+  msm_scratch_free_g1(s->g1s_a);
   for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
@@ -1127,8 +1133,81 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   return ZKFL_OK;
 }
 
+// The overlapped low-latency schedule (ZKFL_LOWLAT=2): the witness-scalar MSMs no longer precede
+// ABC / NTT on the main stream.  The wave timeline of the one-proof chain (tools/wtrace.py
+// --isolated) had the C + H chain critical -- ABC, NTT, join, its sort, accumulation and tail
+// (~4 ms) started only after A and B1 (~1.2 ms) -- and B2's chain (sort, G2 accumulation, G2
+// tail: ~3.4 ms) second.  Here both long chains start at once:
+//   main : r, s, tails reset [ev_ready] ABC, coset NTT, join, C + H (sort + accumulate), its tail,
+//          wait(B2, T), k_assemble_c, proof D2H [ev_done]
+//   lat0 : wait(ev_ready) B sort (own scratch) [ev B sorted] B2 + its tail [ev B2]
+//   lat1 : wait(ev B sorted) B1, A (sort into its own scratch + accumulate), the tails of A and
+//          B1, k_assemble_t [ev T]
+int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w) {
+  Profiler* prof = &ctx->prof;
+  hipStream_t st = s->st_main;
+  for (int i = 0; i < 2; i++)
+    if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
+  for (int i = 0; i < 3; i++)
+    if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
+  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
+  if (!s->g1s_a.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, st), "A sort scratch");
+  hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
+  // ev_lat[0] marks "ready" then (re-recorded on lat0) "B sorted": each wait is enqueued before
+  // the next record, so every wait sees the record it was meant for
+  hipEvent_t ev = s->ev_lat[0], ev_b2 = s->ev_lat[1], ev_t = s->ev_lat[2];
+  const uint32_t* W = (const uint32_t*)d_w;
+  const uint32_t* E = (const uint32_t*)s->extra;
+  MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
+  MsmTail<Fq2Ops>* t2 = &s->g2t;
+  G2P* o2 = s->resB2;
+  HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
+  HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
+  HIP_TRY(hipEventRecord(ev, st), "event");
+  // lat0: B's sort, then B2 and its tail
+  HIP_TRY(hipStreamWaitEvent(sb, ev, 0), "wait");
+  HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, sb), "msm B sort");
+  HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, sb), "nnz");
+  HIP_TRY(hipEventRecord(ev, sb), "event");
+  HIP_TRY(hipStreamWaitEvent(sa, ev, 0), "wait");
+  HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
+                                   "msm_accumulate_g2"), "msm B2");
+  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb), "msm B2 tail");
+  HIP_TRY(hipEventRecord(ev_b2, sb), "event");
+  // lat1: B1 (B's pairs), A, their tails, then T = s pi_A + r B1 and pi_a
+  HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], sa, prof,
+                                   "msm_accumulate_g1"), "msm B1");
+  HIP_TRY(msm_accumulate_g1(k->bA, s->g1s_a, s->g1t[0], W, E, sa, prof, "msm_accumulate_g1"), "msm A");
+  {
+    G1P* outs[2] = {s->res + 0, s->res + 1};
+    HIP_TRY(msm_tails_g1(tails, outs, 2, sa), "msm tails A, B1");
+  }
+  hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
+                     reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+  HIP_TRY(hipEventRecord(ev_t, sa), "event");
+  // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
+  {
+    const int rc = enqueue_abc_ntt(k, s, d_w, st, prof);
+    if (rc) return rc;
+  }
+  HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+          "msm C+H");
+  HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
+  {
+    G1P* out2 = s->res + 2;
+    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st), "msm tail C+H");
+  }
+  HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
+  HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
+  const int pa = prof->begin("assemble", st);
+  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, s->d_proof);
+  prof->end(pa, st, 1.0);
+  HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
+  return ZKFL_OK;
+}
+
 int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain,
-                  bool lowlat = false) {
+                  int lowlat = 0) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
@@ -1142,7 +1221,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
           "upload r,s");
   hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain == 1);
   if (lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT) {
-    const int rc = enqueue_proof_lowlat(ctx, k, s, d_w);
+    const int rc = lowlat == 2 ? enqueue_proof_lowlat2(ctx, k, s, d_w) : enqueue_proof_lowlat(ctx, k, s, d_w);
     if (rc) return rc;
     prof->end(pp, st, 1.0);
     HIP_TRY(hipEventRecord(s->ev_done, st), "event");
@@ -1164,9 +1243,10 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   // Stage order.  Every slot runs the same chain, so under load the slots move as a convoy: the
   // accumulations fill the GPU one at a time, and the slots that leave them together reach ABC +
   // NTT together -- the wave timeline (tools/wtrace.py) showed stretches of ~4 ms with no
-  // accumulation resident at all.  ZKFL_STAGGER=1: odd slots run ABC + NTT before their
-  // witness-scalar MSMs instead of after, so their light phase falls beside the others' heavy one.
-  static const int stagger = getenv("ZKFL_STAGGER") ? atoi(getenv("ZKFL_STAGGER")) : 0;
+  // accumulation resident at all.  Staggered (the default; ZKFL_STAGGER=0 turns it off): odd slots
+  // run ABC + NTT before their witness-scalar MSMs instead of after, so their light phase falls
+  // beside the others' heavy one (+2.3 %, 407.5 vs 398.6 proofs/s, 3 same-box alternations).
+  static const int stagger = getenv("ZKFL_STAGGER") ? atoi(getenv("ZKFL_STAGGER")) : 1;
   const bool light_first = stagger && (s->index & 1) && !prof->serialize;
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
@@ -1304,9 +1384,10 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
       hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
       if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
     }
-    // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain)
-    static const bool lowlat = !getenv("ZKFL_LOWLAT") || atoi(getenv("ZKFL_LOWLAT")) != 0;
-    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, lowlat && n == 1);
+    // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
+    // 1: A and B before ABC / NTT, 2: overlapped)
+    static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
+    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, n == 1 ? lowlat : 0);
     if (rc) break;
     s->busy = true;
   }
@@ -1584,9 +1665,11 @@ int zkfl_ctx_synchronize(zkfl_ctx* ctx) {
 }
 
 namespace {
-int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t nshards,
-                   zkfl_key** out) {
-  if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
+// Make a parsed key device-resident.  z's pointers address the key bytes (len of them), which
+// stay valid for the call; parse_ms: the parse's duration for the load timing.
+int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_ms, uint32_t shard, uint32_t nshards,
+                     zkfl_key** out) {
+  if (!ctx || !out) return fail(ZKFL_E_ARG, "null argument");
   if (nshards < 1 || nshards > 1024 || shard >= nshards) return fail(ZKFL_E_ARG, "shard must be < n_shards <= 1024");
   // ZKFL_LOAD_TIMING=<file>: one JSON line per load with the host-side stages (bench.py cli_prove)
   const char* timing_path = getenv("ZKFL_LOAD_TIMING");
@@ -1598,13 +1681,7 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
     marks.emplace_back(what, std::chrono::duration<double, std::milli>(t - t_last).count());
     t_last = t;
   };
-  ZkeyHost z;
-  {
-    std::string err;
-    int rc = zkey_parse(buf, len, z, err);  // csrc/host_parse.cc: header, sections, CSR + dictionary
-    if (rc) return fail(rc, err);
-  }
-  mark("parse");
+  if (timing_path) marks.emplace_back("parse", parse_ms);
   const uint32_t nVars = z.nVars, nPub = z.nPub, dom = z.dom;
   const int logn = z.logn;
   const size_t nC = z.nC;
@@ -1677,85 +1754,88 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
     // H with one shard keeps every point and no index map (scalar j = h[j]); sharded, it is
     // compacted like the others, its map indexing h directly (no extra slots)
     const bool h_identity = nshards == 1;
-    // Build the compacted (host) base image + index map, upload, expand.
-    std::vector<uint32_t> sidx_b1, sidx_b2;
-    auto build = [&](auto& mb, size_t psz, const uint8_t* sec, size_t cnt, uint32_t scalar_off,
-                     std::initializer_list<Aug> aug, bool identity,
-                     std::vector<uint32_t>* keep = nullptr) -> hipError_t {
+    // The compacted (host) base images + index maps of every query are built on host threads at
+    // once (they only read the key bytes), then uploaded and expanded back to back on the stream
+    // with one synchronisation at the end (the images stay alive until then).
+    struct Img {
       std::vector<uint8_t> img;
       std::vector<uint32_t> sidx;
-      img.reserve((cnt + aug.size()) * psz);
-      sidx.reserve(cnt + aug.size());
+    };
+    auto image = [&](Img& o, size_t psz, const uint8_t* sec, size_t cnt, uint32_t scalar_off,
+                     std::vector<Aug> aug, bool identity) {
+      size_t kept = 0;
+      for (size_t i = 0; i < cnt; i++) kept += mine(i) && (identity || nonzero(sec + i * psz, psz));
+      o.img.resize((kept + aug.size()) * psz);
+      o.sidx.reserve(kept + aug.size());
+      uint8_t* w = o.img.data();
       for (size_t i = 0; i < cnt; i++) {
         const uint8_t* p = sec + i * psz;
         if (!mine(i) || (!identity && !nonzero(p, psz))) continue;
-        img.insert(img.end(), p, p + psz);
-        sidx.push_back(scalar_off + (uint32_t)i);
+        memcpy(w, p, psz);
+        w += psz;
+        o.sidx.push_back(scalar_off + (uint32_t)i);
       }
       if (aug_here)
-        for (const Aug& a : aug) {
-          img.insert(img.end(), a.pt, a.pt + psz);
-          sidx.push_back(a.sidx);
+        for (const Aug& x : aug) {
+          memcpy(w, x.pt, psz);
+          w += psz;
+          o.sidx.push_back(x.sidx);
         }
-      if (keep) *keep = sidx;
-      hipError_t e = bases_alloc_any(mb, sidx.size());
-      if (e != hipSuccess || sidx.empty()) return e;
+      o.img.resize((size_t)(w - o.img.data()));
+    };
+    // C (private wires -> the witness) then H (h_j -> extra[j], the slot's h vector), then delta1
+    // with -rs (extra[dom + 3]: the extra slots sit behind h)
+    auto image_ch = [&](Img& o) {
+      Img c, h;
+      image(c, 64, z.secC, nC, nPub + 1, {}, false);
+      image(h, 64, z.secH, dom, X, {{delta1, (uint32_t)(X + dom + 3)}}, false);
+      o.img.swap(c.img);
+      o.img.insert(o.img.end(), h.img.begin(), h.img.end());
+      o.sidx.swap(c.sidx);
+      o.sidx.insert(o.sidx.end(), h.sidx.begin(), h.sidx.end());
+    };
+    enum { QA, QB1, QB2, QC, QH, QCH, NQ };
+    std::vector<Img> im(NQ);
+    {
+      std::vector<std::thread> th;
+      th.emplace_back([&] { image(im[QA], 64, z.secA, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false); });
+      th.emplace_back([&] { image(im[QB1], 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false); });
+      th.emplace_back([&] { image(im[QB2], 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false); });
+      if (MSM_MERGE_CH) {
+        th.emplace_back([&] { image_ch(im[QCH]); });
+      } else {
+        th.emplace_back([&] { image(im[QC], 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false); });
+        // aug.size() == 0 (H): no extra slots, the map indexes the main scalars only
+        th.emplace_back([&] { image(im[QH], 64, z.secH, dom, 0, {}, h_identity); });
+      }
+      for (auto& t : th) t.join();
+    }
+    mark("bases_host");
+    std::vector<void*> d_imgs;
+    auto upload = [&](auto& mb, Img& o, bool identity, uint32_t xs) -> hipError_t {
+      hipError_t e = bases_alloc_any(mb, o.sidx.size());
+      if (e != hipSuccess || o.sidx.empty()) return e;
       void* d_img = nullptr;
-      e = hipMalloc(&d_img, img.size());
-      if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
-      const uint32_t* hs = identity ? nullptr : sidx.data();
-      // aug.size() == 0 (H): no extra slots, the map indexes the main scalars only
-      const uint32_t xs = (identity || aug.size() == 0) ? 0xFFFFFFFFu : X;
-      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, hs, xs, st);
-      if (e == hipSuccess) e = hipStreamSynchronize(st);
-      if (d_img) (void)hipFree(d_img);
+      e = hipMalloc(&d_img, o.img.size());
+      if (e != hipSuccess) return e;
+      d_imgs.push_back(d_img);
+      e = hipMemcpyAsync(d_img, o.img.data(), o.img.size(), hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = bases_set_map_any(mb, d_img, identity ? nullptr : o.sidx.data(), xs, st);
       return e;
     };
-    hipError_t e = build(k->bA, 64, z.secA, nVars, 0, {{alpha1, X + 0}, {delta1, X + 1}}, false);
-    mark("bases_A");
-    if (e == hipSuccess)
-      e = build(k->bB1, 64, z.secB1, nVars, 0, {{beta1, X + 0}, {delta1, X + 2}}, false, &sidx_b1);
-    mark("bases_B1");
-    if (e == hipSuccess)
-      e = build(k->bB2, 128, z.secB2, nVars, 0, {{beta2, X + 0}, {delta2, X + 2}}, false, &sidx_b2);
-    mark("bases_B2");
+    hipError_t e = upload(k->bA, im[QA], false, X);
+    if (e == hipSuccess) e = upload(k->bB1, im[QB1], false, X);
+    if (e == hipSuccess) e = upload(k->bB2, im[QB2], false, X);
     // B_i(tau) G1 and B_i(tau) G2 vanish together in an honest zkey; the sort is shared only when
     // the two index maps really are equal
-    k->share_b = !ZK_NO_SHARE_B && sidx_b1 == sidx_b2 && !sidx_b1.empty();
-    if (e == hipSuccess && !MSM_MERGE_CH) e = build(k->bC, 64, z.secC, nC, nPub + 1, {{delta1, X + 3}}, false);
-    if (e == hipSuccess && !MSM_MERGE_CH) e = build(k->bH, 64, z.secH, dom, 0, {}, h_identity);
-    if (e == hipSuccess && MSM_MERGE_CH) {
-      // C (private wires -> the witness) then H (h_j -> extra[j], the slot's h vector), then
-      // delta1 with -rs (extra[dom + 3]: the extra slots sit behind h)
-      std::vector<uint8_t> img;
-      std::vector<uint32_t> sidx;
-      img.reserve((nC + dom + 1) * 64);
-      sidx.reserve(nC + dom + 1);
-      for (size_t i = 0; i < nC; i++) {
-        const uint8_t* p = z.secC + i * 64;
-        if (!mine(i) || !nonzero(p, 64)) continue;
-        img.insert(img.end(), p, p + 64);
-        sidx.push_back(nPub + 1 + (uint32_t)i);
-      }
-      for (size_t j = 0; j < dom; j++) {
-        const uint8_t* p = z.secH + j * 64;
-        if (!mine(j) || !nonzero(p, 64)) continue;
-        img.insert(img.end(), p, p + 64);
-        sidx.push_back(X + (uint32_t)j);
-      }
-      if (aug_here) {
-        img.insert(img.end(), delta1, delta1 + 64);
-        sidx.push_back(X + dom + 3);
-      }
-      e = bases_alloc_any(k->bCH, sidx.size());
-      void* d_img = nullptr;
-      if (e == hipSuccess) e = hipMalloc(&d_img, img.size());
-      if (e == hipSuccess) e = hipMemcpyAsync(d_img, img.data(), img.size(), hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) e = bases_set_map_any(k->bCH, d_img, sidx.data(), X, st);
-      if (e == hipSuccess) e = hipStreamSynchronize(st);
-      if (d_img) (void)hipFree(d_img);
-    }
-    mark("bases_CH");
+    k->share_b = !ZK_NO_SHARE_B && im[QB1].sidx == im[QB2].sidx && !im[QB1].sidx.empty();
+    if (e == hipSuccess && MSM_MERGE_CH) e = upload(k->bCH, im[QCH], false, X);
+    if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bC, im[QC], false, X);
+    if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bH, im[QH], h_identity, 0xFFFFFFFFu);
+    const hipError_t es = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = es;
+    for (void* d : d_imgs) (void)hipFree(d);
+    mark("bases_upload");
     if (e != hipSuccess) return cleanup(hip_fail(e, "base expansion"));
   }
   KTRY(ntt_plan_alloc(k->ntt, logn, st), "ntt plan");
@@ -1784,10 +1864,76 @@ int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard
   *out = k;
   return ZKFL_OK;
 }
+
+int zkey_load_impl(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t nshards,
+                   zkfl_key** out) {
+  if (!ctx || !buf || !out) return fail(ZKFL_E_ARG, "null argument");
+  if (nshards < 1 || nshards > 1024 || shard >= nshards) return fail(ZKFL_E_ARG, "shard must be < n_shards <= 1024");
+  const auto t0 = std::chrono::steady_clock::now();
+  ZkeyHost z;
+  std::string err;
+  const int rc = zkey_parse(buf, len, z, err);  // csrc/host_parse.cc: header, sections, CSR + dictionary
+  if (rc) return fail(rc, err);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return zkey_load_parsed(ctx, z, len, ms, shard, nshards, out);
+}
 }  // namespace
+
+struct zkfl_zkey_file {
+  int fd = -1;
+  void* map = nullptr;
+  size_t len = 0;
+  ZkeyHost z;
+  double parse_ms = 0;
+};
 
 int zkfl_zkey_load(zkfl_ctx* ctx, const uint8_t* buf, size_t len, zkfl_key** out) {
   return zkey_load_impl(ctx, buf, len, 0, 1, out);
+}
+
+int zkfl_zkey_file_open(const char* path, zkfl_zkey_file** out) {
+  if (!path || !out) return fail(ZKFL_E_ARG, "null argument");
+  *out = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  zkfl_zkey_file* f = new zkfl_zkey_file();
+  f->fd = open(path, O_RDONLY | O_CLOEXEC);
+  struct stat stt;
+  if (f->fd < 0 || fstat(f->fd, &stt) != 0) {
+    zkfl_zkey_file_close(f);
+    return fail(ZKFL_E_ARG, std::string("cannot open ") + path);
+  }
+  f->len = (size_t)stt.st_size;
+  if (f->len) {
+    f->map = mmap(nullptr, f->len, PROT_READ, MAP_PRIVATE, f->fd, 0);
+    if (f->map == MAP_FAILED) {
+      f->map = nullptr;
+      zkfl_zkey_file_close(f);
+      return fail(ZKFL_E_ARG, std::string("cannot map ") + path);
+    }
+    (void)madvise(f->map, f->len, MADV_WILLNEED);
+  }
+  std::string err;
+  const int rc = zkey_parse(static_cast<const uint8_t*>(f->map), f->len, f->z, err);
+  if (rc) {
+    zkfl_zkey_file_close(f);
+    return fail(rc, err);
+  }
+  f->parse_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = f;
+  return ZKFL_OK;
+}
+
+int zkfl_zkey_load_file(zkfl_ctx* ctx, const zkfl_zkey_file* f, zkfl_key** out) {
+  if (!f) return fail(ZKFL_E_ARG, "null argument");
+  return zkey_load_parsed(ctx, f->z, f->len, f->parse_ms, 0, 1, out);
+}
+
+int zkfl_zkey_file_close(zkfl_zkey_file* f) {
+  if (!f) return ZKFL_OK;
+  if (f->map) munmap(f->map, f->len);
+  if (f->fd >= 0) close(f->fd);
+  delete f;
+  return ZKFL_OK;
 }
 
 int zkfl_zkey_load_shard(zkfl_ctx* ctx, const uint8_t* buf, size_t len, uint32_t shard, uint32_t n_shards,

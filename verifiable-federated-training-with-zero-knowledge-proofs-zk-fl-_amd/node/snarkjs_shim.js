@@ -83,11 +83,19 @@ function key(zkey) {
   const id = Buffer.isBuffer(zkey) ? zkey : path.resolve(zkey);
   let k = keys.get(id);
   if (!k) {
+    // the context comes up on a thread of its own (addon.createContext) while this thread maps and
+    // parses the key file (zkfl_zkey_file_open); the load then waits for it
     const c = context();
     mark('context');
-    const buf = read(zkey);
-    mark('zkey_read');
-    k = addon.loadKey(c, buf);
+    if (Buffer.isBuffer(zkey)) {
+      k = addon.loadKey(c, zkey);
+    } else {
+      const f = addon.openKeyFile(id);
+      mark('zkey_read');
+      addon.contextReady(c);
+      mark('context_wait');
+      k = addon.loadKeyFile(c, f);
+    }
     mark('key_load');
     keys.set(id, k);
   }
@@ -253,8 +261,20 @@ module.exports = {
   addon, proofToJson, vkBuffer,
 };
 
+// A CLI command's end: its outputs are written (synchronously) by now, so after the 'exit'
+// listeners (the timing record) the process leaves with _exit -- the device memory of its key and
+// context goes back with the process, without the HIP runtime's teardown (tens of ms for a large
+// key).  ZKFL_CLI_FULL_EXIT=1: a normal process.exit.
+function quit(code) {
+  if (addon.quickExit && !process.env.ZKFL_CLI_FULL_EXIT) {
+    process.emit('exit', code);
+    addon.quickExit(code);
+  }
+  process.exit(code);
+}
+
 function done(p) {
-  p.then((code) => process.exit(code || 0)).catch((e) => { console.error('[ERROR] snarkJS: ' + e.message); process.exit(1); });
+  p.then((code) => quit(code || 0)).catch((e) => { console.error('[ERROR] snarkJS: ' + e.message); quit(1); });
 }
 
 // The one-time ceremony commands (powersoftau new|contribute|prepare phase2, groth16 setup,

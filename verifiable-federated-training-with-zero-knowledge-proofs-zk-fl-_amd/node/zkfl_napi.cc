@@ -9,8 +9,13 @@
 // JS surface (see snarkjs_shim.js):
 //   version() -> number
 //   deviceCount() -> number
-//   createContext(device) -> ctx
+//   createContext(device) -> ctx      (created on a thread of its own: the call returns at once and
+//                                      the first use waits for it, so a CLI maps its key meanwhile)
 //   loadKey(ctx, zkeyBuffer) -> key                       (zkfl_zkey_load)
+//   openKeyFile(path) -> file                             (zkfl_zkey_file_open: map + host parse)
+//   loadKeyFile(ctx, file) -> key                         (zkfl_zkey_load_file)
+//   contextReady(ctx) -> true                             (waits for the context; throws if it failed)
+//   quickExit(code)                                       (the CLI's exit: _exit after stdio flush)
 //   keyInfo(key) -> {nVars, nPublic, domainSize}
 //   prove(ctx, key, wtnsBuffer[, rsBuffer]) -> Promise<{proof: Buffer(256), publicSignals: Buffer}>
 //   verify(ctx, vkBuffer, publicBuffer, proofBuffer) -> Promise<boolean>   (zkfl_groth16_verify)
@@ -22,8 +27,12 @@
 //   poseidon / vectorHash / merkleBuild                                    (node/circomlibjs, see below)
 #include <node_api.h>
 
+#include <unistd.h>
+
+#include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "zkfl.h"
@@ -50,7 +59,42 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
   return v;
 }
 
-void ctx_finalize(napi_env, void* data, void*) { zkfl_ctx_destroy(static_cast<zkfl_ctx*>(data)); }
+// A context being created on its own thread (hipInit and the device's context take ~80 ms of a
+// CLI run); get() waits for it.
+struct CtxBox {
+  std::thread th;
+  zkfl_ctx* ctx = nullptr;
+  int rc = 0;
+  std::string err;
+  zkfl_ctx* get() {
+    if (th.joinable()) th.join();
+    return ctx;
+  }
+};
+
+// argv value -> the context (waiting for its creation); throws and returns nullptr when it failed
+zkfl_ctx* ctx_arg(napi_env env, napi_value v) {
+  void* data = nullptr;
+  if (napi_get_value_external(env, v, &data) != napi_ok || !data) return nullptr;
+  CtxBox* b = static_cast<CtxBox*>(data);
+  zkfl_ctx* c = b->get();
+  if (!c) {
+    std::string msg = std::string("zkfl error ") + std::to_string(b->rc) + ": " + b->err;
+    napi_throw_error(env, nullptr, msg.c_str());
+  }
+  return c;
+}
+
+// the context behind an external (waiting for its creation; nullptr if that failed: the zkfl
+// call it goes to then reports a null context)
+zkfl_ctx* ctx_box(void* data) { return data ? static_cast<CtxBox*>(data)->get() : nullptr; }
+
+void ctx_finalize(napi_env, void* data, void*) {
+  CtxBox* b = static_cast<CtxBox*>(data);
+  zkfl_ctx_destroy(b->get());
+  delete b;
+}
+void file_finalize(napi_env, void* data, void*) { zkfl_zkey_file_close(static_cast<zkfl_zkey_file*>(data)); }
 void key_finalize(napi_env, void* data, void*) { zkfl_key_free(static_cast<zkfl_key*>(data)); }
 void prog_finalize(napi_env, void* data, void*) { zkfl_wprog_free(static_cast<zkfl_wprog*>(data)); }
 
@@ -60,11 +104,13 @@ napi_value CreateContext(napi_env env, napi_callback_info info) {
   napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
   int32_t dev = 0;
   if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
-  zkfl_ctx* ctx = nullptr;
-  int rc = zkfl_ctx_create(dev, &ctx);
-  if (rc) return throw_err(env, rc);
+  CtxBox* b = new CtxBox();
+  b->th = std::thread([b, dev] {
+    b->rc = zkfl_ctx_create(dev, &b->ctx);
+    if (b->rc) b->err = zkfl_last_error();
+  });
   napi_value ext;
-  napi_create_external(env, ctx, ctx_finalize, nullptr, &ext);
+  napi_create_external(env, b, ctx_finalize, nullptr, &ext);
   return ext;
 }
 
@@ -80,12 +126,73 @@ napi_value LoadKey(napi_env env, napi_callback_info info) {
     napi_throw_type_error(env, nullptr, "loadKey(ctx, zkeyBuffer)");
     return nullptr;
   }
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
   zkfl_key* key = nullptr;
-  int rc = zkfl_zkey_load(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(data), len, &key);
+  int rc = zkfl_zkey_load(c, static_cast<const uint8_t*>(data), len, &key);
   if (rc) return throw_err(env, rc);
   napi_value ext;
   napi_create_external(env, key, key_finalize, nullptr, &ext);
   return ext;
+}
+
+napi_value OpenKeyFile(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  size_t n = 0;
+  if (argc < 1 || napi_get_value_string_utf8(env, argv[0], nullptr, 0, &n) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "openKeyFile(path)");
+    return nullptr;
+  }
+  std::string path(n, '\0');
+  napi_get_value_string_utf8(env, argv[0], &path[0], n + 1, &n);
+  zkfl_zkey_file* f = nullptr;
+  int rc = zkfl_zkey_file_open(path.c_str(), &f);
+  if (rc) return throw_err(env, rc);
+  napi_value ext;
+  napi_create_external(env, f, file_finalize, nullptr, &ext);
+  return ext;
+}
+
+napi_value LoadKeyFile(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  void* f = nullptr;
+  if (argc < 2 || napi_get_value_external(env, argv[1], &f) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "loadKeyFile(ctx, file)");
+    return nullptr;
+  }
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
+  zkfl_key* key = nullptr;
+  int rc = zkfl_zkey_load_file(c, static_cast<const zkfl_zkey_file*>(f), &key);
+  if (rc) return throw_err(env, rc);
+  napi_value ext;
+  napi_create_external(env, key, key_finalize, nullptr, &ext);
+  return ext;
+}
+
+napi_value ContextReady(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  if (argc < 1 || !ctx_arg(env, argv[0])) return nullptr;
+  napi_value t;
+  napi_get_boolean(env, true, &t);
+  return t;
+}
+
+// quickExit(code): stdio flushed, then _exit (no atexit handlers, no static destructors)
+napi_value QuickExit(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  int32_t code = 0;
+  if (argc >= 1) napi_get_value_int32(env, argv[0], &code);
+  fflush(nullptr);
+  _exit(code);
 }
 
 napi_value KeyInfo(napi_env env, napi_callback_info info) {
@@ -169,7 +276,7 @@ napi_value Prove(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   ProveWork* w = new ProveWork();
-  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->ctx = ctx_box(ctx);
   w->key = static_cast<zkfl_key*>(key);
   w->wtns.assign(static_cast<uint8_t*>(wt), static_cast<uint8_t*>(wt) + wlen);
   if (argc >= 4 && napi_get_buffer_info(env, argv[3], &rs, &rslen) == napi_ok && rslen == 64)
@@ -229,7 +336,7 @@ napi_value Verify(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   VerifyWork* w = new VerifyWork();
-  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->ctx = ctx_box(ctx);
   w->vk.assign(static_cast<uint8_t*>(vk), static_cast<uint8_t*>(vk) + vlen);
   w->pub.assign(static_cast<uint8_t*>(pub), static_cast<uint8_t*>(pub) + plen);
   w->pub.resize(plen + 32);  // never empty (data() of an empty vector may be null)
@@ -256,7 +363,7 @@ napi_value LoadProgram(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   zkfl_wprog* prog = nullptr;
-  int rc = zkfl_wprog_load(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(data), len, &prog);
+  int rc = zkfl_wprog_load(ctx_box(ctx), static_cast<const uint8_t*>(data), len, &prog);
   if (rc) return throw_err(env, rc);
   napi_value ext;
   napi_create_external(env, prog, prog_finalize, nullptr, &ext);
@@ -312,7 +419,7 @@ napi_value Witness(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   WitnessWork* w = new WitnessWork();
-  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->ctx = ctx_box(ctx);
   w->prog = static_cast<zkfl_wprog*>(prog);
   w->json.resize(jlen + 1);
   napi_get_value_string_utf8(env, argv[2], &w->json[0], jlen + 1, &jlen);
@@ -387,7 +494,7 @@ napi_value FullProve(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   FullProveWork* w = new FullProveWork();
-  w->ctx = static_cast<zkfl_ctx*>(ctx);
+  w->ctx = ctx_box(ctx);
   w->key = static_cast<zkfl_key*>(key);
   w->prog = static_cast<zkfl_wprog*>(prog);
   w->json.resize(jlen + 1);
@@ -416,7 +523,7 @@ napi_value Pairing(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   uint8_t gt[384];
-  int rc = zkfl_pairing(static_cast<zkfl_ctx*>(ctx), 1, static_cast<const uint8_t*>(g1),
+  int rc = zkfl_pairing(ctx_box(ctx), 1, static_cast<const uint8_t*>(g1),
                         static_cast<const uint8_t*>(g2), gt);
   if (rc) return throw_err(env, rc);
   napi_value buf;
@@ -451,8 +558,8 @@ napi_value HashCall(napi_env env, napi_callback_info info, bool vector) {
     return nullptr;
   }
   std::vector<uint8_t> out((size_t)n * 32 + 32);
-  int rc = vector ? zkfl_vector_hash_batch(static_cast<zkfl_ctx*>(ctx), width, n, static_cast<const uint8_t*>(in), out.data())
-                  : zkfl_poseidon_batch(static_cast<zkfl_ctx*>(ctx), width, n, static_cast<const uint8_t*>(in), out.data());
+  int rc = vector ? zkfl_vector_hash_batch(ctx_box(ctx), width, n, static_cast<const uint8_t*>(in), out.data())
+                  : zkfl_poseidon_batch(ctx_box(ctx), width, n, static_cast<const uint8_t*>(in), out.data());
   if (rc) return throw_err(env, rc);
   napi_value buf;
   void* p;
@@ -477,7 +584,7 @@ napi_value MerkleBuild(napi_env env, napi_callback_info info) {
   }
   const size_t nodes = ((size_t)2 << depth) - 1;
   std::vector<uint8_t> out(nodes * 32);
-  int rc = zkfl_merkle_build(static_cast<zkfl_ctx*>(ctx), static_cast<const uint8_t*>(in), len / 32, depth, out.data());
+  int rc = zkfl_merkle_build(ctx_box(ctx), static_cast<const uint8_t*>(in), len / 32, depth, out.data());
   if (rc) return throw_err(env, rc);
   napi_value buf;
   void* p;
@@ -491,6 +598,10 @@ napi_value Init(napi_env env, napi_value exports) {
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"loadKey", nullptr, LoadKey, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"openKeyFile", nullptr, OpenKeyFile, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"loadKeyFile", nullptr, LoadKeyFile, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"contextReady", nullptr, ContextReady, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"quickExit", nullptr, QuickExit, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"keyInfo", nullptr, KeyInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},

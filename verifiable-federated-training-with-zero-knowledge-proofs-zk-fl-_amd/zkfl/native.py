@@ -41,6 +41,9 @@ SIGNATURES = {
     "zkfl_ctx_synchronize": (C.c_int, [_P]),
     "zkfl_zkey_load": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "zkfl_zkey_load_shard": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
+    "zkfl_zkey_file_open": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    "zkfl_zkey_load_file": (C.c_int, [_P, _P, C.POINTER(_P)]),
+    "zkfl_zkey_file_close": (C.c_int, [_P]),
     "zkfl_key_shard": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "zkfl_groth16_prove_part_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_groth16_assemble": (C.c_int, [_P, C.c_size_t, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
@@ -440,11 +443,25 @@ class Context:
 class ProvingKey:
     """A .zkey made device-resident (bases expanded per MSM window)."""
 
-    def __init__(self, ctx: Context, zkey: bytes, shard: int = 0, n_shards: int = 1):
-        """shard / n_shards: keep only this shard's share of every query (split proofs,
-        zkfl_zkey_load_shard); the default is the whole key."""
+    def __init__(self, ctx: Context, zkey, shard: int = 0, n_shards: int = 1):
+        """zkey: the key bytes, or its path (mapped and parsed on host threads: zkfl_zkey_file_open
+        + zkfl_zkey_load_file).  shard / n_shards: keep only this shard's share of every query
+        (split proofs, zkfl_zkey_load_shard); the default is the whole key."""
         h = _P()
-        if n_shards == 1 and shard == 0:
+        if isinstance(zkey, (str, os.PathLike)):
+            if (shard, n_shards) != (0, 1):
+                with open(zkey, "rb") as f:
+                    zkey = f.read()
+            else:
+                fh = _P()
+                check(lib().zkfl_zkey_file_open(os.fsencode(zkey), C.byref(fh)))
+                try:
+                    check(lib().zkfl_zkey_load_file(ctx.h, fh, C.byref(h)))
+                finally:
+                    lib().zkfl_zkey_file_close(fh)
+        if h:
+            pass
+        elif n_shards == 1 and shard == 0:
             check(lib().zkfl_zkey_load(ctx.h, zkey, len(zkey), C.byref(h)))
         else:
             check(lib().zkfl_zkey_load_shard(ctx.h, zkey, len(zkey), shard, n_shards, C.byref(h)))
