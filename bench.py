@@ -261,7 +261,7 @@ def latency_leg(key, ws, n=24):
             "path": "prove_batch of one resident witness -> low-latency schedule (3 streams), host wall clock"}
 
 
-def roofline_pass(key, ctx, ws, slots, n=6):
+def roofline_pass(key, ctx, ws, slots, n=12):
     """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's
     streams serialized onto one), after the timed region: the roofline's average launch time."""
     key.set_slots(1)
@@ -308,6 +308,20 @@ def _measured_clock(kernel):
             return v["clock_GHz"], (f"profiles/sq_counters.json ({'this build' if same else 'build ' + str(d.get('build_id'))}"
                                     f", single-slot PMC run: GRBM_GUI_ACTIVE / 8 / kernel duration)")
     return None, "kernel absent from the counter summary"
+
+
+def stage_times(prof, nprof):
+    """Per-proof stage times of the serialized pass.  A stage with one timed region per proof
+    (ntt, abc, assemble, prove) reports the MEDIAN over the proofs -- robust to the one proof whose
+    region a clock change or a late launch stretched; the accumulations (several launches of
+    different sizes per proof) report their summed time per proof."""
+    out = {}
+    for k, (tot, launches, _, med) in prof.items():
+        if launches == nprof and med:
+            out[k] = round(med, 3)
+        else:
+            out[k] = round(tot / max(1, nprof), 3)
+    return out
 
 
 def roofline(prof, key, traffic=True, nprof=1):
@@ -480,7 +494,7 @@ def extra_circuit_leg(ctx, rank, world, circuit, steps, slots, dist):
     rep = {"value": round(world * n / elapsed, 3), "unit": "proofs/s", "proofs": world * n, "verified": ok,
            "workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
            "constraints": b.n_constraints, "domain": key.domain_size, "ms_per_step": round(elapsed / steps * 1e3, 3),
-           "stage_ms_isolated_per_proof": {k: round(v[0] / max(1, nprof), 3) for k, v in prof.items()},
+           "stage_ms_isolated_per_proof": stage_times(prof, nprof),
            "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key, traffic=False,
                                    nprof=nprof)}
     key.close()
@@ -681,7 +695,7 @@ def launch_ranks(n):
 
 def report(args, world, elapsed, n_timed_all, verified_all, prof, nprof, key, config, extra):
     """The bench JSON line (rank 0).  `extra`: roofline / end_to_end / c5 / cpu_baseline fields."""
-    stage_ms = {k: round(v[0] / max(1, nprof), 3) for k, v in prof.items()}  # summed event time per proof
+    stage_ms = stage_times(prof, nprof)
     line = {
         "metric": METRIC, "value": round(n_timed_all / elapsed, 4), "unit": "proofs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),

@@ -5,6 +5,7 @@
 # VARIANT: LIB[+VAR=VALUE...]; LIB "cur" = the in-tree libzkfl.so, otherwise build_ab/<LIB>/libzkfl.so
 # (tools/build_ab.sh NAME "-DKNOB=..." builds one on the CPU first); +VAR=VALUE sets an environment
 # knob for that variant's runs (e.g. cur+ZKFL_STAGGER=1).
+# AB_PROBE=tools/c5_probe.py runs that probe instead of tools/ko_probe.py (same one-line output).
 # Output: gpurun_out/TAG/ab.log (every line) and a per-variant summary (mean, min, max, spread).
 # A run that fails, times out or crashes ends the script (nothing is retried).
 set -o pipefail
@@ -14,7 +15,7 @@ VARS=()
 while [ $# -gt 0 ] && [ "$1" != "--" ]; do VARS+=("$1"); shift; done
 [ "${1:-}" = "--" ] && shift
 PROBE=("$@")
-[ ${#PROBE[@]} -eq 0 ] && PROBE=(--steps 40 --warmup 6)
+[ ${#PROBE[@]} -eq 0 ] && [ -z "${AB_PROBE:-}" ] && PROBE=(--steps 40 --warmup 6)
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
@@ -23,7 +24,7 @@ for r in $(seq 1 "$ROUNDS"); do
     IFS=+ read -r -a parts <<< "$v"
     base=${parts[0]}
     if [ "$base" = cur ]; then lib=""; else lib=build_ab/$base/libzkfl.so; fi
-    line=$(env ZKFL_LIB="$lib" "${parts[@]:1}" timeout -k 10 180 python -u tools/ko_probe.py "${PROBE[@]}" \
+    line=$(env ZKFL_LIB="$lib" "${parts[@]:1}" timeout -k 10 180 python -u "${AB_PROBE:-tools/ko_probe.py}" "${PROBE[@]}" \
            2>>"$OUT/stderr.log" | tail -n 1)
     rc=$?
     [ $rc -ne 0 ] && { echo "$v round $r failed (rc $rc)"; exit $rc; }

@@ -785,11 +785,21 @@ template <class S>
 constexpr int msm_wsum_q0() {
   return sizeof(typename S::T) == 32 ? MSM_G1_WSUM_Q : MSM_G2_WSUM_Q;
 }
+// Q0 of the latency schedule's reduction (one proof alone, msm_tails(..., fast = true)): 4 buckets
+// per level-0 lane, 128 level-0 blocks, a 128-lane level 1 -- about 45 dependent point operations
+// on the chain instead of ~70, for ~1.8x the reduction's (small) work
+constexpr int MSM_WSUM_Q_FAST = 4;
+// lanes of a reduction block: level 0 one wave (MSM_RB), level 1 one lane per level-0 block
+template <bool L0, int Q0>
+constexpr int msm_wsum_rb() {
+  return L0 || MSM_NB / (MSM_RB * Q0) <= MSM_RB ? MSM_RB : MSM_NB / (MSM_RB * Q0);
+}
 static_assert(MSM_NB % (MSM_RB * MSM_G1_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G1_WSUM_Q) <= MSM_RB &&
-                  MSM_NB % (MSM_RB * MSM_G2_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G2_WSUM_Q) <= MSM_RB,
-              "two reduction levels cover the buckets");
-template <class F, int MINW, bool L0, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__(MSM_RB * MsmIO<F>::LANES) __attribute__((amdgpu_waves_per_eu(MINW)))
+                  MSM_NB % (MSM_RB * MSM_G2_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G2_WSUM_Q) <= MSM_RB &&
+                  MSM_NB % (MSM_RB * MSM_WSUM_Q_FAST) == 0 && msm_wsum_rb<false, MSM_WSUM_Q_FAST>() <= 2 * MSM_RB,
+              "two reduction levels cover the buckets; red_a / red_s hold 2 x the level-1 block");
+template <class F, int MINW, bool L0, int Q0, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__((msm_wsum_rb<L0, Q0>() * MsmIO<F>::LANES)) __attribute__((amdgpu_waves_per_eu(MINW)))
 k_msm_wsum(const MsmTailArgs<S> ta) {
   ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
   ZK_LIGHT();
@@ -798,15 +808,16 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
   const int yb = blockIdx.y;
   const XYZZ<S>* __restrict__ in_a = L0 ? ta.buckets[yb] : ta.red_a[yb];
   const XYZZ<S>* __restrict__ in_s = L0 ? ta.buckets[yb] : ta.red_s[yb];
-  constexpr int Q0 = msm_wsum_q0<S>(), B0 = MSM_NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
+  constexpr int B0 = MSM_NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
+  constexpr int RB = msm_wsum_rb<L0, Q0>();
   constexpr int N = L0 ? MSM_NB : B0, Q = L0 ? Q0 : 1;
   constexpr int log2g = L0 ? 0 : __builtin_ctz((unsigned)(Q0 * MSM_RB));
   XYZZ<S>* __restrict__ out_a = L0 ? ta.red_a[yb] : ta.out[yb];
-  XYZZ<S>* __restrict__ out_s = L0 ? ta.red_s[yb] : ta.red_s[yb] + MSM_RB;
+  XYZZ<S>* __restrict__ out_s = L0 ? ta.red_s[yb] : ta.red_s[yb] + RB;
   using IO = MsmIO<F>;
-  __shared__ XYZZ<S> sh[MSM_RB], shy[MSM_RB];
+  __shared__ XYZZ<S> sh[RB], shy[RB];
   const int t = threadIdx.x / IO::LANES;
-  const int i0 = (blockIdx.x * MSM_RB + t) * Q;  // this lane's items [i0, i0 + Q)
+  const int i0 = (blockIdx.x * RB + t) * Q;  // this lane's items [i0, i0 + Q)
   XYZZ<F> R = xyzz_inf<F>(), y = xyzz_inf<F>();
   if constexpr (L0) {  // serial fold over Q buckets (a = s: the buckets themselves, g = 1)
     XYZZ<F> W = xyzz_inf<F>();
@@ -821,10 +832,10 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
     y = IO::ld(in_a, i0);
   }
 #pragma unroll 1
-  for (int d = 1; d < MSM_RB; d <<= 1) {  // suffix scan of s
+  for (int d = 1; d < RB; d <<= 1) {  // suffix scan of s
     IO::st(sh, t, R);
     __syncthreads();
-    if (t + d < MSM_RB) R = xyzz_add<F>(R, IO::ld(sh, t + d));
+    if (t + d < RB) R = xyzz_add<F>(R, IO::ld(sh, t + d));
     __syncthreads();
   }
   // The tree sums of R_{t>=1} (x) and of a (y) side by side: at step d, lanes [0, d) add x
@@ -832,7 +843,7 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
   IO::st(sh, t, t >= 1 ? R : xyzz_inf<F>());
   IO::st(shy, t, y);
   __syncthreads();
-  constexpr int H = MSM_RB / 2;
+  constexpr int H = RB / 2;
   const bool ty = t >= H;
   const int tt = ty ? t - H : t;
   XYZZ<S>* tree = ty ? shy : sh;
@@ -942,7 +953,10 @@ uint32_t msm_resident_chunks() {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_msm_accumulate<FC, AW>, 64, 0) != hipSuccess) return 0;
   if (ncu <= 0 || nb <= 0) return 0;
-  return (uint32_t)ncu * (uint32_t)nb * (64u / MsmIO<FC>::LANES);
+  const uint32_t t = (uint32_t)ncu * (uint32_t)nb * (64u / MsmIO<FC>::LANES);
+  // A/B knob: ZKFL_MSM_TARGET_SCALE=<x> resizes the target (x < 1: longer chunks, fewer items)
+  if (const char* e = getenv("ZKFL_MSM_TARGET_SCALE")) return std::max<uint32_t>(64, (uint32_t)(t * atof(e)));
+  return t;
 #endif
 }
 
@@ -959,8 +973,8 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
     ZK_CHECK(hipMalloc(&t.item_val[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(XYZZ<F>)));
   }
   ZK_CHECK(hipMalloc(&t.buckets, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&t.red_a, 2 * MSM_RB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&t.red_s, 2 * MSM_RB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.red_a, 4 * MSM_RB * sizeof(XYZZ<F>)));  // <= 2 level-1 blocks (fast: 128 lanes)
+  ZK_CHECK(hipMalloc(&t.red_s, 4 * MSM_RB * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.nnz, sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&t.live, MSM_LIVE_LEVELS * sizeof(uint32_t)));
   return hipSuccess;
@@ -1087,9 +1101,10 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
 
 // Tails of n accumulated MSMs in one batch: stitching levels until one lane holds every
 // remaining item (item counts here are host-side upper bounds; the kernels use each nnz), then
-// the two weighted-reduction levels, the last writing outs[i].
+// the two weighted-reduction levels, the last writing outs[i].  fast: the latency schedule's
+// reduction (MSM_WSUM_Q_FAST: shorter dependent chain, more waves).
 template <class F>
-hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {
+hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast = false) {
   if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
@@ -1109,9 +1124,14 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
     cur ^= 1;
   }
   if (ZK_KNOCKOUT & 16) return hipGetLastError();
-  hipLaunchKernelGGL((k_msm_wsum<FC, TW, true>), dim3(MSM_NB / (MSM_RB * msm_wsum_q0<F>()), n), dim3(MSM_RB * LN), 0,
-                     st, ta);
-  hipLaunchKernelGGL((k_msm_wsum<FC, TW, false>), dim3(1, n), dim3(MSM_RB * LN), 0, st, ta);
+  constexpr int Q0 = msm_wsum_q0<F>(), QF = MSM_WSUM_Q_FAST;
+  if (fast) {
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, QF>), dim3(MSM_NB / (MSM_RB * QF), n), dim3(MSM_RB * LN), 0, st, ta);
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, QF>), dim3(1, n), dim3(msm_wsum_rb<false, QF>() * LN), 0, st, ta);
+  } else {
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, Q0>), dim3(MSM_NB / (MSM_RB * Q0), n), dim3(MSM_RB * LN), 0, st, ta);
+    hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, Q0>), dim3(1, n), dim3(msm_wsum_rb<false, Q0>() * LN), 0, st, ta);
+  }
   return hipGetLastError();
 }
 
@@ -1152,8 +1172,8 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
                                          MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag) { \
     return msm_accumulate_sorted(b, keys, vals, t, st, prof, tag);                                       \
   }                                                                                                      \
-  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st) {         \
-    return msm_tails(t, outs, n, st);                                                                    \
+  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) { \
+    return msm_tails(t, outs, n, st, fast);                                                              \
   }                                                                                                      \
   hipError_t msm_tails_reset_##SUF(MsmTail<F>* const* t, int n, hipStream_t st) {                        \
     return msm_tails_reset(t, n, st);                                                                    \

@@ -177,7 +177,8 @@ constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs 
   hipError_t msm_accumulate_sorted_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, \
                                          MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag);  \
   /* stitching + bucket reduction of n <= MSM_TAIL_MAX accumulated MSMs -> outs[i] (device) */      \
-  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st);    \
+  hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st,     \
+                             bool fast = false);                                                      \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \
                            const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
 

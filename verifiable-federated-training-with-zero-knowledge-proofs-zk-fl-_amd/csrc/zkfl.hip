@@ -781,6 +781,13 @@ struct ProofSlot {
   hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
   MsmScratch<FqOps> g1s_b;
   MsmScratch<FqOps> g1s_a;  // A's sort scratch in the overlapped schedule (A beside C + H)
+  // graph replay (ZKFL_GRAPH=1): the one-stream proof chain captured once per witness address
+  struct Graph {
+    const Fr* w = nullptr;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ex = nullptr;
+  };
+  std::vector<Graph> graphs;
   bool busy = false;
   int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
@@ -858,6 +865,11 @@ void slot_release(ProofSlot* s) {
     if (st) (void)hipStreamSynchronize(st);
   msm_scratch_free_g1(s->g1s_b);
   msm_scratch_free_g1(s->g1s_a);
+  for (auto& gr : s->graphs) {
+    if (gr.ex) (void)hipGraphExecDestroy(gr.ex);
+    if (gr.g) (void)hipGraphDestroy(gr.g);
+  }
+  s->graphs.clear();
   for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
@@ -1065,6 +1077,13 @@ int enqueue_abc_ntt(zkfl_key* k, ProofSlot* s, const Fr* d_w, hipStream_t st, Pr
   return ZKFL_OK;
 }
 
+// The latency schedules reduce their buckets with the shorter-chain reduction (msm.h
+// MSM_WSUM_Q_FAST); ZKFL_FAST_WSUM=0 keeps the throughput form (A/B).
+bool lowlat_fast_wsum() {
+  static const bool on = !getenv("ZKFL_FAST_WSUM") || atoi(getenv("ZKFL_FAST_WSUM")) != 0;
+  return on;
+}
+
 // One proof alone (a batch of one: the CLI's `groth16 prove`, the API's prove): its latency is
 // the metric, and the GPU is mostly idle along the one-stream chain, so independent stages run on
 // side streams:
@@ -1101,13 +1120,13 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   HIP_TRY(hipStreamWaitEvent(sb, ev_b, 0), "wait");
   HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
                                    "msm_accumulate_g2"), "msm B2");
-  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb), "msm B2 tail");
+  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
   HIP_TRY(hipEventRecord(ev_b2, sb), "event");
   // lat1: the tails of A and B1, then T = s pi_A + r B1 and pi_a
   HIP_TRY(hipStreamWaitEvent(sa, ev_b, 0), "wait");
   {
     G1P* outs[2] = {s->res + 0, s->res + 1};
-    HIP_TRY(msm_tails_g1(tails, outs, 2, sa), "msm tails A, B1");
+    HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
   }
   hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
                      reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
@@ -1122,7 +1141,7 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
   {
     G1P* out2 = s->res + 2;
-    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st), "msm tail C+H");
+    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
   }
   HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
   HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
@@ -1172,7 +1191,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   HIP_TRY(hipStreamWaitEvent(sa, ev, 0), "wait");
   HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
                                    "msm_accumulate_g2"), "msm B2");
-  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb), "msm B2 tail");
+  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
   HIP_TRY(hipEventRecord(ev_b2, sb), "event");
   // lat1: B1 (B's pairs), A, their tails, then T = s pi_A + r B1 and pi_a
   HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], sa, prof,
@@ -1180,7 +1199,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   HIP_TRY(msm_accumulate_g1(k->bA, s->g1s_a, s->g1t[0], W, E, sa, prof, "msm_accumulate_g1"), "msm A");
   {
     G1P* outs[2] = {s->res + 0, s->res + 1};
-    HIP_TRY(msm_tails_g1(tails, outs, 2, sa), "msm tails A, B1");
+    HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
   }
   hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
                      reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
@@ -1195,7 +1214,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
   {
     G1P* out2 = s->res + 2;
-    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st), "msm tail C+H");
+    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
   }
   HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
   HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
@@ -1206,16 +1225,14 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   return ZKFL_OK;
 }
 
-int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain,
-                  int lowlat = 0) {
+// The device work of one proof on the slot's streams, after the host has put r, s and the GLV
+// halves into the pinned buffer.  graph: being captured (one stream): the events that only order
+// the one stream against itself are left out.
+int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, int plain, int lowlat, bool graph) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
   const size_t n = k->n;
-  memcpy(s->pinned + 256, rs_host, 64);
-  GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
-  glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
-  glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
   int pp = prof->begin("prove", st);
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
           "upload r,s");
@@ -1224,13 +1241,11 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     const int rc = lowlat == 2 ? enqueue_proof_lowlat2(ctx, k, s, d_w) : enqueue_proof_lowlat(ctx, k, s, d_w);
     if (rc) return rc;
     prof->end(pp, st, 1.0);
-    HIP_TRY(hipEventRecord(s->ev_done, st), "event");
-    HIP_TRY(hipGetLastError(), "launch");
     return ZKFL_OK;
   }
   const uint32_t* W = (const uint32_t*)d_w;
   const uint32_t* E = (const uint32_t*)s->extra;
-  HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
+  if (!graph) HIP_TRY(hipEventRecord(s->ev_ready, st), "event");
   MsmTail<FqOps>* tails[4] = {&s->g1t[0], &s->g1t[1], &s->g1t[2], &s->g1t[3]};
   // C + H as one MSM into tail 2 (res[2] = C' + H, res[3] = infinity); the parity hook (plain)
   // keeps them apart
@@ -1281,7 +1296,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(msm_accumulate_sorted_g2(k->bB2, sB.keys_out, sB.vals_out, s->g2t, st, prof,
                                      "msm_accumulate_g2"), "msm B2");
     HIP_TRY(msm_tails_g2(&t2, &o2, 1, st), "msm B2 tail");
-    HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
+    if (!graph) HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
   } else {
     HIP_TRY(msm_accumulate_g1(k->bB1, sB, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   }
@@ -1308,7 +1323,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
     HIP_TRY(msm_tails_g1(tails, outs, ntails, st), "msm tails");
   }
-  HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
+  if (!graph) HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (plain == 2) {
     hipLaunchKernelGGL(k_part_out, dim3(1), dim3(64), 0, st, s->res, s->resB2, s->d_parts);
     HIP_TRY(hipMemcpyAsync(s->pinned + 512, s->d_parts, PART_WORDS * 4, hipMemcpyDeviceToHost, st), "download part");
@@ -1321,7 +1336,61 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
     HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   }
   prof->end(pp, st, 1.0);
-  HIP_TRY(hipEventRecord(s->ev_done, st), "event");
+  return ZKFL_OK;
+}
+
+// Graph replay of the one-stream chain (ZKFL_GRAPH=1): a slot captures its proof's ~40 launches
+// once per witness address (a batch cycles its slots over a few witness buffers) and then
+// launches the graph -- one host call per proof instead of one per kernel.  Kernel arguments are
+// the slot's own buffers, the key's and the witness address, all fixed per cache entry; r and s
+// reach the device through the captured copy from the slot's pinned buffer.
+int enqueue_proof_graph(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, int plain) {
+  hipStream_t st = s->st_main;
+  ProofSlot::Graph* gr = nullptr;
+  for (auto& x : s->graphs)
+    if (x.w == d_w) gr = &x;
+  if (!gr) {
+    if (s->graphs.size() >= 8) {  // bounded cache: drop the oldest
+      ProofSlot::Graph& o = s->graphs.front();
+      if (o.ex) (void)hipGraphExecDestroy(o.ex);
+      if (o.g) (void)hipGraphDestroy(o.g);
+      s->graphs.erase(s->graphs.begin());
+    }
+    ProofSlot::Graph ng;
+    ng.w = d_w;
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "begin capture");
+    const int rc = enqueue_proof_body(ctx, k, s, d_w, plain, 0, true);
+    const hipError_t ec = hipStreamEndCapture(st, &ng.g);
+    if (rc) {
+      if (ng.g) (void)hipGraphDestroy(ng.g);
+      return rc;
+    }
+    HIP_TRY(ec, "end capture");
+    const hipError_t ei = hipGraphInstantiate(&ng.ex, ng.g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(ng.g);
+      return hip_fail(ei, "graph instantiate");
+    }
+    s->graphs.push_back(ng);
+    gr = &s->graphs.back();
+  }
+  HIP_TRY(hipGraphLaunch(gr->ex, st), "graph launch");
+  return ZKFL_OK;
+}
+
+int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const uint32_t rs_host[16], int plain,
+                  int lowlat = 0) {
+  Profiler* prof = &ctx->prof;
+  memcpy(s->pinned + 256, rs_host, 64);
+  GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
+  glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
+  glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
+  static const int use_graph = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 0;
+  const bool graph = use_graph && !lowlat && plain == 0 && !prof->on && !prof->serialize && !s->st_g2 &&
+                     k->share_b && !ZK_KNOCKOUT;
+  const int rc = graph ? enqueue_proof_graph(ctx, k, s, d_w, plain) : enqueue_proof_body(ctx, k, s, d_w, plain, lowlat, false);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(s->ev_done, s->st_main), "event");
   HIP_TRY(hipGetLastError(), "launch");
   return ZKFL_OK;
 }
