@@ -16,6 +16,8 @@ Writes <out>/summary.json, <out>/waves.npz (kind, t0, t1 in 10-ns ticks) for the
 proofs' window and <out>/waves_isolated.npz (every record of the isolated proofs).
 
     ZKFL_LIB=build_ab/wtrace/libzkfl.so python3 tools/wtrace.py --proofs 120 --out gpurun_out/wt
+    --c5 ROUNDS: instead, config 5 (bench.py's c5 leg: ROUNDS federated rounds of 8 clients x
+    {training, secure aggregation} through zkfl_groth16_full_prove_multi, witnesses included)
 """
 import argparse
 import json
@@ -38,7 +40,7 @@ SYMBOL = {"acc": "k_msm_accumulate", "stitch": "k_msm_stitch", "wsum0": "k_msm_w
           "sort_count": "k_msm_bin_count", "sort_scan": "k_msm_bin_scan", "sort_scatter": "k_msm_bin_scatter",
           "sort_bins": "k_msm_bin_sort", "tail_reset": "k_msm_tail_reset", "ntt_cols_inv": "k_ntt_colsILb1",
           "ntt_lds": "k_ntt_lds_pair", "ntt_cols_fwd": "k_ntt_colsILb0", "abc": "k_abc_chunks", "abc_rows": "k_abc_rows",
-          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_set_extra"}
+          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_set_extra", "witness": "k_wit_level"}
 
 
 def kind_name(k):
@@ -106,6 +108,17 @@ def analyse(rec, n_proofs, shares):
         cur += dlt
         last = t
     out["acc_resident_share"] = round(busy / span, 4)
+    # share of the window with ANY instrumented wave resident (the rest: the GPU idle, waiting for
+    # the host or for uninstrumented work such as copies)
+    ev = np.concatenate([np.stack([t0, np.ones(len(t0), np.int64)], 1), np.stack([t1, -np.ones(len(t1), np.int64)], 1)])
+    ev = ev[np.lexsort((-ev[:, 1], ev[:, 0]))]
+    cur, last, busy = 0, lo, 0
+    for t, dlt in ev:
+        if cur > 0:
+            busy += t - last
+        cur += dlt
+        last = t
+    out["any_resident_share"] = round(busy / span, 4)
     out["simd_share_total"] = round(sum(v["mean_simd_share"] for v in out["kinds"].values()), 4)
     return out
 
@@ -143,6 +156,48 @@ def gantt(rec):
     return segs
 
 
+def c5_trace(args, shares, dt):
+    """Config 5 under the tracer: the c5 leg's keys and jobs (bench.py), one full_prove_multi call."""
+    import json as _json
+    sys.path.insert(0, ROOT)
+    import bench
+    from zkfl import circuits, clients, native, wprog, zkey
+    ctx = native.Context(0)
+    circ = {"train": circuits.build("sgd_verified", 8, 4, 3, 1000), "secagg": circuits.build("secure_masked_update", 4, 7)}
+    keys, progs, images = {}, {}, {}
+    for i, (nm, b) in enumerate(circ.items()):
+        zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0xC5 + i, alpha=3, beta=5, gamma=7, delta=11 + i))
+        keys[nm] = native.ProvingKey(ctx, zk)
+        keys[nm].set_slots(args.c5_slots)
+        images[nm] = wprog.compile_program(b)
+        progs[nm] = native.WitnessProgram(ctx, images[nm])
+
+    def jobs(nrounds, first):
+        out = []
+        for r in range(nrounds):
+            for tr, sa, _ in clients.federated_round(8, rnd=r + 1, first_id=first):
+                out += [("train", _json.dumps(tr)), ("secagg", _json.dumps(sa))]
+        return [(keys[nm], progs[nm], native.parse_inputs(images[nm], txt)) for nm, txt in out]
+    ctx.full_prove_multi(jobs(1, 1))
+    ctx.synchronize()
+    js = jobs(args.c5, 1)
+    cap = 200000 * (len(js) + 4)
+    ctx.wtrace_start(cap)
+    t = time.perf_counter()
+    ctx.full_prove_multi(js)
+    ctx.synchronize()
+    wall = time.perf_counter() - t
+    raw, n = ctx.wtrace_stop(cap)
+    rec = np.frombuffer(raw, dtype=dt)
+    out = analyse(rec, len(js), shares)
+    out["host_wall_ms_per_proof"] = wall * 1e3 / len(js)
+    out["proofs_per_s"] = len(js) / wall
+    out["records"], out["overflow"] = int(n), bool(n > cap)
+    np.savez_compressed(os.path.join(args.out, "waves_c5.npz"), rec=rec)
+    ctx.wtrace_free()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--proofs", type=int, default=120)
@@ -150,7 +205,25 @@ def main():
     ap.add_argument("--isolated", type=int, default=4, help="proofs run one at a time afterwards")
     ap.add_argument("--keep", type=int, default=30, help="proofs whose raw waves go to waves.npz")
     ap.add_argument("--out", default="gpurun_out/wtrace")
+    ap.add_argument("--c5", type=int, default=0, help="config-5 rounds to trace instead of M")
+    ap.add_argument("--c5-slots", type=int, default=8)
     args = ap.parse_args()
+    if args.c5:
+        from zkfl import native
+        os.makedirs(args.out, exist_ok=True)
+        dt = np.dtype([("kind", "<u4"), ("hwid", "<u4"), ("t0", "<u8"), ("t1", "<u8"), ("c0", "<u8"), ("c1", "<u8")])
+        shares = vgpr_share(native.LIB_PATH)
+        s = c5_trace(args, shares, dt)
+        with open(os.path.join(args.out, "summary_c5.json"), "w") as f:
+            json.dump(s, f, indent=1)
+        print(f"== c5: {s['proofs_per_s']:.1f} proofs/s under the tracer, {s['ms_per_proof']:.3f} ms per proof (trace "
+              f"window), any wave resident {100 * s['any_resident_share']:.1f}%, accumulation resident "
+              f"{100 * s['acc_resident_share']:.1f}%, SIMD share {s['simd_share_total']:.3f}")
+        for k, v in sorted(s["kinds"].items(), key=lambda kv: -kv[1]["wave_ms_per_proof"]):
+            print(f"   {k:14s} waves/proof {v['waves_per_proof']:9.1f}  wave-ms/proof {v['wave_ms_per_proof']:9.3f}  "
+                  f"mean wave {v['mean_wave_us']:8.1f} us  resident {v['mean_resident_waves']:7.1f}  "
+                  f"SIMD share {v['mean_simd_share']:.4f}")
+        return
     from zkfl import circuits, clients, native, wprog, zkey
     os.makedirs(args.out, exist_ok=True)
     b = circuits.build("sgd_verified", 128, 4, 7, 1000)

@@ -25,6 +25,7 @@
 #include "field.h"
 #include "host_parse.h"
 #include "witness.h"
+#include "wtrace.h"
 #include "zkfl.h"
 
 namespace zkfl {
@@ -70,6 +71,7 @@ ZK_DEV Fr lc_eval(const ProgView& P, const Fr* w, uint32_t lc) {
 // the shuffles; lanes without a job compute on zeros and store nothing.
 __global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t op0, uint32_t cnt, uint32_t T,
                                                 Fr* W) {
+  ZK_WT(WT_WITNESS);
   const uint32_t lane = threadIdx.x, G = 64 / T;
   const uint32_t g = lane / T, i = lane - g * T;
   const size_t job = (size_t)blockIdx.x * G + g;
@@ -148,6 +150,7 @@ __global__ __launch_bounds__(64) void k_wit_inputs(size_t n, uint32_t nw, uint32
 }
 
 __global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t op0, uint32_t cnt, Fr* W) {
+  ZK_WT(WT_WITNESS);
   size_t l = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= n * cnt) return;
   const size_t j = l / cnt;
@@ -392,5 +395,7 @@ int wprog_run(const WProg* p, size_t n, const uint8_t* inputs, Fr* const* outs_h
     if (q) (void)hipFree(q);
   return rc;
 }
+
+hipError_t zk_wtrace_bind_wit(const WtBuf& b) { return zk_wtrace_bind_tu(b); }
 
 }  // namespace zkfl

@@ -77,9 +77,10 @@ static inline hipError_t zk_wtrace_bind_tu(const WtBuf& b) {
 static inline hipError_t zk_wtrace_bind_tu(const WtBuf&) { return hipErrorNotSupported; }
 #endif
 
-// binders of the other translation units (msm_g1.hip, msm_g2.hip, ntt.hip)
+// binders of the other translation units (msm_g1.hip, msm_g2.hip, ntt.hip, witness.hip)
 hipError_t zk_wtrace_bind_g1(const WtBuf& b);
 hipError_t zk_wtrace_bind_g2(const WtBuf& b);
 hipError_t zk_wtrace_bind_ntt(const WtBuf& b);
+hipError_t zk_wtrace_bind_wit(const WtBuf& b);
 
 }  // namespace zkfl

@@ -2487,6 +2487,7 @@ int zkfl_debug_wtrace(zkfl_ctx* ctx, int op, uint32_t cap, void* out, uint32_t* 
     if (e == hipSuccess) e = zk_wtrace_bind_g1(b);
     if (e == hipSuccess) e = zk_wtrace_bind_g2(b);
     if (e == hipSuccess) e = zk_wtrace_bind_ntt(b);
+    if (e == hipSuccess) e = zk_wtrace_bind_wit(b);
     return e;
   };
   HIP_TRY(hipDeviceSynchronize(), "wave trace: sync");
