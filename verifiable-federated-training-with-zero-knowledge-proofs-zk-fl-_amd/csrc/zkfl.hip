@@ -2528,7 +2528,12 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
   if (rc == ZKFL_OK && MSM_MERGE_CH && !key->dbg_zero) {  // see zkfl_key::dbg_zero
     const size_t bytes = std::max<size_t>(key->nVars, (size_t)key->n + 4) * 32;
     hipError_t e = hipMalloc(&key->dbg_zero, bytes);
-    if (e == hipSuccess) e = hipMemset(key->dbg_zero, 0, bytes);
+    // on the slot's stream and waited for: hipMemset is asynchronous to the host and runs on the
+    // null stream, which the slots' non-blocking streams do not wait for -- the MSMs below read
+    // the zeros, and a recycled allocation (a freed key's memory) is not zero.  (Found as a
+    // parity failure that appeared only after earlier tests had freed large keys.)
+    if (e == hipSuccess) e = hipMemsetAsync(key->dbg_zero, 0, bytes, s->st_main);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->st_main);
     if (e != hipSuccess) rc = hip_fail(e, "parity hook zeros");
   }
   if (rc == ZKFL_OK && s->busy) rc = wait_slot(s);

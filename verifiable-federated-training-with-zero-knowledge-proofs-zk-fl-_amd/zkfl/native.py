@@ -193,13 +193,23 @@ class Context:
     """One device, one HIP stream (one process per GPU for multi-GPU)."""
 
     def __init__(self, device: int = 0):
+        import weakref
         h = _P()
         check(lib().zkfl_ctx_create(device, C.byref(h)))
         self.h = h
         self.device = device
+        # keys, programs and resident witnesses made on this context: closed before it, so none
+        # outlives the context it points into (a key freed after its context reads freed memory)
+        self._deps = weakref.WeakSet()
+
+    def _own(self, obj):
+        self._deps.add(obj)
+        return obj
 
     def close(self):
         if self.h:
+            for d in list(self._deps):
+                d.close()
             lib().zkfl_ctx_destroy(self.h)
             self.h = None
 
@@ -468,6 +478,7 @@ class ProvingKey:
         self.h = h
         self.shard, self.n_shards = shard, n_shards
         self.ctx = ctx
+        ctx._own(self)
         nv, npub, dom = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib().zkfl_key_info(h, C.byref(nv), C.byref(npub), C.byref(dom)))
         self.n_vars, self.n_public, self.domain_size = nv.value, npub.value, dom.value
@@ -574,10 +585,12 @@ class ResidentWitness:
     def __init__(self, key: ProvingKey, wtns: bytes | None = None, handle=None):
         if handle is not None:
             self.h = handle
+            key.ctx._own(self)
             return
         h = _P()
         check(lib().zkfl_witness_upload(key.ctx.h, key.h, wtns, len(wtns), C.byref(h)))
         self.h = h
+        key.ctx._own(self)
 
     def close(self):
         if self.h:
@@ -610,6 +623,7 @@ class WitnessProgram:
         h = _P()
         check(lib().zkfl_wprog_load(ctx.h, image, len(image), C.byref(h)))
         self.h, self.ctx = h, ctx
+        ctx._own(self)
         nw, ni, npub = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib().zkfl_wprog_info(h, C.byref(nw), C.byref(ni), C.byref(npub)))
         self.n_wires, self.n_inputs, self.n_public = nw.value, ni.value, npub.value
