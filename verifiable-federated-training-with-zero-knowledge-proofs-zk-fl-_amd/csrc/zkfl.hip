@@ -1084,6 +1084,15 @@ bool lowlat_fast_wsum() {
   return on;
 }
 
+// Small keys (domain <= 2^ZKFL_FAST_WSUM_LOGN, default 2^16: config 5's circuits) take the
+// shorter-chain reduction in batches too: their proofs are chains of small latency-bound kernels
+// that leave most of the GPU idle (config-5 wave trace: SIMD share 0.135 with a wave resident 99%
+// of the time), so the reduction's extra waves are free and its shorter chain is not.
+bool small_key_fast_wsum(const zkfl_key* k) {
+  static const int logn = getenv("ZKFL_FAST_WSUM_LOGN") ? atoi(getenv("ZKFL_FAST_WSUM_LOGN")) : 16;
+  return lowlat_fast_wsum() && k->logn <= logn;
+}
+
 // One proof alone (a batch of one: the CLI's `groth16 prove`, the API's prove): its latency is
 // the metric, and the GPU is mostly idle along the one-stream chain, so independent stages run on
 // side streams:
@@ -1295,7 +1304,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
     HIP_TRY(msm_accumulate_sorted_g2(k->bB2, sB.keys_out, sB.vals_out, s->g2t, st, prof,
                                      "msm_accumulate_g2"), "msm B2");
-    HIP_TRY(msm_tails_g2(&t2, &o2, 1, st), "msm B2 tail");
+    HIP_TRY(msm_tails_g2(&t2, &o2, 1, st, small_key_fast_wsum(k)), "msm B2 tail");
     if (!graph) HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
   } else {
     HIP_TRY(msm_accumulate_g1(k->bB1, sB, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
@@ -1321,7 +1330,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   {
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
-    HIP_TRY(msm_tails_g1(tails, outs, ntails, st), "msm tails");
+    HIP_TRY(msm_tails_g1(tails, outs, ntails, st, small_key_fast_wsum(k)), "msm tails");
   }
   if (!graph) HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (plain == 2) {
