@@ -369,9 +369,6 @@ constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (th
 static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 256 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
 constexpr int MSM_SORT_BT = 1024;         // threads of the scan workgroup
 constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin workgroup
-#ifndef MSM_SORT_SMALL_BIN
-#define MSM_SORT_SMALL_BIN 4096  // <= this many entries per high bin: 256-thread bins workgroups
-#endif
 static_assert(MSM_SORT_BINT >= MSM_SORT_NL && MSM_SORT_BINT <= 1024, "bins: one thread per low counter");
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
@@ -484,8 +481,8 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
 }
 
 // One workgroup per high bin: [bin_start[b], bin_start[b+1]) of (tk, tv) -> buckets in (ko, vo).
-// BINT threads per workgroup: MSM_SORT_BINT (1024) for the large MSMs; a small MSM (a few
-// entries per thread at most) takes 256, a quarter of the waves for the same placing work.
+// BINT threads per workgroup (MSM_SORT_BINT).  A 256-thread variant for small MSMs measured
+// neutral on config 5 (1906.7 vs 1894.0 proofs/s, 3 alternations, profiles/r04_ab_c5_small_keys.log).
 template <int BINT>
 __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
                                                       const uint16_t* __restrict__ tk,
@@ -1046,15 +1043,8 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
     pl.ko_sorted = 1;
     hipLaunchKernelGGL(k_msm_bin_scatter, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
                        b.extra_start, b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
-    // entries per high bin, bounded by all 16 digits of every base being non-zero
-    static const size_t small_bin =
-        getenv("ZKFL_SORT_SMALL_BIN") ? strtoul(getenv("ZKFL_SORT_SMALL_BIN"), nullptr, 10) : MSM_SORT_SMALL_BIN;
-    if ((size_t)b.n * MSM_W / MSM_SORT_HB <= small_bin)
-      hipLaunchKernelGGL(k_msm_bin_sort<256>, dim3(MSM_SORT_HB), dim3(256), 0, st, bin_start, pl.keys_in, pl.vals_in,
-                         pl.keys_out, pl.vals_out);
-    else
-      hipLaunchKernelGGL(k_msm_bin_sort<MSM_SORT_BINT>, dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st, bin_start,
-                         pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+    hipLaunchKernelGGL(k_msm_bin_sort<MSM_SORT_BINT>, dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st, bin_start,
+                       pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
   }
   return hipGetLastError();
 #else
