@@ -261,19 +261,26 @@ def latency_leg(key, ws, n=24):
             "path": "prove_batch of one resident witness -> low-latency schedule (3 streams), host wall clock"}
 
 
-def roofline_pass(key, ctx, ws, slots, n=12):
+def roofline_pass(key, ctx, ws, slots, n=6, reps=3):
     """Per-kernel HIP-event timings with every kernel running alone (one slot, a proof's
-    streams serialized onto one), after the timed region: the roofline's average launch time."""
+    streams serialized onto one), after the timed region: the roofline's average launch time.
+    `reps` passes of n proofs; the pass with the shortest summed proof time is kept -- the boxes
+    show occasional ~10 ms stalls of a whole process (the latency leg's max), and one such stall
+    inside a pass moved the mean G1 launch time 2x while its median stayed put."""
     key.set_slots(1)
     key.prove_batch(ws[:1])
-    ctx.profile_reset()
-    ctx.set_profiling(True, serialize=True)
-    key.prove_batch([ws[i % len(ws)] for i in range(n)])
-    ctx.set_profiling(False)
-    prof = {k: ctx.profile(k) for k in PROFILED}
+    best = None
+    for _ in range(reps):
+        ctx.profile_reset()
+        ctx.set_profiling(True, serialize=True)
+        key.prove_batch([ws[i % len(ws)] for i in range(n)])
+        ctx.set_profiling(False)
+        prof = {k: ctx.profile(k) for k in PROFILED}
+        if best is None or prof["prove"][0] < best["prove"][0]:
+            best = prof
     ctx.profile_reset()
     key.set_slots(slots)
-    return prof, n
+    return best, n
 
 
 def _pmc_traffic(kernel):
@@ -788,6 +795,13 @@ def main():
     t0 = time.perf_counter()
     zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
     log(f"[bench r{rank}] dev setup {len(zk) / 1e6:.0f} MB zkey ({time.perf_counter() - t0:.1f} s)")
+    # config 5 first, with only its own two keys on the device: the main key's slots (20 streams and
+    # their scratch) stay out of its way (the same c5 code read 1894 proofs/s alone and 1440 after
+    # the main legs on one box, round 4)
+    c5 = c5w = None
+    if args.c5_rounds:
+        c5, c5w = c5_leg(ctx, rank, world, args.c5_rounds, args.c5_slots, dist, args.c5_weak_rounds)
+        log(f"[bench r{rank}] config 5: {c5}; weak: {c5w}")
     t0 = time.perf_counter()
     key = native.ProvingKey(ctx, zk)
     key.set_slots(args.slots)
@@ -830,10 +844,6 @@ def main():
         r_.close()
     wp.close()
     key.set_slots(1)
-    c5 = c5w = None
-    if args.c5_rounds:
-        c5, c5w = c5_leg(ctx, rank, world, args.c5_rounds, args.c5_slots, dist, args.c5_weak_rounds)
-        log(f"[bench r{rank}] config 5: {c5}; weak: {c5w}")
     extra = None
     if args.extra_circuit and args.extra_circuit != "none" and args.extra_circuit != args.circuit:
         extra = extra_circuit_leg(ctx, rank, world, args.extra_circuit, args.extra_steps, args.slots, dist)

@@ -781,7 +781,7 @@ struct ProofSlot {
   hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
   MsmScratch<FqOps> g1s_b;
   MsmScratch<FqOps> g1s_a;  // A's sort scratch in the overlapped schedule (A beside C + H)
-  // graph replay (ZKFL_GRAPH=1): the one-stream proof chain captured once per witness address
+  // graph replay (default on; ZKFL_GRAPH=0 off): the one-stream proof chain captured once per witness address
   struct Graph {
     const Fr* w = nullptr;
     hipGraph_t g = nullptr;
@@ -1348,7 +1348,9 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   return ZKFL_OK;
 }
 
-// Graph replay of the one-stream chain (ZKFL_GRAPH=1): a slot captures its proof's ~40 launches
+// Graph replay of the one-stream chain (the default; ZKFL_GRAPH=0 launches kernel by kernel;
+// config 5 +3.5%, 1894 vs 1831 proofs/s, M +0.6% inside the spread, 3 same-box alternations,
+// profiles/r04_ab_c5_small_keys.log, r04_ab_m_graph_target.log): a slot captures its proof's ~40 launches
 // once per witness address (a batch cycles its slots over a few witness buffers) and then
 // launches the graph -- one host call per proof instead of one per kernel.  Kernel arguments are
 // the slot's own buffers, the key's and the witness address, all fixed per cache entry; r and s
@@ -1394,7 +1396,7 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
   glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
   glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
-  static const int use_graph = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 0;
+  static const int use_graph = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 1;
   const bool graph = use_graph && !lowlat && plain == 0 && !prof->on && !prof->serialize && !s->st_g2 &&
                      k->share_b && !ZK_KNOCKOUT;
   const int rc = graph ? enqueue_proof_graph(ctx, k, s, d_w, plain) : enqueue_proof_body(ctx, k, s, d_w, plain, lowlat, false);
@@ -1465,7 +1467,10 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
     // 1: A and B before ABC / NTT, 2: overlapped)
     static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
-    if (rc == ZKFL_OK) rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, n == 1 ? lowlat : 0);
+    // A/B knob: ZKFL_LOWLAT_BATCH=1 runs every proof of a batch on the low-latency schedule
+    static const bool lowlat_batch = getenv("ZKFL_LOWLAT_BATCH") && atoi(getenv("ZKFL_LOWLAT_BATCH")) != 0;
+    if (rc == ZKFL_OK)
+      rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, (n == 1 || lowlat_batch) ? lowlat : 0);
     if (rc) break;
     s->busy = true;
   }
