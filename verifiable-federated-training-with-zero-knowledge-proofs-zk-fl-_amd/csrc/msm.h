@@ -1084,8 +1084,11 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
       done = true;
     }
   }
+  // measurement knob: ZKFL_ACC_PAD_LDS=<bytes> reserves unused LDS per accumulation block, which
+  // lowers the number of resident waves without changing the chunking (PMC traffic attribution)
+  static const size_t pad_lds = getenv("ZKFL_ACC_PAD_LDS") ? strtoul(getenv("ZKFL_ACC_PAD_LDS"), nullptr, 10) : 0;
   if (!done && !((ZK_KNOCKOUT & 64) && LN == 1))
-    hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), 0, st, keys, vals,
+    hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), pad_lds, st, keys, vals,
                        b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, t.target, t.live);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
   return hipGetLastError();

@@ -497,6 +497,7 @@ class ProvingKey:
     def set_slots(self, slots: int):
         """Proofs kept in flight by prove_batch (each slot = 3 HIP streams + scratch)."""
         check(lib().zkfl_key_set_slots(self.h, slots))
+        self.slots = slots
 
     def prove(self, wtns: bytes, rs: bytes | None = None):
         """-> (proof 256 B, [public signal ints])"""
