@@ -249,8 +249,8 @@ def latency_leg(key, ws, n=24):
     prove_batch([w]) -- witness resident, from the call to the proof bytes in host memory --, n
     times after a warm-up call: median, spread and the verdict's <= 4.5 ms target."""
     import statistics
-    # one slot, as a CLI process holds: the 20 idle slot streams of the throughput legs cost a lone
-    # proof ~0.4 ms (4.5-4.6 ms median with them, 4.1 ms with one, round-4 boxes)
+    # one slot, as a CLI process holds (idle slots measured no effect: 4.12 vs 4.13 ms with 20 / 1,
+    # profiles/r04_ab_latency_slots.log)
     slots = getattr(key, "slots", None)
     key.set_slots(1)
     key.prove_batch(ws[:1])
@@ -824,6 +824,11 @@ def main():
     warm_w = [res[i % len(res)] for i in range(args.warmup * args.slots)]
     rs = draw_rs(n_timed)
 
+    # one proof alone first, on the idle chip a CLI invocation meets (measured after the 20-slot
+    # run it read 4.49 / 4.64 ms on two boxes, against 4.06-4.22 ms for tools/ko_probe.py --latency
+    # on a fresh process on others)
+    lat = latency_leg(key, res)
+    log(f"[bench r{rank}] one proof alone: {lat}")
     elapsed, proofs = timed_run(key, warm_w, steps_w, rs, ctx, dist)
     assert len(proofs) == n_timed and all(len(p) == 256 for p in proofs)
     pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]   # wtns v2: header 76 B, wire 0 = 1
@@ -832,8 +837,6 @@ def main():
     verified_all = _sum_over_ranks(verified, dist)
     if verified_all != n_timed * world:
         raise SystemExit(f"[bench r{rank}] {n_timed * world - verified_all} timed proofs do not verify")
-    lat = latency_leg(key, res)
-    log(f"[bench r{rank}] one proof alone: {lat}")
     prof, nprof = roofline_pass(key, ctx, res, args.slots)
     kinfo = KeyInfo(key.n_vars, key.n_public, key.domain_size)
     e2e = None
