@@ -194,6 +194,19 @@ def c5_trace(args, shares, dt):
     out["proofs_per_s"] = len(js) / wall
     out["records"], out["overflow"] = int(n), bool(n > cap)
     np.savez_compressed(os.path.join(args.out, "waves_c5.npz"), rec=rec)
+    # the batch chain of one small proof with nothing beside it: the training key on one slot, two
+    # proofs through the same pipe (witness group, then the proofs one after the other); the
+    # timeline of the second
+    keys["train"].set_slots(1)
+    one = [j for j in jobs(1, 1) if j[0] is keys["train"]][:2]
+    ctx.full_prove_multi(one)
+    ctx.synchronize()
+    ctx.wtrace_start(200000)
+    ctx.full_prove_multi(one)
+    ctx.synchronize()
+    raw, n = ctx.wtrace_stop(200000)
+    rec1 = np.frombuffer(raw, dtype=dt)
+    out["isolated_gantt"] = gantt(rec1)
     ctx.wtrace_free()
     return out
 
@@ -223,6 +236,10 @@ def main():
             print(f"   {k:14s} waves/proof {v['waves_per_proof']:9.1f}  wave-ms/proof {v['wave_ms_per_proof']:9.3f}  "
                   f"mean wave {v['mean_wave_us']:8.1f} us  resident {v['mean_resident_waves']:7.1f}  "
                   f"SIMD share {v['mean_simd_share']:.4f}")
+        print("== c5 training proofs alone (witness group, then two proofs on one slot):")
+        for g in s["isolated_gantt"]:
+            print(f"   {g['kind']:14s} {g['start_us']:8.1f} .. {g['end_us']:8.1f} us  waves {g['waves']:6d}  "
+                  f"mean wave {g['mean_wave_us']:7.1f} us  clock {g['clock_GHz']} GHz")
         return
     from zkfl import circuits, clients, native, wprog, zkey
     os.makedirs(args.out, exist_ok=True)
