@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/sq3
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
-BENCH="$R/bench.py --steps 3 --warmup 1 --slots 1 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --c5-weak-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0"
+BENCH="$R/bench.py --steps 3 --warmup 1 --slots 1 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --c5-weak-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 --cli-runs 0"
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/sq" -o run -- python3 $BENCH > "$OUT/sq.log" 2>&1
 MIX=""
 n=0
