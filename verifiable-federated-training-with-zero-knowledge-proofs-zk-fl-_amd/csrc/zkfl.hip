@@ -778,7 +778,7 @@ struct ProofSlot {
   // events (B sorted and B1 accumulated | B2 final | T = s pi_A + r B1 final) and B's own sort
   // scratch, so C + H can sort on the main stream while B2 still reads B's pairs; made on first use
   hipStream_t st_lat[2] = {nullptr, nullptr};
-  hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_lat[4] = {nullptr, nullptr, nullptr, nullptr};
   MsmScratch<FqOps> g1s_b;
   MsmScratch<FqOps> g1s_a;  // A's sort scratch in the overlapped schedule (A beside C + H)
   // graph replay (default on; ZKFL_GRAPH=0 off): the one-stream proof chain captured once per witness address
@@ -870,7 +870,7 @@ void slot_release(ProofSlot* s) {
     if (gr.g) (void)hipGraphDestroy(gr.g);
   }
   s->graphs.clear();
-  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
+  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2], s->ev_lat[3]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
     if (st) (void)hipStreamDestroy(st);
@@ -1107,7 +1107,7 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   hipStream_t st = s->st_main;
   for (int i = 0; i < 2; i++)
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
-  for (int i = 0; i < 3; i++)
+  for (int i = 0; i < 4; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
   if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
   hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
@@ -1119,14 +1119,27 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   G2P* o2 = s->resB2;
   HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
   HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
-  HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
-  HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
-  HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
-                                   "msm_accumulate_g1"), "msm B1");
-  HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
-  HIP_TRY(hipEventRecord(ev_b, st), "event");
+  // A/B knob ZKFL_LOWLAT_BFIRST=1: B's sort first, so B2 (the G2 chain) starts before A and B1
+  static const bool bfirst = getenv("ZKFL_LOWLAT_BFIRST") && atoi(getenv("ZKFL_LOWLAT_BFIRST")) != 0;
+  hipEvent_t ev_b2start = bfirst ? s->ev_lat[3] : ev_b;
+  if (bfirst) {
+    HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
+    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    HIP_TRY(hipEventRecord(ev_b2start, st), "event");
+    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
+                                     "msm_accumulate_g1"), "msm B1");
+    HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+    HIP_TRY(hipEventRecord(ev_b, st), "event");
+  } else {
+    HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+    HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
+    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
+                                     "msm_accumulate_g1"), "msm B1");
+    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    HIP_TRY(hipEventRecord(ev_b, st), "event");
+  }
   // lat0: B2 and its tail
-  HIP_TRY(hipStreamWaitEvent(sb, ev_b, 0), "wait");
+  HIP_TRY(hipStreamWaitEvent(sb, ev_b2start, 0), "wait");
   HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
                                    "msm_accumulate_g2"), "msm B2");
   HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
@@ -1176,7 +1189,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   hipStream_t st = s->st_main;
   for (int i = 0; i < 2; i++)
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
-  for (int i = 0; i < 3; i++)
+  for (int i = 0; i < 4; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
   if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
   if (!s->g1s_a.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, st), "A sort scratch");
