@@ -80,6 +80,23 @@ def test_metric_key_by_path_equals_key_by_bytes(metric, gpu_ctx, tmp_path):
         k2.close()
 
 
+def test_metric_latency_schedule_graph_replay(metric):
+    """A batch of one takes the latency schedule; its per-stream segments are captured as graphs on
+    a witness address's second proof and replayed after (enqueue_proof_lowlat / run_segment).
+    Direct, captured and replayed proofs of one resident witness equal the one-stream batch proof
+    of the same (witness, r, s) -- which test_metric_proof_and_parts_bit_exact_vs_c_oracle pins to
+    the C oracle."""
+    _, _, key, _, wts = metric
+    w = key.upload(wts[1])
+    try:
+        rs = _le(0x1111) + _le(0x2222)
+        singles = [key.prove_batch([w], rs)[0] for _ in range(4)]
+        pair = key.prove_batch([w, w], rs + rs)
+        assert all(p == pair[0] for p in singles) and pair[0] == pair[1]
+    finally:
+        w.close()
+
+
 def test_metric_concurrent_slots_equal_single_slot(metric):
     """bench.py's concurrency (20 slots x 1 stream each over 28 HW queues): 40 proofs with
     distinct fixed (r, s) from the batch prover equal one-at-a-time proofs; 2 vs the oracle."""

@@ -778,7 +778,7 @@ struct ProofSlot {
   // events (B sorted and B1 accumulated | B2 final | T = s pi_A + r B1 final) and B's own sort
   // scratch, so C + H can sort on the main stream while B2 still reads B's pairs; made on first use
   hipStream_t st_lat[2] = {nullptr, nullptr};
-  hipEvent_t ev_lat[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_lat[3] = {nullptr, nullptr, nullptr};
   MsmScratch<FqOps> g1s_b;
   MsmScratch<FqOps> g1s_a;  // A's sort scratch in the overlapped schedule (A beside C + H)
   // graph replay (default on; ZKFL_GRAPH=0 off): the one-stream proof chain captured once per witness address
@@ -788,6 +788,12 @@ struct ProofSlot {
     hipGraphExec_t ex = nullptr;
   };
   std::vector<Graph> graphs;
+  // the latency schedule's per-stream segments, each captured as its own one-stream graph
+  // (enqueue_proof_lowlat): index = segment, entries per witness address
+  std::vector<Graph> seg_graphs[4];
+  // witness addresses seen once: a graph is captured on an address's second proof, so a one-off
+  // proof (a CLI run, a freshly uploaded witness) pays no capture
+  std::vector<const Fr*> seen;
   bool busy = false;
   int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
@@ -870,7 +876,14 @@ void slot_release(ProofSlot* s) {
     if (gr.g) (void)hipGraphDestroy(gr.g);
   }
   s->graphs.clear();
-  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2], s->ev_lat[3]})
+  for (auto& v : s->seg_graphs) {
+    for (auto& gr : v) {
+      if (gr.ex) (void)hipGraphExecDestroy(gr.ex);
+      if (gr.g) (void)hipGraphDestroy(gr.g);
+    }
+    v.clear();
+  }
+  for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
     if (st) (void)hipStreamDestroy(st);
@@ -1102,12 +1115,65 @@ bool small_key_fast_wsum(const zkfl_key* k) {
 //   lat0 : wait(ev B) B2 (from B's pairs) + its tail [ev B2]
 //   lat1 : wait(ev B) the tails of A and B1, k_assemble_t (T = s pi_A + r B1, pi_a) [ev T]
 // Same proof bytes as the one-stream schedule (k_assemble_t / _c form the same points).
+// ZKFL_GRAPH (default 1): graph replay of the proof chains (0: launch kernel by kernel)
+int graph_mode() {
+  static const int m = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 1;
+  return m;
+}
+
+// One segment of a schedule on one stream: captured once per (slot, segment, witness address)
+// as a one-stream graph and replayed, or enqueued directly (graphs off, or profiling).  body()
+// enqueues on `st` only; the segments' cross-stream order stays in events recorded between them.
+// true once d_w has been proved on this slot before (it is then worth a graph)
+bool seen_before(ProofSlot* s, const Fr* d_w) {
+  for (const Fr* x : s->seen)
+    if (x == d_w) return true;
+  if (s->seen.size() >= 32) s->seen.erase(s->seen.begin());
+  s->seen.push_back(d_w);
+  return false;
+}
+
+template <class Body>
+int run_segment(ProofSlot* s, int seg, const Fr* d_w, hipStream_t st, bool use_graph, Body body) {
+  if (!use_graph) return body();
+  std::vector<ProofSlot::Graph>& cache = s->seg_graphs[seg];
+  ProofSlot::Graph* gr = nullptr;
+  for (auto& x : cache)
+    if (x.w == d_w) gr = &x;
+  if (!gr) {
+    if (cache.size() >= 8) {
+      if (cache.front().ex) (void)hipGraphExecDestroy(cache.front().ex);
+      if (cache.front().g) (void)hipGraphDestroy(cache.front().g);
+      cache.erase(cache.begin());
+    }
+    ProofSlot::Graph ng;
+    ng.w = d_w;
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "begin capture");
+    const int rc = body();
+    const hipError_t ec = hipStreamEndCapture(st, &ng.g);
+    if (rc) {
+      if (ng.g) (void)hipGraphDestroy(ng.g);
+      return rc;
+    }
+    HIP_TRY(ec, "end capture");
+    const hipError_t ei = hipGraphInstantiate(&ng.ex, ng.g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(ng.g);
+      return hip_fail(ei, "graph instantiate");
+    }
+    cache.push_back(ng);
+    gr = &cache.back();
+  }
+  HIP_TRY(hipGraphLaunch(gr->ex, st), "graph launch");
+  return ZKFL_OK;
+}
+
 int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   for (int i = 0; i < 2; i++)
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < 3; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
   if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
   hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
@@ -1117,54 +1183,55 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
   MsmTail<Fq2Ops>* t2 = &s->g2t;
   G2P* o2 = s->resB2;
-  HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
-  HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
-  // A/B knob ZKFL_LOWLAT_BFIRST=1: B's sort first, so B2 (the G2 chain) starts before A and B1
-  static const bool bfirst = getenv("ZKFL_LOWLAT_BFIRST") && atoi(getenv("ZKFL_LOWLAT_BFIRST")) != 0;
-  hipEvent_t ev_b2start = bfirst ? s->ev_lat[3] : ev_b;
-  if (bfirst) {
-    HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
-    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
-    HIP_TRY(hipEventRecord(ev_b2start, st), "event");
-    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
-                                     "msm_accumulate_g1"), "msm B1");
-    HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
-    HIP_TRY(hipEventRecord(ev_b, st), "event");
-  } else {
+  // Each stream's stretch between two events is one segment, replayed from a graph: launched one
+  // by one, dependent kernels on an idle chip started 30-40 us apart (wave timeline), ~35 of
+  // them on the critical path.  (One graph for the whole multi-stream schedule ran ~7x slower.)
+  const bool seg_graphs = graph_mode() && !prof->on && seen_before(s, d_w);
+  int rc = run_segment(s, 0, d_w, st, seg_graphs, [&]() -> int {
+    HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
+    HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
     HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
     HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
     HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
                                      "msm_accumulate_g1"), "msm B1");
     HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
-    HIP_TRY(hipEventRecord(ev_b, st), "event");
-  }
+    return ZKFL_OK;
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(ev_b, st), "event");
   // lat0: B2 and its tail
-  HIP_TRY(hipStreamWaitEvent(sb, ev_b2start, 0), "wait");
-  HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
-                                   "msm_accumulate_g2"), "msm B2");
-  HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
+  HIP_TRY(hipStreamWaitEvent(sb, ev_b, 0), "wait");
+  rc = run_segment(s, 1, d_w, sb, seg_graphs, [&]() -> int {
+    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
+                                     "msm_accumulate_g2"), "msm B2");
+    HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
+    return ZKFL_OK;
+  });
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(ev_b2, sb), "event");
   // lat1: the tails of A and B1, then T = s pi_A + r B1 and pi_a
   HIP_TRY(hipStreamWaitEvent(sa, ev_b, 0), "wait");
-  {
+  rc = run_segment(s, 2, d_w, sa, seg_graphs, [&]() -> int {
     G1P* outs[2] = {s->res + 0, s->res + 1};
     HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
-  }
-  hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
-                     reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+    hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
+                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+    return ZKFL_OK;
+  });
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(ev_t, sa), "event");
   // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
-  {
-    const int rc = enqueue_abc_ntt(k, s, d_w, st, prof);
-    if (rc) return rc;
-  }
-  HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
-          "msm C+H");
-  HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
-  {
+  rc = run_segment(s, 3, d_w, st, seg_graphs, [&]() -> int {
+    const int r = enqueue_abc_ntt(k, s, d_w, st, prof);
+    if (r) return r;
+    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
+            "msm C+H");
+    HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
     G1P* out2 = s->res + 2;
     HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
-  }
+    return ZKFL_OK;
+  });
+  if (rc) return rc;
   HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
   HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
   const int pa = prof->begin("assemble", st);
@@ -1189,7 +1256,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   hipStream_t st = s->st_main;
   for (int i = 0; i < 2; i++)
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < 3; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
   if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
   if (!s->g1s_a.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, st), "A sort scratch");
@@ -1409,9 +1476,9 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
   glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
   glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
-  static const int use_graph = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 1;
+  const int use_graph = graph_mode();
   const bool graph = use_graph && !lowlat && plain == 0 && !prof->on && !prof->serialize && !s->st_g2 &&
-                     k->share_b && !ZK_KNOCKOUT;
+                     k->share_b && !ZK_KNOCKOUT && seen_before(s, d_w);
   const int rc = graph ? enqueue_proof_graph(ctx, k, s, d_w, plain) : enqueue_proof_body(ctx, k, s, d_w, plain, lowlat, false);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->ev_done, s->st_main), "event");
