@@ -81,9 +81,9 @@ def test_metric_key_by_path_equals_key_by_bytes(metric, gpu_ctx, tmp_path):
 
 
 def test_metric_latency_schedule_graph_replay(metric):
-    """A batch of one takes the latency schedule; its per-stream segments are captured as graphs on
-    a witness address's second proof and replayed after (enqueue_proof_lowlat / run_segment).
-    Direct, captured and replayed proofs of one resident witness equal the one-stream batch proof
+    """A batch of one takes the latency schedule (enqueue_proof_lowlat; with ZKFL_GRAPH=2 its
+    per-stream segments are captured as graphs on a witness address's second proof, run_segment).
+    Repeated latency-schedule proofs of one resident witness equal the one-stream batch proof
     of the same (witness, r, s) -- which test_metric_proof_and_parts_bit_exact_vs_c_oracle pins to
     the C oracle."""
     _, _, key, _, wts = metric

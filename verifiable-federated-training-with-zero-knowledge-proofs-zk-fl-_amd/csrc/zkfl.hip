@@ -1115,7 +1115,8 @@ bool small_key_fast_wsum(const zkfl_key* k) {
 //   lat0 : wait(ev B) B2 (from B's pairs) + its tail [ev B2]
 //   lat1 : wait(ev B) the tails of A and B1, k_assemble_t (T = s pi_A + r B1, pi_a) [ev T]
 // Same proof bytes as the one-stream schedule (k_assemble_t / _c form the same points).
-// ZKFL_GRAPH (default 1): graph replay of the proof chains (0: launch kernel by kernel)
+// ZKFL_GRAPH (default 1): graph replay of the one-stream proof chain (0: launch kernel by kernel;
+// 2: also the latency schedule's stream segments)
 int graph_mode() {
   static const int m = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 1;
   return m;
@@ -1183,10 +1184,11 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
   MsmTail<Fq2Ops>* t2 = &s->g2t;
   G2P* o2 = s->resB2;
-  // Each stream's stretch between two events is one segment, replayed from a graph: launched one
-  // by one, dependent kernels on an idle chip started 30-40 us apart (wave timeline), ~35 of
-  // them on the critical path.  (One graph for the whole multi-stream schedule ran ~7x slower.)
-  const bool seg_graphs = graph_mode() && !prof->on && seen_before(s, d_w);
+  // ZKFL_GRAPH=2: each stream's stretch between two events is one segment, replayed from its own
+  // one-stream graph.  Measured no gain (median 4.128 vs 4.125 ms over 3 same-box alternations,
+  // profiles/r04_ab_lowlat_seg_graphs.log): the gaps on the critical path are not launch cost, so
+  // it stays an A/B knob.  (One graph for the whole multi-stream schedule ran ~7x slower.)
+  const bool seg_graphs = graph_mode() >= 2 && !prof->on && seen_before(s, d_w);
   int rc = run_segment(s, 0, d_w, st, seg_graphs, [&]() -> int {
     HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
     HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
