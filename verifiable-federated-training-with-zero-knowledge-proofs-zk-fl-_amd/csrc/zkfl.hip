@@ -788,6 +788,10 @@ struct ProofSlot {
     hipGraphExec_t ex = nullptr;
   };
   std::vector<Graph> graphs;
+  // the graph's witness: each graph-replayed proof first copies its witness here (nVars x 32 B,
+  // a few us of HBM time), so one graph per slot serves every witness buffer
+  Fr* w_stage = nullptr;
+  uint32_t direct_proofs = 0;     // proofs this slot ran kernel by kernel (the first one: no capture)
   // the latency schedule's per-stream segments, each captured as its own one-stream graph
   // (enqueue_proof_lowlat): index = segment, entries per witness address
   std::vector<Graph> seg_graphs[4];
@@ -863,7 +867,8 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof, s->d_parts};  // extra lives in h
+  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof, s->d_parts,
+                  s->w_stage};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -888,6 +893,23 @@ void slot_release(ProofSlot* s) {
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
     if (st) (void)hipStreamDestroy(st);
   delete s;
+}
+
+int graph_mode();
+
+// Release a slot's latency-schedule streams and events (made again on its next batch of one).
+void slot_drop_lowlat(ProofSlot* s) {
+  for (hipStream_t& st : s->st_lat)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+      st = nullptr;
+    }
+  for (hipEvent_t& e : s->ev_lat)
+    if (e) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
 }
 
 hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
@@ -917,7 +939,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
-  (void)nV;
+  if (graph_mode()) ZK_CHECK(hipMalloc(&s->w_stage, nV * 32));
   ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
   s->extra = s->h + n;
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
@@ -1433,9 +1455,9 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
 // Graph replay of the one-stream chain (the default; ZKFL_GRAPH=0 launches kernel by kernel;
 // config 5 +3.5%, 1894 vs 1831 proofs/s, M +0.6% inside the spread, 3 same-box alternations,
 // profiles/r04_ab_c5_small_keys.log, r04_ab_m_graph_target.log): a slot captures its proof's ~40 launches
-// once per witness address (a batch cycles its slots over a few witness buffers) and then
-// launches the graph -- one host call per proof instead of one per kernel.  Kernel arguments are
-// the slot's own buffers, the key's and the witness address, all fixed per cache entry; r and s
+// once per witness address (enqueue_proof passes the slot's witness stage, so once per slot) and
+// then launches the graph -- one host call per proof instead of one per kernel.  Kernel arguments
+// are the slot's own buffers, the key's and the witness address, all fixed per cache entry; r and s
 // reach the device through the captured copy from the slot's pinned buffer.
 int enqueue_proof_graph(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, int plain) {
   hipStream_t st = s->st_main;
@@ -1478,10 +1500,18 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   GlvScalar* ks = reinterpret_cast<GlvScalar*>(s->pinned + 320);
   glv_split(rs_host + 8, ks[0], ks[1]);  // s -> s1, s2 (for pi_A, phi(pi_A))
   glv_split(rs_host, ks[2], ks[3]);      // r -> r1, r2 (for B1, phi(B1))
-  const int use_graph = graph_mode();
-  const bool graph = use_graph && !lowlat && plain == 0 && !prof->on && !prof->serialize && !s->st_g2 &&
-                     k->share_b && !ZK_KNOCKOUT && seen_before(s, d_w);
-  const int rc = graph ? enqueue_proof_graph(ctx, k, s, d_w, plain) : enqueue_proof_body(ctx, k, s, d_w, plain, lowlat, false);
+  // graph replay from a slot's second proof on (a one-off proof pays no capture); the witness is
+  // staged into the slot's own buffer so the captured kernel arguments hold for every witness
+  const bool graph = graph_mode() && s->w_stage && !lowlat && plain == 0 && !prof->on && !prof->serialize &&
+                     !s->st_g2 && k->share_b && !ZK_KNOCKOUT && s->direct_proofs > 0;
+  int rc;
+  if (graph) {
+    HIP_TRY(hipMemcpyAsync(s->w_stage, d_w, (size_t)k->nVars * 32, hipMemcpyDeviceToDevice, s->st_main), "witness stage");
+    rc = enqueue_proof_graph(ctx, k, s, s->w_stage, plain);
+  } else {
+    s->direct_proofs++;
+    rc = enqueue_proof_body(ctx, k, s, d_w, plain, lowlat, false);
+  }
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->ev_done, s->st_main), "event");
   HIP_TRY(hipGetLastError(), "launch");
@@ -2167,6 +2197,11 @@ int zkfl_key_set_slots(zkfl_key* key, int slots) {
     slot_release(key->slots.back());
     key->slots.pop_back();
   }
+  // a slot's latency-schedule streams (made by a batch of one) hold HW queues: with many slots
+  // they would push the slots' own streams past the ~24 HW queues and make slots share them
+  // (a latency pass on a one-slot key before a 20-slot run: 395 vs 415 proofs/s)
+  if (slots > 1)
+    for (ProofSlot* s : key->slots) slot_drop_lowlat(s);
   key->max_slots = slots;
   return ZKFL_OK;
 }
