@@ -745,8 +745,10 @@ def main():
     ap.add_argument("--slots", type=int, default=20, help="proofs in flight per GPU (one HIP stream each)")
     ap.add_argument("--clients", type=int, default=4, help="distinct synthetic client witnesses, cycled")
     ap.add_argument("--e2e-steps", type=int, default=16, help="steps of the input.json -> proof leg (0: skip)")
-    ap.add_argument("--c5-rounds", type=int, default=8, help="federated rounds of the config-5 leg (0: skip)")
-    ap.add_argument("--c5-weak-rounds", type=int, default=4,
+    # 16 rounds: at 8 (~75 ms timed) the first round's ramp (slots filling, the first witness group)
+    # weighed 1/8 -- bench 1751-1828 against 1900-1915 from tools/c5_probe.py's 16 rounds, same box
+    ap.add_argument("--c5-rounds", type=int, default=16, help="federated rounds of the config-5 leg (0: skip)")
+    ap.add_argument("--c5-weak-rounds", type=int, default=16,
                     help="config-5 weak-scaling leg: federated rounds of 8 own clients per GPU (0: skip)")
     ap.add_argument("--merkle-log2n", type=int, default=20, help="dataset-commitment leg: 2^k samples (0: skip)")
     ap.add_argument("--extra-circuit", default="M19", help="second training-circuit size leg ('' or none: skip)")
