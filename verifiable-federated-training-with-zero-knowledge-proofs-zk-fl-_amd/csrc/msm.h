@@ -964,11 +964,24 @@ uint32_t msm_resident_chunks() {
 #endif
 }
 
+// Minimum entries per accumulation lane for an MSM of `cap` bases.  Small MSMs (<= 2^16 bases:
+// config 5's keys) are latency-bound chains, so they take short chunks: a shorter serial walk
+// per lane for a few more stitching items (config 5 1970 vs 1893 proofs/s at 8 vs 16, same box,
+// DESIGN.md §12).  ZKFL_MSM_L0 / ZKFL_MSM_L0_SMALL override (A/B knobs).
+template <class F>
+uint32_t msm_tail_l0(size_t cap) {
+  const bool small = cap <= ((size_t)1 << 16);
+  const char* e = getenv(small ? "ZKFL_MSM_L0_SMALL" : "ZKFL_MSM_L0");
+  const uint32_t l = e ? (uint32_t)atoi(e) : (small ? MSM_SMALL_L : (uint32_t)MsmChunk<F>::L);
+  return l < 1 ? 1u : l > 255 ? 255u : l;
+}
+
 template <class F>
 hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
   const size_t m = cap * MSM_W;
-  t.target = msm_resident_chunks<F>();
-  t.max_chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  t.target = std::min<uint32_t>(msm_resident_chunks<F>(), 0xFFFFFFu);
+  t.l0 = msm_tail_l0<F>(cap);
+  t.max_chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) t.max_chunks = std::min<size_t>(t.max_chunks, t.target);  // msm_chunk_len bounds the lanes
   t.item_cap[0] = 2 * t.max_chunks;
   t.item_cap[1] = 2 * ((t.item_cap[0] + MSM_SG - 1) / MSM_SG);
@@ -1007,7 +1020,7 @@ MsmTailArgs<F> msm_tail_args(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n) 
     ta.nnz[i] = t[i]->nnz;
     ta.out[i] = outs ? outs[i] : nullptr;
     ta.live[i] = t[i]->live;
-    ta.target[i] = t[i]->target;
+    ta.target[i] = msm_target_arg(*t[i]);
   }
   return ta;
 }
@@ -1069,7 +1082,7 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
                                  hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
   if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
-  size_t chunks = (m + MsmChunk<F>::L - 1) / MsmChunk<F>::L;
+  size_t chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) chunks = std::min<size_t>(chunks, t.target);  // lanes of msm_chunk_len(nnz, target)
   if (chunks > t.max_chunks) return hipErrorInvalidValue;
   const int pidx = prof ? prof->begin(tag, st) : -1;
@@ -1089,7 +1102,7 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
   static const size_t pad_lds = getenv("ZKFL_ACC_PAD_LDS") ? strtoul(getenv("ZKFL_ACC_PAD_LDS"), nullptr, 10) : 0;
   if (!done && !((ZK_KNOCKOUT & 64) && LN == 1))
     hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), pad_lds, st, keys, vals,
-                       b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, t.target, t.live);
+                       b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, msm_target_arg(t), t.live);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
   return hipGetLastError();
 }

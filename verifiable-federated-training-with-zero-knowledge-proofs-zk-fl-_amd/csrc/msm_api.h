@@ -63,6 +63,10 @@ constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every buck
 #ifndef MSM_G2_L
 #define MSM_G2_L 16
 #endif
+// minimum chunk length of small MSMs (<= 2^16 bases), both curves (msm_tail_l0)
+#ifndef MSM_SMALL_L
+#define MSM_SMALL_L 8
+#endif
 // Chunk length per curve (storage field type S)
 template <class S>
 struct MsmChunk {
@@ -77,15 +81,17 @@ struct MsmChunk<Fq2Ops> {
 #ifndef MSM_ADAPTIVE_L
 #define MSM_ADAPTIVE_L 1
 #endif
-// Entries per accumulation lane for an MSM with nnz sorted non-zero digits: the minimum
-// MsmChunk<S>::L, or the fewest that keep the lanes within `target` = the lanes the device holds
-// at once for the accumulation kernel (0: always the minimum).  A longer chunk leaves fewer chunk
+// Entries per accumulation lane for an MSM with nnz sorted non-zero digits: the minimum L0, or the
+// fewest that keep the lanes within `target` = the lanes the device holds at once for the
+// accumulation kernel (0: always the minimum).  The kernel argument carries both: bits 0-23 the
+// lanes, bits 24-31 the tail's minimum L0 (0: MsmChunk<S>::L) -- msm_target_arg.  A longer chunk leaves fewer chunk
 // edges inside a bucket, and every such edge costs one full point addition in the stitching;
 // the launch stays one full round of lanes, so the accumulation's own duration does not change.
 // The accumulation and the stitching levels derive the same value from nnz on the device.
 template <class S>
 __host__ __device__ inline uint32_t msm_chunk_len(uint32_t nnz, uint32_t target) {
-  constexpr uint32_t L0 = MsmChunk<S>::L;
+  const uint32_t L0 = (target >> 24) ? (target >> 24) : (uint32_t)MsmChunk<S>::L;
+  target &= 0xFFFFFFu;
   if (target == 0) return L0;
   const uint32_t l = (uint32_t)(((uint64_t)nnz + target - 1) / target);
   return l > L0 ? l : L0;
@@ -152,8 +158,15 @@ struct MsmTail {
   // something to stitch; a level whose predecessor emitted none returns at once (device)
   uint32_t* live = nullptr;
   uint32_t target = 0;          // accumulation lanes resident at once (msm_chunk_len; 0: fixed L)
+  uint32_t l0 = 0;              // minimum entries per accumulation lane (msm_tail_l0)
   const MsmAffScratch* aff = nullptr;  // G1: batch-affine scratch to accumulate with (not owned)
 };
+
+// msm_chunk_len's argument: resident lanes (bits 0-23) | minimum chunk length (bits 24-31)
+template <class F>
+inline uint32_t msm_target_arg(const MsmTail<F>& t) {
+  return (t.l0 << 24) | (t.target & 0xFFFFFFu);
+}
 
 constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs of a proof)
 
