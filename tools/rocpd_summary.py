@@ -105,10 +105,10 @@ def _short(name):
 
 
 def breakdown(db, out, proofs=6):
-    """k_set_extra opens every proof (zkfl.hip enqueue_proof); the roofline pass is the last
+    """k_proof_start opens every proof (zkfl.hip enqueue_proof_body); the roofline pass is the last
     `proofs` proofs of the run, serialized on one stream."""
     c = sqlite3.connect(db)
-    starts = [r[0] for r in c.execute("select start from kernels where name like '%k_set_extra%' order by start")]
+    starts = [r[0] for r in c.execute("select start from kernels where name like '%k_proof_start%' or name like '%k_set_extra%' order by start")]
     t0 = starts[-proofs]
     rows = c.execute("select name, count(*), sum(end-start) from kernels where start >= ? group by name", (t0,)).fetchall()
     span = c.execute("select max(end) - ? from kernels where start >= ?", (t0, t0)).fetchone()[0]

@@ -40,7 +40,7 @@ SYMBOL = {"acc": "k_msm_accumulate", "stitch": "k_msm_stitch", "wsum0": "k_msm_w
           "sort_count": "k_msm_bin_count", "sort_scan": "k_msm_bin_scan", "sort_scatter": "k_msm_bin_scatter",
           "sort_bins": "k_msm_bin_sort", "tail_reset": "k_msm_tail_reset", "ntt_cols_inv": "k_ntt_colsILb1",
           "ntt_lds": "k_ntt_lds_pair", "ntt_cols_fwd": "k_ntt_colsILb0", "abc": "k_abc_chunks", "abc_rows": "k_abc_rows",
-          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_set_extra", "witness": "k_wit_level"}
+          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_proof_start", "witness": "k_wit_level"}
 
 
 def kind_name(k):
@@ -51,7 +51,7 @@ def kind_name(k):
 def vgpr_share(lib_path):
     """kind name -> SIMD share of one wave (VGPRs rounded to the allocation granule of 8, / 512)."""
     import isa_check
-    res = isa_check.resources(lib_path, r"k_msm_|k_ntt_|k_abc_|k_join|k_assemble|k_set_extra")
+    res = isa_check.resources(lib_path, r"k_msm_|k_ntt_|k_abc_|k_join|k_assemble|k_proof_start")
     out = {}
     for name, pat in SYMBOL.items():
         import re

@@ -233,18 +233,42 @@ __global__ void k_join(const Fr* __restrict__ abc, size_t n, Fr* __restrict__ h)
 
 // Blinding scalar slots referenced by the compacted bases' index maps (std form):
 // extra = [1, r, s, -r*s].  plain -> all zero (parity hook: pure MSMs).
-__global__ void k_set_extra(const Fr* __restrict__ rs, Fr* __restrict__ extra, int plain) {
+// The tails a proof chain empties at its start (k_proof_start): up to 4 G1 and 1 G2, each as
+// its bucket array (16-B vectors), nnz counter and liveness flags.
+struct ProofStart {
+  uint4* buckets[5];
+  uint32_t nvec[5];
+  uint32_t* nnz[5];
+  uint32_t* live[5];
+  int n;
+};
+
+// A proof chain's first kernel, one launch for what were up to four: the augmentation scalars
+// (1, r, s, -rs) of the merged MSMs, res[3] = infinity (the merged C + H leaves the H slot
+// empty), and the proof's MSM tails emptied (buckets, nnz, liveness: blockIdx.y = tail).
+__global__ void __launch_bounds__(256) k_proof_start(const Fr* __restrict__ rs, Fr* __restrict__ extra, int plain,
+                                                     uint32_t* __restrict__ res3, const ProofStart ps) {
   ZK_WT(WT_SET_EXTRA);
   ZK_LIGHT();
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Fr one = fp_zero<FrP>();
-  one.v[0] = plain ? 0u : 1u;
-  Fr r = plain ? fp_zero<FrP>() : rs[0];
-  Fr s = plain ? fp_zero<FrP>() : rs[1];
-  extra[0] = one;
-  extra[1] = r;
-  extra[2] = s;
-  extra[3] = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
+  const int y = blockIdx.y;
+  if (y == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    Fr one = fp_zero<FrP>();
+    one.v[0] = plain ? 0u : 1u;
+    Fr r = plain ? fp_zero<FrP>() : rs[0];
+    Fr s = plain ? fp_zero<FrP>() : rs[1];
+    extra[0] = one;
+    extra[1] = r;
+    extra[2] = s;
+    extra[3] = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
+  }
+  if (y == 0 && blockIdx.x == 1 && res3 && threadIdx.x < sizeof(G1P) / 4) res3[threadIdx.x] = 0u;  // ZZ = 0
+  if (y >= ps.n) return;
+  uint4* b = ps.buckets[y];
+  const size_t nv = ps.nvec[y];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
+    b[i] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ps.nnz[y] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ps.live[y][threadIdx.x] = 0;
 }
 
 template <class F>
@@ -792,6 +816,9 @@ struct ProofSlot {
   // a few us of HBM time), so one graph per slot serves every witness buffer
   Fr* w_stage = nullptr;
   uint32_t direct_proofs = 0;     // proofs this slot ran kernel by kernel (the first one: no capture)
+  // B2 shares B1's digit sort, so its tail counts with B1's nnz (g2t.nnz == g1t[1].nnz, owned
+  // by g1t[1]): no copy between them
+  bool nnz_alias = false;
   // the latency schedule's per-stream segments, each captured as its own one-stream graph
   // (enqueue_proof_lowlat): index = segment, entries per witness address
   std::vector<Graph> seg_graphs[4];
@@ -860,6 +887,7 @@ void slot_release(ProofSlot* s) {
   if (!s) return;
   for (hipStream_t st : {s->st_main, s->st_g2})
     if (st) (void)hipStreamSynchronize(st);
+  if (s->nnz_alias) s->g2t.nnz = nullptr;
   msm_scratch_free_g1(s->g1s);
 #if ZK_KNOCKOUT & 2
   for (MsmScratch<FqOps>& x : s->g1s_ko) msm_scratch_free_g1(x);
@@ -939,6 +967,11 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
+  if (k->share_b && !s->st_g2 && !ZK_KNOCKOUT) {
+    ZK_CHECK(hipFree(s->g2t.nnz));
+    s->g2t.nnz = s->g1t[1].nnz;
+    s->nnz_alias = true;
+  }
   if (graph_mode()) ZK_CHECK(hipMalloc(&s->w_stage, nV * 32));
   ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
   s->extra = s->h + n;
@@ -1211,14 +1244,13 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   // profiles/r04_ab_lowlat_seg_graphs.log): the gaps on the critical path are not launch cost, so
   // it stays an A/B knob.  (One graph for the whole multi-stream schedule ran ~7x slower.)
   const bool seg_graphs = graph_mode() >= 2 && !prof->on && seen_before(s, d_w);
-  int rc = run_segment(s, 0, d_w, st, seg_graphs, [&]() -> int {
-    HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
-    HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
+  int rc = run_segment(s, 0, d_w, st, seg_graphs, [&]() -> int {  // (tails emptied by k_proof_start)
     HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
     HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
     HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
                                      "msm_accumulate_g1"), "msm B1");
-    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    if (!s->nnz_alias)
+      HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
     return ZKFL_OK;
   });
   if (rc) return rc;
@@ -1250,7 +1282,6 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
     if (r) return r;
     HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
-    HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
     G1P* out2 = s->res + 2;
     HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
     return ZKFL_OK;
@@ -1293,13 +1324,12 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
   MsmTail<Fq2Ops>* t2 = &s->g2t;
   G2P* o2 = s->resB2;
-  HIP_TRY(msm_tails_reset_g1(tails, 3, st), "msm reset");
-  HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
-  HIP_TRY(hipEventRecord(ev, st), "event");
+  HIP_TRY(hipEventRecord(ev, st), "event");  // (tails emptied by k_proof_start)
   // lat0: B's sort, then B2 and its tail
   HIP_TRY(hipStreamWaitEvent(sb, ev, 0), "wait");
   HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, sb), "msm B sort");
-  HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, sb), "nnz");
+  if (!s->nnz_alias)
+    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, sb), "nnz");
   HIP_TRY(hipEventRecord(ev, sb), "event");
   HIP_TRY(hipStreamWaitEvent(sa, ev, 0), "wait");
   HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
@@ -1324,7 +1354,6 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   }
   HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
           "msm C+H");
-  HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
   {
     G1P* out2 = s->res + 2;
     HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
@@ -1349,8 +1378,27 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   int pp = prof->begin("prove", st);
   HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
           "upload r,s");
-  hipLaunchKernelGGL(k_set_extra, dim3(1), dim3(1), 0, st, s->d_rs, s->extra, plain == 1);
-  if (lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT) {
+  const bool lowlat_path =
+      lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT;
+  {
+    // the tails this chain accumulates into: G1 A, B1, C (+ H), [H]; G2 B2 when it shares B1's sort
+    // on this stream (a separate G2 stream's msm_run empties its own)
+    const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1) ? 3 : 4;
+    const bool g2 = lowlat_path || (k->share_b && !s->st_g2 && !(ZK_KNOCKOUT & 32));
+    ProofStart ps = {};
+    auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
+      ps.buckets[ps.n] = static_cast<uint4*>(buckets);
+      ps.nvec[ps.n] = (uint32_t)(bytes / sizeof(uint4));
+      ps.nnz[ps.n] = nnz;
+      ps.live[ps.n] = live;
+      ps.n++;
+    };
+    for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, MSM_NB * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
+    if (g2) add(s->g2t.buckets, MSM_NB * sizeof(G2P), s->g2t.nnz, s->g2t.live);
+    uint32_t* res3 = MSM_MERGE_CH && plain != 1 ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
+    hipLaunchKernelGGL(k_proof_start, dim3(128, ps.n), dim3(256), 0, st, s->d_rs, s->extra, plain == 1, res3, ps);
+  }
+  if (lowlat_path) {
     const int rc = lowlat == 2 ? enqueue_proof_lowlat2(ctx, k, s, d_w) : enqueue_proof_lowlat(ctx, k, s, d_w);
     if (rc) return rc;
     prof->end(pp, st, 1.0);
@@ -1387,7 +1435,6 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   auto abc_ntt = [&]() { return enqueue_abc_ntt(k, s, d_w, st, prof); };
   // main: the witness-scalar G1 MSMs, then ABC / NTT / H, then all four G1 tails in one batch
-  HIP_TRY(msm_tails_reset_g1(tails, ntails, st), "msm reset");
 #if ZK_KNOCKOUT & 2
   MsmScratch<FqOps>&sA = s->g1s_ko[0], &sB = s->g1s_ko[1], &sCH = s->g1s_ko[2];
 #else
@@ -1401,11 +1448,11 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   if (share) {
     MsmTail<Fq2Ops>* t2 = &s->g2t;
     G2P* o2 = s->resB2;
-    HIP_TRY(msm_tails_reset_g2(&t2, 1, st), "msm reset");
     HIP_TRY(msm_sort_g1(k->bB1, sB, s->g1t[1].nnz, W, E, st), "msm B1 sort");
     HIP_TRY(msm_accumulate_sorted_g1(k->bB1, sB.keys_out, sB.vals_out, s->g1t[1], st, prof,
                                      "msm_accumulate_g1"), "msm B1");
-    HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    if (!s->nnz_alias)
+      HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
     HIP_TRY(msm_accumulate_sorted_g2(k->bB2, sB.keys_out, sB.vals_out, s->g2t, st, prof,
                                      "msm_accumulate_g2"), "msm B2");
     HIP_TRY(msm_tails_g2(&t2, &o2, 1, st, small_key_fast_wsum(k)), "msm B2 tail");
@@ -1424,7 +1471,6 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   if (merge) {
     HIP_TRY(msm_accumulate_g1(k->bCH, sCH, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
-    HIP_TRY(hipMemsetAsync(s->res + 3, 0, sizeof(G1P), st), "res H");  // ZZ = 0: infinity
   } else if (split_ch) {
     HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[3], Z, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm H");
