@@ -246,12 +246,18 @@ struct ProofStart {
 // A proof chain's first kernel, one launch for what were up to four: the augmentation scalars
 // (1, r, s, -rs) of the merged MSMs, res[3] = infinity (the merged C + H leaves the H slot
 // empty), and the proof's MSM tails emptied (buckets, nnz, liveness: blockIdx.y = tail).
-__global__ void __launch_bounds__(256) k_proof_start(const Fr* __restrict__ rs, Fr* __restrict__ extra, int plain,
-                                                     uint32_t* __restrict__ res3, const ProofStart ps) {
+// rs_host: the slot's pinned r | s | GLV halves (host memory, coherent), copied to d_rs for the
+// assembly; the augmentation scalars are computed from the host copy directly.
+constexpr int RS_WORDS = (64 + 4 * (int)sizeof(GlvScalar)) / 4;
+__global__ void __launch_bounds__(256) k_proof_start(const uint32_t* __restrict__ rs_host, uint32_t* __restrict__ d_rs,
+                                                     Fr* __restrict__ extra, int plain, uint32_t* __restrict__ res3,
+                                                     const ProofStart ps) {
   ZK_WT(WT_SET_EXTRA);
   ZK_LIGHT();
   const int y = blockIdx.y;
+  if (y == 0 && blockIdx.x == 2 && threadIdx.x < RS_WORDS) d_rs[threadIdx.x] = rs_host[threadIdx.x];
   if (y == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    const Fr* rs = reinterpret_cast<const Fr*>(rs_host);
     Fr one = fp_zero<FrP>();
     one.v[0] = plain ? 0u : 1u;
     Fr r = plain ? fp_zero<FrP>() : rs[0];
@@ -795,7 +801,6 @@ struct ProofSlot {
   G1P* res = nullptr;     // [5]: A', B1', C', H, T
   G2P* resB2 = nullptr;   // [1]
   Fr* d_rs = nullptr;     // r, s (64 B) | GLV halves s1, s2, r1, r2 (4 x 32 B)
-  uint32_t* d_proof = nullptr;  // [64]
   uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
   uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (768 at 512)
   // the low-latency schedule (enqueue_proof_lowlat, one proof alone): two side streams, their
@@ -883,6 +888,9 @@ struct zkfl_wprog {
 
 namespace {
 
+// the proof's 256 bytes go straight into the slot's pinned buffer (k_assemble*)
+inline uint32_t* proof_out(ProofSlot* s) { return reinterpret_cast<uint32_t*>(s->pinned); }
+
 void slot_release(ProofSlot* s) {
   if (!s) return;
   for (hipStream_t st : {s->st_main, s->st_g2})
@@ -895,7 +903,7 @@ void slot_release(ProofSlot* s) {
   for (auto& t : s->g1t) msm_tail_free_g1(t);
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
-  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_proof, s->d_parts,
+  void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_parts,
                   s->w_stage};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -982,9 +990,10 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ZK_CHECK(hipMalloc(&s->res, 5 * sizeof(G1P)));
   ZK_CHECK(hipMalloc(&s->resB2, sizeof(G2P)));
   ZK_CHECK(hipMalloc(&s->d_rs, 2 * 32 + 4 * sizeof(GlvScalar)));
-  ZK_CHECK(hipMalloc(&s->d_proof, 256));
   ZK_CHECK(hipMalloc(&s->d_parts, PART_WORDS * 4));
-  ZK_CHECK(hipHostMalloc(&s->pinned, 2048));
+  // coherent (fine-grained): the proof chain reads r, s and the GLV halves from it and writes the
+  // proof into it directly (k_proof_start, k_assemble*), so no copy launches open or close a proof
+  ZK_CHECK(hipHostMalloc(&s->pinned, 2048, hipHostMallocCoherent));
   return hipStreamSynchronize(st);
 }
 
@@ -1271,7 +1280,7 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
     G1P* outs[2] = {s->res + 0, s->res + 1};
     HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
     hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
-                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
     return ZKFL_OK;
   });
   if (rc) return rc;
@@ -1290,9 +1299,8 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
   HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
   const int pa = prof->begin("assemble", st);
-  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, s->d_proof);
+  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, proof_out(s));
   prof->end(pa, st, 1.0);
-  HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   return ZKFL_OK;
 }
 
@@ -1345,7 +1353,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
     HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
   }
   hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
-                     reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+                     reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
   HIP_TRY(hipEventRecord(ev_t, sa), "event");
   // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
   {
@@ -1361,9 +1369,8 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
   HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
   HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
   const int pa = prof->begin("assemble", st);
-  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, s->d_proof);
+  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, proof_out(s));
   prof->end(pa, st, 1.0);
-  HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   return ZKFL_OK;
 }
 
@@ -1376,8 +1383,6 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   hipStream_t st_g2 = (prof->serialize || !s->st_g2) ? st : s->st_g2;
   const size_t n = k->n;
   int pp = prof->begin("prove", st);
-  HIP_TRY(hipMemcpyAsync(s->d_rs, s->pinned + 256, 64 + 4 * sizeof(GlvScalar), hipMemcpyHostToDevice, st),
-          "upload r,s");
   const bool lowlat_path =
       lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT;
   {
@@ -1396,7 +1401,8 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, MSM_NB * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
     if (g2) add(s->g2t.buckets, MSM_NB * sizeof(G2P), s->g2t.nnz, s->g2t.live);
     uint32_t* res3 = MSM_MERGE_CH && plain != 1 ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
-    hipLaunchKernelGGL(k_proof_start, dim3(128, ps.n), dim3(256), 0, st, s->d_rs, s->extra, plain == 1, res3, ps);
+    hipLaunchKernelGGL(k_proof_start, dim3(128, ps.n), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(s->pinned + 256),
+                       reinterpret_cast<uint32_t*>(s->d_rs), s->extra, plain == 1, res3, ps);
   }
   if (lowlat_path) {
     const int rc = lowlat == 2 ? enqueue_proof_lowlat2(ctx, k, s, d_w) : enqueue_proof_lowlat(ctx, k, s, d_w);
@@ -1490,9 +1496,8 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
     hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
-                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), s->d_proof);
+                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
     prof->end(pa, st, 1.0);
-    HIP_TRY(hipMemcpyAsync(s->pinned, s->d_proof, 256, hipMemcpyDeviceToHost, st), "download proof");
   }
   prof->end(pp, st, 1.0);
   return ZKFL_OK;
