@@ -241,6 +241,11 @@ struct ProofStart {
   uint32_t* nnz[5];
   uint32_t* live[5];
   int n;
+  // graph replay: the proof's witness, copied into the slot's stage (w_dst, w_nvec 16-B vectors)
+  // from the device address the host left in the pinned buffer (w_src_host); w_dst null: none
+  const uint64_t* w_src_host;
+  uint4* w_dst;
+  uint32_t w_nvec;
 };
 
 // A proof chain's first kernel, one launch for what were up to four: the augmentation scalars
@@ -255,6 +260,14 @@ __global__ void __launch_bounds__(256) k_proof_start(const uint32_t* __restrict_
   ZK_WT(WT_SET_EXTRA);
   ZK_LIGHT();
   const int y = blockIdx.y;
+  if (ps.w_dst) {  // uniform per launch
+    __shared__ const uint4* src;
+    if (threadIdx.x == 0) src = reinterpret_cast<const uint4*>(*ps.w_src_host);
+    __syncthreads();
+    const size_t nb = (size_t)gridDim.x * gridDim.y * blockDim.x;
+    for (size_t i = ((size_t)y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < ps.w_nvec; i += nb)
+      ps.w_dst[i] = src[i];
+  }
   if (y == 0 && blockIdx.x == 2 && threadIdx.x < RS_WORDS) d_rs[threadIdx.x] = rs_host[threadIdx.x];
   if (y == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
     const Fr* rs = reinterpret_cast<const Fr*>(rs_host);
@@ -802,7 +815,8 @@ struct ProofSlot {
   G2P* resB2 = nullptr;   // [1]
   Fr* d_rs = nullptr;     // r, s (64 B) | GLV halves s1, s2, r1, r2 (4 x 32 B)
   uint32_t* d_parts = nullptr;  // [96]: this rank's part of a split proof (A'|B1'|B2'|C'|H, std affine)
-  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | pad | part (768 at 512)
+  uint8_t* pinned = nullptr;    // proof (256) | r, s (64) | GLV halves (128) | witness address (8, at
+                                // W_PTR_OFF) | pad | part (768 at 512)
   // the low-latency schedule (enqueue_proof_lowlat, one proof alone): two side streams, their
   // events (B sorted and B1 accumulated | B2 final | T = s pi_A + r B1 final) and B's own sort
   // scratch, so C + H can sort on the main stream while B2 still reads B's pairs; made on first use
@@ -887,6 +901,8 @@ struct zkfl_wprog {
 };
 
 namespace {
+
+constexpr size_t W_PTR_OFF = 448;  // pinned: the graph-replayed proof's witness address
 
 // the proof's 256 bytes go straight into the slot's pinned buffer (k_assemble*)
 inline uint32_t* proof_out(ProofSlot* s) { return reinterpret_cast<uint32_t*>(s->pinned); }
@@ -1401,6 +1417,11 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, MSM_NB * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
     if (g2) add(s->g2t.buckets, MSM_NB * sizeof(G2P), s->g2t.nnz, s->g2t.live);
     uint32_t* res3 = MSM_MERGE_CH && plain != 1 ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
+    if (s->w_stage && d_w == s->w_stage) {  // graph replay (enqueue_proof): stage the witness here
+      ps.w_src_host = reinterpret_cast<const uint64_t*>(s->pinned + W_PTR_OFF);
+      ps.w_dst = reinterpret_cast<uint4*>(s->w_stage);
+      ps.w_nvec = (uint32_t)((size_t)k->nVars * 32 / sizeof(uint4));
+    }
     hipLaunchKernelGGL(k_proof_start, dim3(128, ps.n), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(s->pinned + 256),
                        reinterpret_cast<uint32_t*>(s->d_rs), s->extra, plain == 1, res3, ps);
   }
@@ -1557,7 +1578,9 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
                      !s->st_g2 && k->share_b && !ZK_KNOCKOUT && s->direct_proofs > 0;
   int rc;
   if (graph) {
-    HIP_TRY(hipMemcpyAsync(s->w_stage, d_w, (size_t)k->nVars * 32, hipMemcpyDeviceToDevice, s->st_main), "witness stage");
+    // k_proof_start copies the witness into the stage from the address left here
+    const uint64_t src = reinterpret_cast<uint64_t>(d_w);
+    memcpy(s->pinned + W_PTR_OFF, &src, sizeof(src));
     rc = enqueue_proof_graph(ctx, k, s, s->w_stage, plain);
   } else {
     s->direct_proofs++;
