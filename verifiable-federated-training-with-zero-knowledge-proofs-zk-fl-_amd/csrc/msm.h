@@ -718,24 +718,16 @@ __global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta)
   if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ta.live[y][threadIdx.x] = 0;
 }
 
-template <class F, int MINW, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
-    const MsmTailArgs<S> ta, int level, int src) {
-  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
-  ZK_LIGHT();
+// One stitching level for lane g of MSM y (N = the level's item count).
+template <class F, class S = typename MsmIO<F>::S>
+ZK_DEV void msm_stitch_lane(const MsmTailArgs<S>& ta, int y, int level, int src, uint32_t g, uint32_t N) {
   using IO = MsmIO<F>;
-  const int y = blockIdx.y;
   const uint32_t* __restrict__ in_key = ta.key[y][src];
   const XYZZ<S>* __restrict__ in_val = ta.val[y][src];
   uint32_t* __restrict__ out_key = ta.key[y][src ^ 1];
   XYZZ<S>* __restrict__ out_val = ta.val[y][src ^ 1];
   XYZZ<S>* __restrict__ buckets = ta.buckets[y];
-  // the level before emitted no real open run: every bucket is final already
-  if (ta.live[y][level - 1] == 0u) return;
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
-  const uint32_t N = msm_items_at<S>(*ta.nnz[y], level, ta.target[y]);
   const uint32_t q0 = g * MSM_SG;
-  if (q0 >= N) return;
   const uint32_t q1 = q0 + MSM_SG < N ? q0 + MSM_SG : N;
   constexpr uint32_t KM = ~MSM_ITEM_DUMMY;
   const uint32_t kprev = q0 > 0 ? (in_key[q0 - 1] & KM) : 0xFFFFFFFFu;
@@ -766,7 +758,43 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   }
   if (!slot0) okey[0] = (in_key[q0] & KM) | MSM_ITEM_DUMMY;
   if (!slot1) okey[1] = (in_key[q1 - 1] & KM) | MSM_ITEM_DUMMY;
-  if (level < MSM_LIVE_LEVELS) msm_mark_live(ta.live[y], level, open);
+  if (level < MSM_LIVE_LEVELS && open) ta.live[y][level] = 1u;
+}
+
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_stitch(
+    const MsmTailArgs<S> ta, int level, int src) {
+  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
+  const int y = blockIdx.y;
+  // the level before emitted no real open run: every bucket is final already
+  if (ta.live[y][level - 1] == 0u) return;
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / MsmIO<F>::LANES;
+  const uint32_t N = msm_items_at<S>(*ta.nnz[y], level, ta.target[y]);
+  if (g * MSM_SG >= N) return;
+  msm_stitch_lane<F>(ta, y, level, src, g, N);
+}
+
+// The last stitching levels of MSM y in one workgroup (blockIdx.y = MSM): from `level` on, every
+// level has at most MSM_STITCH_LAST lanes, so the workgroup runs them back to back with a barrier
+// between levels (the items pass through global memory inside one CU) until one lane holds every
+// item -- one launch instead of ~4 dependent ones per tail batch.
+constexpr int MSM_STITCH_LAST = 128;
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(MSM_STITCH_LAST * MsmIO<F>::LANES) k_msm_stitch_last(const MsmTailArgs<S> ta,
+                                                                                       int level, int src) {
+  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
+  const int y = blockIdx.y;
+  const uint32_t g = threadIdx.x / MsmIO<F>::LANES;
+  const uint32_t nnz = *ta.nnz[y];
+  for (; level < MSM_LIVE_LEVELS; level++, src ^= 1) {
+    const uint32_t N = msm_items_at<S>(nnz, level, ta.target[y]);
+    if (ta.live[y][level - 1] != 0u && g * MSM_SG < N) msm_stitch_lane<F>(ta, y, level, src, g, N);
+    __threadfence_block();
+    __syncthreads();
+    if (N <= (uint32_t)MSM_SG) break;
+  }
 }
 
 // Weighted bucket reduction sum_b (b+1) S_b.  An item i stands for a group of g = 2^log2g
@@ -1135,9 +1163,14 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   for (int i = 0; i < n; i++) N = std::max(N, t[i]->item_cap[0]);
   N = std::max<size_t>(N, 2);
   int cur = 0;
+  static const bool last_kernel = !getenv("ZKFL_STITCH_LAST") || atoi(getenv("ZKFL_STITCH_LAST")) != 0;
   for (int level = 1; !(ZK_KNOCKOUT & 8); level++) {
     if (level >= MSM_LIVE_LEVELS) return hipErrorInvalidValue;  // liveness flags per level
     const size_t lanes = (N + MSM_SG - 1) / MSM_SG;
+    if (last_kernel && lanes <= (size_t)MSM_STITCH_LAST) {  // the remaining levels in one workgroup
+      hipLaunchKernelGGL((k_msm_stitch_last<FC, SW>), dim3(1, n), dim3(MSM_STITCH_LAST * LN), 0, st, ta, level, cur);
+      break;
+    }
     hipLaunchKernelGGL((k_msm_stitch<FC, SW>), dim3(zk_grid(lanes * LN, 64), n), dim3(64), 0, st, ta, level, cur);
     if (N <= (size_t)MSM_SG) break;
     N = 2 * lanes;
