@@ -675,6 +675,93 @@ def _distinct_over_ranks(device, dist):
     return int(t.sum().item())
 
 
+def _cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _gpu_local_cpus():
+    """Host CPUs local to each visible GPU, in HIP's device order, from sysfs alone (no HIP call:
+    this runs before the rank initializes the runtime).  KFD topology nodes with SIMDs are the GPUs
+    (node order = device order); a node's PCI location gives /sys/bus/pci/devices/<bdf>/local_cpulist.
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES (numeric lists) select and reorder them.  [] if unknown."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    gpus = []
+    try:
+        for node in sorted(os.listdir(base), key=int):
+            props = {}
+            for ln in open(os.path.join(base, node, "properties")):
+                k, _, v = ln.partition(" ")
+                props[k] = v.strip()
+            if int(props.get("simd_count", "0")) <= 0:
+                continue
+            loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+            bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7}"
+            try:
+                cpus = _cpulist(open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read())
+            except OSError:
+                cpus = []
+            gpus.append(cpus)
+    except (OSError, ValueError):
+        return []
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        sel = os.environ.get(var)
+        if sel:
+            try:
+                gpus = [gpus[int(x)] for x in sel.split(",") if x.strip()]
+            except (ValueError, IndexError):
+                return []
+    return gpus
+
+
+def pin_host_cores(local_rank, local_world):
+    """With several ranks on one node, pins this rank (before its first HIP call) to the host cores
+    local to its GPU, shared evenly with the other ranks whose GPUs hang off the same cores; when
+    the topology is unknown or leaves too few allowed cores, to an even 1/local_world share of the
+    allowed cores.  The config-5 legs parse input.json and launch ~50 kernels per proof on host
+    threads (0.6-0.9 ms of host CPU per proof, ~1.2-1.8 cores per rank), so 8 unpinned ranks
+    compete for the same cores and cross NUMA nodes.  One rank alone is left unpinned.
+    ZKFL_PIN=0 disables it.  Returns what was done (reported per rank in the bench line)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    info = {"allowed_cpus": len(allowed), "pinned": False, "cpus": len(allowed), "source": "none"}
+    if local_world <= 1 or os.environ.get("ZKFL_PIN", "1") == "0":
+        return info
+    gpus = _gpu_local_cpus()
+    share, source = None, "even split of the allowed cores"
+    if gpus:
+        mine = gpus[local_rank % len(gpus)]
+        pool = [c for c in allowed if c in set(mine)]
+        peers = [r for r in range(local_world) if gpus[r % len(gpus)] == mine]
+        n, k = len(peers), peers.index(local_rank)
+        if len(pool) >= max(2, len(allowed) // (2 * local_world)) * n:
+            share = pool[k * len(pool) // n:(k + 1) * len(pool) // n]
+            source = f"GPU-local cores ({len(pool)} allowed, {n} ranks on them)"
+    if not share:
+        n = len(allowed)
+        share = allowed[local_rank * n // local_world:(local_rank + 1) * n // local_world] or allowed
+    os.sched_setaffinity(0, share)
+    info.update(pinned=True, cpus=len(share), source=source, cpulist=f"{share[0]}-{share[-1]}"
+                if share == list(range(share[0], share[-1] + 1)) else ",".join(map(str, share)))
+    return info
+
+
+def host_report(rank, device, dist, pin, cpu):
+    """Per-rank host facts for the line: the node's CPUs, each rank's pinning and host CPU per
+    proof of the timed legs (`cpu`: leg -> ms per proof), gathered to rank 0 (gloo)."""
+    mine = {"rank": rank, "device": device, "pin": pin, "host_cpu_ms_per_proof": cpu}
+    ranks = [mine]
+    if dist is not None:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, mine)
+    return {"node_cpus": os.cpu_count(), "ranks": ranks}
+
+
 def launch_ranks(n):
     """bench.py --gpus N without a launcher: N child processes of this script, one per GPU, with
     the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).
@@ -755,7 +842,9 @@ def main():
     ap.add_argument("--extra-steps", type=int, default=16,
                     help="timed steps of the extra-circuit leg (16 x 20 proofs: over 1 s, VERDICT r3)")
     ap.add_argument("--c5-slots", type=int, default=8, help="proof slots per key in the config-5 legs")
-    ap.add_argument("--split-proofs", type=int, default=8,
+    # off by default: the split proof is dominated by one GPU's latency schedule (the
+    # Amdahl bound at G = 8 is above one proof alone), and the leg loads a second (shard) key
+    ap.add_argument("--split-proofs", type=int, default=0,
                     help="split-proof leg: proofs, one at a time, each split over all ranks (0: skip)")
     ap.add_argument("--cli-runs", type=int, default=5,
                     help="cli_prove leg: `npx snarkjs groth16 prove` invocations per circuit (0: skip; 1 GPU only)")
@@ -770,6 +859,7 @@ def main():
                          "(or drop the launcher and let bench.py start them)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    pin = pin_host_cores(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))  # before any HIP call
     from zkfl import circuits, clients, native, wprog, zkey
     # libzkfl (and with it /opt/rocm's HIP runtime) is loaded before torch, whose wheel carries its
     # own libamdhip64 under the same soname: one HIP runtime per process.  torch.distributed is the
@@ -831,7 +921,10 @@ def main():
     # on a fresh process on others)
     lat = latency_leg(key, res)
     log(f"[bench r{rank}] one proof alone: {lat}")
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     elapsed, proofs = timed_run(key, warm_w, steps_w, rs, ctx, dist)
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    host_cpu = {"main": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) * 1e3 / n_timed, 3)}
     assert len(proofs) == n_timed and all(len(p) == 256 for p in proofs)
     pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]   # wtns v2: header 76 B, wire 0 = 1
     verified = verify_all(ctx, zk, proofs, lambda i: pubs[i % len(pubs)])
@@ -868,6 +961,10 @@ def main():
     if args.split_proofs:  # last: the other legs never run beside a second (shard) key
         split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
         log(f"[bench r{rank}] split proof: {split_res}")
+    for tag, leg in (("c5", c5), ("c5_weak", c5w)):
+        if leg:
+            host_cpu[tag] = leg["host_cpu_ms_per_proof"]
+    host = host_report(rank, device, dist, pin, host_cpu)   # collective: every rank
     cli = None
     if args.cli_runs and world == 1:
         try:
@@ -895,7 +992,7 @@ def main():
                        "build_matches_sources": build_id == source_id, "oracle_match": oracle_match,
                        "end_to_end": e2e, "c5": c5, "c5_weak": c5w, "extra_circuit": extra,
                        "latency_single_proof": lat, "dataset_commit": merkle, "split_proof": split_res,
-                       "cli_prove": cli, "cpu_baseline": cpu})
+                       "cli_prove": cli, "cpu_baseline": cpu, "host": host})
         print(json.dumps(line), flush=True)
         if oracle_match is False:
             raise SystemExit("[bench] timed proof 0 differs from the C oracle")

@@ -138,3 +138,41 @@ const fs = require('fs');
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["ok"] is True and r["bad"] is False
     assert _oracle_verify(os.path.join(circuitDir, f"{name}_final.zkey"), public, r["proof"])
+
+
+def test_addon_gc_any_finalizer_order(harness):
+    """A long-lived Node process drops every reference and forces GC before a normal exit: the
+    context's external goes first (its finalizer runs before the key's and the program's), which
+    is safe because the C ABI keeps the context alive for its children (zkfl_ctx_destroy only drops
+    the handle's reference).  Then a second context proves again and the process exits normally
+    (no quickExit)."""
+    proj, circ, name, inp = harness
+    circuitDir = str(circ)
+    addon = os.path.join(PKG, "node", "zkfl.node")
+    script = proj / "gc.js"
+    script.write_text(f"""
+const a = require({json.dumps(addon)});
+const fs = require('fs');
+const dir = {json.dumps(circuitDir)};
+const zk = fs.readFileSync(dir + '/{name}_final.zkey');
+const wp = fs.readFileSync(dir + '/{name}_js/{name}.wasm');
+const input = fs.readFileSync(dir + '/client1_training_input.json', 'utf8');
+const tick = () => new Promise((r) => setImmediate(r));
+(async () => {{
+  let c = a.createContext(0);
+  let k = a.loadKey(c, zk);
+  let p = a.loadProgram(c, wp);
+  const r1 = await a.fullProve(c, k, p, input);
+  c = null;                       // the context first
+  for (let i = 0; i < 4; i++) {{ global.gc(); await tick(); }}
+  k = null; p = null;             // then its children
+  for (let i = 0; i < 4; i++) {{ global.gc(); await tick(); }}
+  const c2 = a.createContext(0);
+  const k2 = a.loadKey(c2, zk);
+  const r2 = await a.fullProve(c2, k2, a.loadProgram(c2, wp), input);
+  console.log(JSON.stringify({{ n1: r1.proof.length, n2: r2.proof.length, pub: r1.publicSignals.equals(r2.publicSignals) }}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    p = _run("node --expose-gc gc.js", proj)
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r == {"n1": 256, "n2": 256, "pub": True}

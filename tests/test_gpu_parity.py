@@ -122,7 +122,8 @@ def test_msm_g1_matches_oracle_pippenger(gpu_ctx):
     assert _g1_std(gpu_ctx.msm_g1(bases, _scal(ss))) == bn.msm(pts, ss)
 
 
-@pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max", "binedge"])
+@pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max", "binedge",
+                                  "binedge17"])
 def test_msm_g1_edge_cases(gpu_ctx, case):
     rnd = random.Random(zlib.crc32(case.encode()))
     n = 3000
@@ -133,7 +134,8 @@ def test_msm_g1_edge_cases(gpu_ctx, case):
     elif case == "ones":          # every entry in bucket 0: skewed accumulation
         ss = [1] * n
     elif case == "small":         # witness-like bits / small ints
-        ss = [rnd.choice([0, 1, 2, 3, 100, 65535, 65536, 1 << 15, (1 << 15) + 1]) for _ in range(n)]
+        ss = [rnd.choice([0, 1, 2, 3, 100, 65535, 65536, 1 << 15, (1 << 15) + 1, (1 << 16) + 1, (1 << 17) - 1,
+                          1 << 17, (1 << 17) + 1]) for _ in range(n)]
     elif case == "neg":           # digits near the signed boundary
         ss = [(R - rnd.randrange(1, 1 << 20)) for _ in range(n)]
     elif case == "dup":           # same base repeated: P + P inside a bucket
@@ -147,6 +149,10 @@ def test_msm_g1_edge_cases(gpu_ctx, case):
     elif case == "binedge":       # bucket sort (csrc/msm.h k_msm_bin_*): digits on high-bin edges
         edge = [1, 2, 255, 256, 257, 512, 32767, 32768, 32769, 65535]
         ss = [sum(rnd.choice(edge) << (16 * j) for j in range(16)) % R for _ in range(n)]
+    elif case == "binedge17":     # the same for 17-bit windows (MSM_WINDOW_BITS=17): bucket 2^16 - 1,
+        # the signed-digit boundary 2^16 / 2^16 + 1 and the high-bin edges of 9 low bits
+        edge = [1, 2, 511, 512, 513, 65535, 65536, 65537, 131071, 0]
+        ss = [sum(rnd.choice(edge) << (17 * j) for j in range(15)) % R for _ in range(n)]
     bases = bytearray(_bases_g1(gpu_ctx, ks))
     if case == "inf_base":
         for i in range(0, n, 3):

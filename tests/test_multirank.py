@@ -43,16 +43,18 @@ def _worker(rank, world, port, out_path):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     import bench
+    pin = bench.pin_host_cores(rank, world)   # the N>1 rule: each rank its share of the host cores
     dist.init_process_group("gloo", rank=rank, world_size=world)
     key = _StubKey(rank)
     elapsed, proofs = bench.timed_run(key, [0], list(range(8)), None, _StubCtx(), dist)
     verified = bench._sum_over_ranks(len(proofs), dist)
+    host = bench.host_report(rank, rank, dist, pin, {"main": 0.5 + rank})
     prof = {k: (0.0, 0, 0.0, 0.0) for k in bench.PROFILED}
 
     class A:
         steps, warmup, slots = 8, 1, 1
     if rank == 0:
-        rep = bench.report(A, world, elapsed, 8 * world, verified, prof, 1, None, {"workload": "stub"}, {})
+        rep = bench.report(A, world, elapsed, 8 * world, verified, prof, 1, None, {"workload": "stub"}, {"host": host})
         with open(out_path, "w") as f:
             json.dump(rep, f)
     dist.destroy_process_group()
@@ -77,6 +79,25 @@ def test_two_rank_gloo_report(tmp_path):
     assert rep["ms_per_step"] >= 8 * 20 / 8 * 0.9
     assert abs(rep["value"] - 2 * 8 / (rep["ms_per_step"] * 8 / 1e3)) < 1e-3 * rep["value"] + 1e-6
     assert rep["metric"].startswith("Groth16 proofs/sec") and rep["verified"] == 16
+    # per-rank host facts (bench.host_report): the node's CPUs, each rank's pinning and host CPU
+    host = rep["host"]
+    assert host["node_cpus"] == os.cpu_count() and [r["rank"] for r in host["ranks"]] == [0, 1]
+    allowed = len(os.sched_getaffinity(0))
+    for r in host["ranks"]:
+        assert r["host_cpu_ms_per_proof"] == {"main": 0.5 + r["rank"]}
+        assert r["pin"]["allowed_cpus"] == allowed
+        if allowed >= 2:   # two ranks: disjoint halves of the allowed cores
+            assert r["pin"]["pinned"] and r["pin"]["cpus"] == allowed // 2 + (allowed % 2) * r["rank"]
+
+
+def test_pin_single_rank_untouched():
+    """One rank on the node keeps the process's affinity (the N=1 headline is not re-pinned)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    before = os.sched_getaffinity(0)
+    info = bench.pin_host_cores(0, 1)
+    assert not info["pinned"] and os.sched_getaffinity(0) == before
+    assert bench._cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
 
 
 def test_bench_refuses_world_size_mismatch():

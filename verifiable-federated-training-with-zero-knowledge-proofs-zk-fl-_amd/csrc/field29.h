@@ -190,6 +190,11 @@ ZK_HD F29 f29_below256(const F29& a) {
 #ifndef F29_SPLIT
 #define F29_SPLIT 1
 #endif
+// 1: the point formulas take their independent products two at a time (f29_mont2); 0: one at a
+// time, each column split over two accumulators (A/B builds)
+#ifndef F29_PAIRED
+#define F29_PAIRED 0
+#endif
 ZK_HD void f29_keep(uint64_t& a) {
 #ifdef __HIP_DEVICE_COMPILE__
   asm volatile("" : "+v"(a));
@@ -272,6 +277,81 @@ ZK_HD F29 f29_sqr(const F29& a) {
   }
   r.v[8] = (uint32_t)carry;
   return r;
+}
+
+// Two INDEPENDENT Montgomery products side by side: A = (sum_j xa_j ya_j) 2^-261 and B likewise,
+// their columns interleaved with ONE 64-bit accumulator per product per column.  f29_mont splits
+// each column over two accumulators so that a product has two dependency chains to issue from,
+// and pays one 64-bit addition per column (17 per product) to join them; here the second chain is
+// the other product, so the joins are gone and a wave still has two chains per column (and the
+// carry of one column no longer waits for the other accumulator's join).  SQA / SQB: that
+// product is the square of xa[0] / xb[0] (normalized), taking each cross product a_i a_j (i < j)
+// once against the doubled limb, as f29_sqr.  Same values and bounds as f29_mont / f29_sqr.
+template <int NA, int NB, bool SQA, bool SQB>
+ZK_HD void f29_mont2(const F29 (&xa)[NA], const F29 (&ya)[NA], const F29 (&xb)[NB], const F29 (&yb)[NB], F29& ra,
+                     F29& rb) {
+  uint32_t da[9], db[9];  // doubled limbs of the squared operands (unused otherwise)
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    da[i] = SQA ? xa[0].v[i] << 1 : 0u;
+    db[i] = SQB ? xb[0].v[i] << 1 : 0u;
+  }
+  uint32_t ma[9], mb[9];
+  uint64_t ca = 0, cb = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t a = ca, b = cb;
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      const int j = k - i;
+      if (SQA) {
+        if (i < j) a += (uint64_t)da[i] * xa[0].v[j];
+        else if (i == j) a += (uint64_t)xa[0].v[i] * xa[0].v[i];
+      } else {
+#pragma unroll
+        for (int q = 0; q < NA; q++) a += (uint64_t)xa[q].v[i] * ya[q].v[j];
+      }
+      if (SQB) {
+        if (i < j) b += (uint64_t)db[i] * xb[0].v[j];
+        else if (i == j) b += (uint64_t)xb[0].v[i] * xb[0].v[i];
+      } else {
+#pragma unroll
+        for (int q = 0; q < NB; q++) b += (uint64_t)xb[q].v[i] * yb[q].v[j];
+      }
+      if (i < k) {
+        a += (uint64_t)ma[i] * P29::P[j];
+        b += (uint64_t)mb[i] * P29::P[j];
+      }
+    }
+    f29_keep(a);
+    f29_keep(b);
+    if (k < 9) {
+      ma[k] = ((uint32_t)a * P29::NINV) & P29::MASK;
+      mb[k] = ((uint32_t)b * P29::NINV) & P29::MASK;
+      a += (uint64_t)ma[k] * P29::P[0];
+      b += (uint64_t)mb[k] * P29::P[0];
+    } else {
+      ra.v[k - 9] = (uint32_t)a & P29::MASK;
+      rb.v[k - 9] = (uint32_t)b & P29::MASK;
+    }
+    ca = a >> 29;
+    cb = b >> 29;
+  }
+  ra.v[8] = (uint32_t)ca;
+  rb.v[8] = (uint32_t)cb;
+}
+
+// ra = a b, rb = c d (two independent products, f29_mont2)
+ZK_HD void f29_mul2(const F29& a, const F29& b, const F29& c, const F29& d, F29& ra, F29& rb) {
+  const F29 xa[1] = {a}, ya[1] = {b}, xb[1] = {c}, yb[1] = {d};
+  f29_mont2<1, 1, false, false>(xa, ya, xb, yb, ra, rb);
+}
+
+// ra = a^2, rb = c^2 of NORMALIZED a, c (two independent squares, f29_mont2)
+ZK_HD void f29_sqr2(const F29& a, const F29& c, F29& ra, F29& rb) {
+  const F29 xa[1] = {a}, xb[1] = {c};
+  f29_mont2<1, 1, true, true>(xa, xa, xb, xb, ra, rb);
 }
 
 // (a b + c d) 2^-261 with one reduction
@@ -389,6 +469,42 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
     }
     return {a.x, y, f29_const(P29::ONE), f29_const(P29::ONE)};
   }
+#if F29_PAIRED
+  // the same products as below, two independent ones at a time (f29_mont2): U2 | S2, PP | RR,
+  // PPP | Q, ZZ3 | ZZZ3, then Y3 (a two-product sum: its own two chains)
+  F29 U2, S2;
+  f29_mul2(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
+  F29 t;
+#pragma unroll
+  for (int i = 0; i < 9; i++) t.v[i] = neg ? P29::K2_1[i] - S2.v[i] : S2.v[i];
+  F29 P = f29_ksub(P29::K7_1, U2, p.X);
+  F29 R = f29_ksub(P29::K7_1, t, p.Y);
+  f29_norm(P);
+  f29_norm(R);
+  F29 PP, RR;
+  f29_sqr2(P, R, PP, RR);
+  if (f29_is_zero(PP)) {
+    if (f29_is_zero(RR)) {
+      F29 y = a.y;
+      if (neg) {
+        y = f29_ksub(P29::K1_1, f29_zero(), a.y);
+        f29_norm(y);
+      }
+      return f29_dbl({a.x, y, f29_const(P29::ONE), f29_const(P29::ONE)});
+    }
+    return f29_inf();
+  }
+  F29 PPP, Q;
+  f29_mul2(P, PP, p.X, PP, PPP, Q);
+  XYZZ<FqOps29> r;
+  f29_mul2(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
+  r.X = f29_ksub3(P29::K4_3, RR, PPP, Q, Q);
+  f29_norm(r.X);
+  const F29 QX = f29_ksub(P29::K6_1, Q, r.X);
+  const F29 nY = f29_ksub(P29::K7_1, f29_zero(), p.Y);
+  r.Y = f29_mulsum2(R, QX, nY, PPP);
+  return r;
+#else
   const F29 U2 = f29_mul(a.x, p.ZZ);
   const F29 S2 = f29_mul(a.y, p.ZZZ);
   F29 t;
@@ -422,6 +538,7 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
   r.ZZ = f29_mul(p.ZZ, PP);
   r.ZZZ = f29_mul(p.ZZZ, PPP);
   return r;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -600,6 +717,31 @@ ZK_HD Affine<FqOps29> f29_affine_add(const Affine<FqOps29>& a, const Affine<FqOp
 ZK_HD XYZZ<FqOps29> f29_add(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
   if (f29_is_zero(q.ZZ)) return p;
   if (f29_is_zero(p.ZZ)) return q;
+#if F29_PAIRED
+  // two independent products at a time (f29_mont2), the same values as below
+  F29 U1, U2, S1, S2, PP, RR, PPP, Q, Z2, Z3;
+  f29_mul2(p.X, q.ZZ, q.X, p.ZZ, U1, U2);
+  f29_mul2(p.Y, q.ZZZ, q.Y, p.ZZZ, S1, S2);
+  F29 P = f29_ksub(P29::K2_1, U2, U1);
+  F29 R = f29_ksub(P29::K2_1, S2, S1);
+  f29_norm(P);
+  f29_norm(R);
+  f29_sqr2(P, R, PP, RR);
+  if (f29_is_zero(PP)) {
+    if (f29_is_zero(RR)) return f29_dbl(p);
+    return f29_inf();
+  }
+  f29_mul2(P, PP, U1, PP, PPP, Q);
+  f29_mul2(p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, Z2, Z3);
+  XYZZ<FqOps29> r;
+  f29_mul2(Z2, PP, Z3, PPP, r.ZZ, r.ZZZ);
+  r.X = f29_ksub3(P29::K4_3, RR, PPP, Q, Q);
+  f29_norm(r.X);
+  const F29 QX = f29_ksub(P29::K6_1, Q, r.X);
+  const F29 nS1 = f29_ksub(P29::K2_1, f29_zero(), S1);
+  r.Y = f29_mulsum2(R, QX, nS1, PPP);
+  return r;
+#else
   const F29 U1 = f29_mul(p.X, q.ZZ);
   const F29 U2 = f29_mul(q.X, p.ZZ);
   const F29 S1 = f29_mul(p.Y, q.ZZZ);
@@ -625,6 +767,7 @@ ZK_HD XYZZ<FqOps29> f29_add(const XYZZ<FqOps29>& p, const XYZZ<FqOps29>& q) {
   r.ZZ = f29_mul(f29_mul(p.ZZ, q.ZZ), PP);
   r.ZZZ = f29_mul(f29_mul(p.ZZZ, q.ZZZ), PPP);
   return r;
+#endif
 }
 
 // ---------------------------------------------------------------------------

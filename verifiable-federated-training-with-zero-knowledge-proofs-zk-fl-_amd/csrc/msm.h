@@ -8,13 +8,13 @@
 //
 // MI355X design:
 //  * Bases are fixed per proving key, so at key-load time every base P_i is expanded into
-//    W = 16 window copies 2^(16 j) P_i (affine, Montgomery), laid out [i][j] (64 B / 128 B
-//    each).  One MSM is then a single bucket set: every (i, j) with a non-zero signed 16-bit
-//    digit d_ij lands in bucket |d_ij|-1 (2^15 buckets), no per-window bucket reduction and
-//    no window combination.  288 GB of HBM makes the 16x base expansion (~2 GB for the
-//    2^18-constraint training circuit) free.
-//  * Signed digits in [-2^15, 2^15]; the sign is applied by negating y on the fly.
-//  * (bucket, entry) pairs are bucket-sorted (two counting passes over the 15-bit bucket
+//    W window copies 2^(c j) P_i (affine, Montgomery; c = MSM_C bits, W = ceil(255 / c): 16 x 16
+//    or 15 x 17), laid out [i][j] (64 B / 128 B each).  One MSM is then a single bucket set:
+//    every (i, j) with a non-zero signed c-bit digit d_ij lands in bucket |d_ij|-1 (2^(c-1)
+//    buckets), no per-window bucket reduction and no window combination.  288 GB of HBM makes
+//    the Wx base expansion (~2 GB for the 2^18-constraint training circuit) free.
+//  * Signed digits in [-(2^(c-1) - 1), 2^(c-1)]; the sign is applied on the fly (f29_madd_signed).
+//  * (bucket, entry) pairs are bucket-sorted (two counting passes over the (c-1)-bit bucket
 //    number, k_msm_bin_*; zero digits dropped).  The sorted entries are cut
 //    into fixed chunks of L entries, one lane each, independent of bucket boundaries: every lane
 //    does exactly L additions.  A bucket run that starts and ends inside its chunk is final and
@@ -24,7 +24,7 @@
 //    lane walking its chunks (that serial walk, not the arithmetic, used to set the MSM's latency).
 //  * Accumulation uses XYZZ + affine mixed additions (10 Fq mul for G1).
 //  * Bucket reduction sum_b (b+1) S_b: 8 buckets folded serially per lane, then 64-lane blocks
-//    (LDS suffix scan + trees); two levels for 2^15 buckets, the second writing the MSM result.
+//    (LDS suffix scan + trees); two levels for the 2^(c-1) buckets, the second writing the MSM result.
 #pragma once
 #include <algorithm>
 #include <cstring>
@@ -265,7 +265,7 @@ struct MsmCompute<Fq2Ops> {
 };
 
 // ---------------------------------------------------------------------------
-// Key-load-time window expansion: out[i*W + j] = 2^(16 j) * in[i]  (affine)
+// Key-load-time window expansion: out[i*W + j] = 2^(c j) * in[i]  (affine)
 // ---------------------------------------------------------------------------
 template <class F>
 __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__ in, size_t n, Affine<F>* __restrict__ out) {
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
     for (int j = 0; j < MSM_W; j++) out[i * MSM_W + j] = p;
     return;
   }
-  // Keep the 16 window copies in XYZZ in the output slots' scratch (global), with a
+  // Keep the W window copies in XYZZ in the output slots' scratch (global), with a
   // Montgomery batch inversion of their ZZZ over the 16 copies.
   XYZZ<F> acc = xyzz_from_affine<F>(p);
   T pref[MSM_W];
@@ -303,6 +303,15 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
 // ---------------------------------------------------------------------------
 // Per-MSM kernels
 // ---------------------------------------------------------------------------
+// Window j of a 256-bit scalar (8 x 32-bit words): bits [c j, c j + c) (j is unrolled, so the
+// word index and shifts are constants).
+ZK_DEV uint32_t msm_window(const uint32_t (&s)[8], int j) {
+  const int b = MSM_C * j, w = b >> 5, sh = b & 31;
+  uint32_t x = s[w] >> sh;
+  if (sh + MSM_C > 32 && w + 1 < 8) x |= s[w + 1] << (32 - sh);
+  return x & ((1u << MSM_C) - 1u);
+}
+
 // Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31, written
 // window-major (position j*n + i: consecutive lanes store consecutive words; the sort that
 // follows does not care about the input order).  Also counts the non-zero digits into *nnz
@@ -323,7 +332,7 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
     uint32_t carry = 0;
 #pragma unroll
     for (int j = 0; j < MSM_W; j++) {
-      uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+      uint32_t raw = msm_window(s, j);
       int32_t d = (int32_t)(raw + carry);
       if (d > MSM_NB) {
         d -= (1 << MSM_C);
@@ -350,7 +359,7 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
 
 // ---------------------------------------------------------------------------
 // Bucket sort of the digits (the default; MSM_SORT_ROCPRIM=1 keeps the rocPRIM radix sort).
-// Keys are 15-bit bucket numbers, so two counting passes put every non-zero digit in bucket
+// Keys are (c-1)-bit bucket numbers, so two counting passes put every non-zero digit in bucket
 // order with no look-back and no memsets:
 //   count   per block of bases: digits -> LDS histogram of the high key bits -> cnt[bin][block]
 //   scan    one workgroup: cnt (bin-major) -> exclusive offsets, bin starts, nnz
@@ -366,7 +375,7 @@ constexpr int MSM_SORT_LB = MSM_SORT_LOW_BITS;       // key bits sorted inside a
 constexpr int MSM_SORT_NL = 1 << MSM_SORT_LB;        // low counters per high-bin workgroup
 constexpr int MSM_SORT_HB = MSM_NB >> MSM_SORT_LB;   // high bins
 constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
-static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 256 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
+static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 512 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
 constexpr int MSM_SORT_BT = 1024;         // threads of the scan workgroup
 constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin workgroup
 static_assert(MSM_SORT_BINT >= MSM_SORT_NL && MSM_SORT_BINT <= 1024, "bins: one thread per low counter");
@@ -384,7 +393,7 @@ ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t*
   uint32_t carry = 0;
 #pragma unroll
   for (int j = 0; j < MSM_W; j++) {
-    const uint32_t raw = (s[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+    const uint32_t raw = msm_window(s, j);
     int32_t d = (int32_t)(raw + carry);
     carry = d > MSM_NB ? 1u : 0u;
     if (carry) d -= (1 << MSM_C);
@@ -525,7 +534,7 @@ __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restric
       if ((t & 63) >= (uint32_t)o) x += y;
     }
   }
-  __shared__ uint32_t wt[4];
+  __shared__ uint32_t wt[MSM_SORT_NL / 64];
   if (t < MSM_SORT_NL && (t & 63) == 63) wt[t >> 6] = x;
   __syncthreads();
   if (t < MSM_SORT_NL) {
@@ -817,10 +826,10 @@ template <class S>
 constexpr int msm_wsum_q0() {
   return sizeof(typename S::T) == 32 ? MSM_G1_WSUM_Q : MSM_G2_WSUM_Q;
 }
-// Q0 of the latency schedule's reduction (one proof alone, msm_tails(..., fast = true)): 4 buckets
-// per level-0 lane, 128 level-0 blocks, a 128-lane level 1 -- about 45 dependent point operations
-// on the chain instead of ~70, for ~1.8x the reduction's (small) work
-constexpr int MSM_WSUM_Q_FAST = 4;
+// Q0 of the latency schedule's reduction (one proof alone, msm_tails(..., fast = true)): 128
+// level-0 blocks (4 buckets per lane at c = 16), a 128-lane level 1 -- about 45 dependent point
+// operations on the chain instead of ~70, for ~1.8x the reduction's (small) work
+constexpr int MSM_WSUM_Q_FAST = MSM_NB / (MSM_RB * 128);  // 128 level-0 blocks: 4 at c = 16, 8 at c = 17
 // lanes of a reduction block: level 0 one wave (MSM_RB), level 1 one lane per level-0 block
 template <bool L0, int Q0>
 constexpr int msm_wsum_rb() {
@@ -1009,6 +1018,10 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
   const size_t m = cap * MSM_W;
   t.target = std::min<uint32_t>(msm_resident_chunks<F>(), 0xFFFFFFu);
   t.l0 = msm_tail_l0<F>(cap);
+  // the batch-affine rounds write their items with the fixed AFF_L: the stitching levels must count
+  // level-0 items with the same chunk length (msm_items_at)
+  if constexpr (std::is_same<F, FqOps>::value)
+    if (MSM_G1_AFFINE) t.l0 = AFF_L;
   t.max_chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) t.max_chunks = std::min<size_t>(t.max_chunks, t.target);  // msm_chunk_len bounds the lanes
   t.item_cap[0] = 2 * t.max_chunks;
@@ -1121,7 +1134,8 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
   if constexpr (std::is_same<F, FqOps>::value) {
     if (MSM_G1_AFFINE && t.aff && t.aff->lanes && !(ZK_KNOCKOUT & 64)) {  // batch-affine rounds
       ZK_CHECK(msm_aff_accumulate<MSM_G1_AFF_WAVES>(b, keys, vals, t, *t.aff, st));
-      ZK_CHECK(hipMemsetAsync(t.live, 1, 1, st));  // it does not track open runs: stitch every level
+      // it does not track open runs: stitch every level (the whole flag word, not its low byte)
+      ZK_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(t.live), 1u, 1, st));
       done = true;
     }
   }

@@ -8,9 +8,19 @@
 
 namespace zkfl {
 
-constexpr int MSM_C = 16;                  // window bits
-constexpr int MSM_W = 16;                  // windows covering 256 bits (scalars < r < 2^254)
+// Window width c of the signed-digit decomposition.  Scalars are < r < 2^254; with signed digits
+// d in [-(2^(c-1) - 1), 2^(c-1)] the top window absorbs the last carry when c W >= 255, so
+// W = ceil(255 / c): 16 windows at c = 16, 15 at c = 17.  Every base is expanded into its W window
+// copies at key load, so an MSM accumulates one entry per non-zero digit into ONE set of 2^(c-1)
+// buckets; c = 17 cuts the entries of a full-width scalar by 1/16 and doubles the buckets the
+// reduction folds.  Bucket keys are |d| - 1 < 2^(c-1), a u16 for c <= 17.
+#ifndef MSM_WINDOW_BITS
+#define MSM_WINDOW_BITS 16
+#endif
+constexpr int MSM_C = MSM_WINDOW_BITS;     // window bits
+constexpr int MSM_W = (255 + MSM_C - 1) / MSM_C;  // windows covering the 254-bit scalars + the last carry
 constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
+static_assert(MSM_C >= 12 && MSM_C <= 17 && MSM_C * MSM_W >= 255, "window width: u16 bucket keys, 254-bit scalars");
 // Knock-out builds for marginal-cost measurements (tools/ko_probe.py; proofs are WRONG, timing
 // only): 1 assembly, 2 digit sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
 // 64 the G1 accumulation kernel.  0 in every real build; a non-zero value only compiles together
@@ -26,9 +36,12 @@ constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
 #ifndef MSM_SORT_ROCPRIM
 #define MSM_SORT_ROCPRIM 0
 #endif
-// key bits sorted inside one high bin of the bucket sort (8: 128 high bins, 7: 256)
+// the rocPRIM path keys zero digits MSM_KEY_NONE = 0xFFFF, a real bucket at c = 17
+static_assert(!MSM_SORT_ROCPRIM || MSM_C <= 16, "rocPRIM digit sort: c <= 16");
+// key bits sorted inside one high bin of the bucket sort (c - 1 - LOW_BITS high bits: 128 high
+// bins at c = 16 with 8, at c = 17 with 9)
 #ifndef MSM_SORT_LOW_BITS
-#define MSM_SORT_LOW_BITS 8
+#define MSM_SORT_LOW_BITS (MSM_C - 8)
 #endif
 // pairs of one high bin staged in LDS by the bucket sort's bins pass (0: the bin is read twice)
 #ifndef MSM_SORT_STAGE
@@ -59,7 +72,7 @@ constexpr int MSM_L = MSM_G1_L;            // sorted entries per accumulation la
 constexpr int MSM_SG = MSM_STITCH_SG;      // partial sums per lane in each stitching level
 constexpr int MSM_RB = 64;                 // items per block (one wave) in the weighted bucket reduction
 constexpr uint32_t MSM_ITEM_DUMMY = 0x80000000u;  // stitch item flag: padding (its value is infinity)
-constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit: sorted past every bucket
+constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit (rocPRIM path only): sorted past every bucket
 #ifndef MSM_G2_L
 #define MSM_G2_L 16
 #endif

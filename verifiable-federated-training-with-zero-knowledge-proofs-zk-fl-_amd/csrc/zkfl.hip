@@ -793,6 +793,10 @@ struct zkfl_ctx {
   void* asm_buf = nullptr;   // zkfl_groth16_assemble's device buffers (grown on demand, reused)
   size_t asm_cap = 0;
   WtBuf wt;                  // wave-timeline records (ZK_WTRACE builds, zkfl_debug_wtrace)
+  // Lifetime: the caller's handle holds one reference and every key and witness program made on
+  // the context holds one more, so zkfl_ctx_destroy and the children's frees may come in any
+  // order (the N-API finalizers run in an unspecified order); the device state goes with the last.
+  std::atomic<int> refs{1};
 };
 
 // One in-flight proof: its own streams, scratch and per-proof vectors.
@@ -899,6 +903,9 @@ struct zkfl_wprog {
   zkfl_ctx* ctx = nullptr;
   WProg* p = nullptr;
 };
+
+static void ctx_retain(zkfl_ctx* ctx);
+static void ctx_release(zkfl_ctx* ctx);
 
 namespace {
 
@@ -1113,7 +1120,9 @@ void key_release(zkfl_key* k) {
   void* ptrs[] = {k->rows, k->cols, k->coefs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  zkfl_ctx* ctx = k->ctx;
   delete k;
+  if (ctx) ctx_release(ctx);  // the key's reference (taken when it was made)
 }
 
 int get_rs(const uint8_t* rs, uint32_t out[16]) {
@@ -1403,9 +1412,10 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
       lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT;
   {
     // the tails this chain accumulates into: G1 A, B1, C (+ H), [H]; G2 B2 when it shares B1's sort
-    // on this stream (a separate G2 stream's msm_run empties its own)
+    // on this stream (a separate G2 stream's msm_run empties its own).  The condition is the body's
+    // `share` below: a slot with a second stream under serialized profiling shares too.
     const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1) ? 3 : 4;
-    const bool g2 = lowlat_path || (k->share_b && !s->st_g2 && !(ZK_KNOCKOUT & 32));
+    const bool g2 = lowlat_path || (k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32));
     ProofStart ps = {};
     auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
       ps.buckets[ps.n] = static_cast<uint4*>(buckets);
@@ -1887,8 +1897,11 @@ int zkfl_ctx_create(int device, zkfl_ctx** out) {
   return ZKFL_OK;
 }
 
-int zkfl_ctx_destroy(zkfl_ctx* ctx) {
-  if (!ctx) return ZKFL_OK;
+static void ctx_retain(zkfl_ctx* ctx) { ctx->refs.fetch_add(1, std::memory_order_relaxed); }
+
+// Drops one reference; the last one tears the context down.
+static void ctx_release(zkfl_ctx* ctx) {
+  if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->st);
   ctx->prof.reset();
@@ -1900,6 +1913,15 @@ int zkfl_ctx_destroy(zkfl_ctx* ctx) {
   }
   (void)hipStreamDestroy(ctx->st);
   delete ctx;
+}
+
+// The caller's handle: after this call the handle is gone, but keys and witness programs still
+// alive keep the device state until they are freed.
+int zkfl_ctx_destroy(zkfl_ctx* ctx) {
+  if (!ctx) return ZKFL_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->st);
+  ctx_release(ctx);
   return ZKFL_OK;
 }
 
@@ -1964,6 +1986,7 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
   hipStream_t st = ctx->st;
   zkfl_key* k = new zkfl_key();
   k->ctx = ctx;
+  ctx_retain(ctx);  // dropped by key_release
   k->nVars = nVars;
   k->nPub = nPub;
   k->n = dom;
@@ -2944,6 +2967,7 @@ int zkfl_wprog_load(zkfl_ctx* ctx, const uint8_t* prog, size_t len, zkfl_wprog**
   if (rc != ZKFL_OK) return fail(rc, err);
   zkfl_wprog* w = new zkfl_wprog();
   w->ctx = ctx;
+  ctx_retain(ctx);  // dropped by zkfl_wprog_free
   w->p = p;
   *out = w;
   return ZKFL_OK;
@@ -2951,9 +2975,12 @@ int zkfl_wprog_load(zkfl_ctx* ctx, const uint8_t* prog, size_t len, zkfl_wprog**
 
 int zkfl_wprog_free(zkfl_wprog* prog) {
   if (!prog) return ZKFL_OK;
-  (void)hipSetDevice(prog->ctx->device);
+  zkfl_ctx* ctx = prog->ctx;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->st);
   wprog_free(prog->p);
   delete prog;
+  ctx_release(ctx);
   return ZKFL_OK;
 }
 

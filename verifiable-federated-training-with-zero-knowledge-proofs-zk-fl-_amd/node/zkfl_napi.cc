@@ -72,7 +72,9 @@ struct CtxBox {
   }
 };
 
-// argv value -> the context (waiting for its creation); throws and returns nullptr when it failed
+// argv value -> the context (waiting for its creation); throws and returns nullptr when it failed.
+// Every entry point that takes a context goes through here, so a failed creation (no device, out
+// of memory) surfaces with its own code and message rather than as a null-context error.
 zkfl_ctx* ctx_arg(napi_env env, napi_value v) {
   void* data = nullptr;
   if (napi_get_value_external(env, v, &data) != napi_ok || !data) return nullptr;
@@ -85,10 +87,8 @@ zkfl_ctx* ctx_arg(napi_env env, napi_value v) {
   return c;
 }
 
-// the context behind an external (waiting for its creation; nullptr if that failed: the zkfl
-// call it goes to then reports a null context)
-zkfl_ctx* ctx_box(void* data) { return data ? static_cast<CtxBox*>(data)->get() : nullptr; }
-
+// Finalizers run in an unspecified order; the C ABI keeps the context alive while keys and
+// programs made on it live (zkfl_ctx_destroy drops only the handle's reference), so any order is safe.
 void ctx_finalize(napi_env, void* data, void*) {
   CtxBox* b = static_cast<CtxBox*>(data);
   zkfl_ctx_destroy(b->get());
@@ -276,7 +276,11 @@ napi_value Prove(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   ProveWork* w = new ProveWork();
-  w->ctx = ctx_box(ctx);
+  w->ctx = ctx_arg(env, argv[0]);  // throws the context's creation error
+  if (!w->ctx) {
+    delete w;
+    return nullptr;
+  }
   w->key = static_cast<zkfl_key*>(key);
   w->wtns.assign(static_cast<uint8_t*>(wt), static_cast<uint8_t*>(wt) + wlen);
   if (argc >= 4 && napi_get_buffer_info(env, argv[3], &rs, &rslen) == napi_ok && rslen == 64)
@@ -336,7 +340,11 @@ napi_value Verify(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   VerifyWork* w = new VerifyWork();
-  w->ctx = ctx_box(ctx);
+  w->ctx = ctx_arg(env, argv[0]);  // throws the context's creation error
+  if (!w->ctx) {
+    delete w;
+    return nullptr;
+  }
   w->vk.assign(static_cast<uint8_t*>(vk), static_cast<uint8_t*>(vk) + vlen);
   w->pub.assign(static_cast<uint8_t*>(pub), static_cast<uint8_t*>(pub) + plen);
   w->pub.resize(plen + 32);  // never empty (data() of an empty vector may be null)
@@ -362,8 +370,10 @@ napi_value LoadProgram(napi_env env, napi_callback_info info) {
     napi_throw_type_error(env, nullptr, "loadProgram(ctx, zkwpBuffer)");
     return nullptr;
   }
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
   zkfl_wprog* prog = nullptr;
-  int rc = zkfl_wprog_load(ctx_box(ctx), static_cast<const uint8_t*>(data), len, &prog);
+  int rc = zkfl_wprog_load(c, static_cast<const uint8_t*>(data), len, &prog);
   if (rc) return throw_err(env, rc);
   napi_value ext;
   napi_create_external(env, prog, prog_finalize, nullptr, &ext);
@@ -419,7 +429,11 @@ napi_value Witness(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   WitnessWork* w = new WitnessWork();
-  w->ctx = ctx_box(ctx);
+  w->ctx = ctx_arg(env, argv[0]);  // throws the context's creation error
+  if (!w->ctx) {
+    delete w;
+    return nullptr;
+  }
   w->prog = static_cast<zkfl_wprog*>(prog);
   w->json.resize(jlen + 1);
   napi_get_value_string_utf8(env, argv[2], &w->json[0], jlen + 1, &jlen);
@@ -494,7 +508,11 @@ napi_value FullProve(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   FullProveWork* w = new FullProveWork();
-  w->ctx = ctx_box(ctx);
+  w->ctx = ctx_arg(env, argv[0]);  // throws the context's creation error
+  if (!w->ctx) {
+    delete w;
+    return nullptr;
+  }
   w->key = static_cast<zkfl_key*>(key);
   w->prog = static_cast<zkfl_wprog*>(prog);
   w->json.resize(jlen + 1);
@@ -522,8 +540,10 @@ napi_value Pairing(napi_env env, napi_callback_info info) {
     napi_throw_type_error(env, nullptr, "pairing(ctx, g1Buffer(64), g2Buffer(128))");
     return nullptr;
   }
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
   uint8_t gt[384];
-  int rc = zkfl_pairing(ctx_box(ctx), 1, static_cast<const uint8_t*>(g1),
+  int rc = zkfl_pairing(c, 1, static_cast<const uint8_t*>(g1),
                         static_cast<const uint8_t*>(g2), gt);
   if (rc) return throw_err(env, rc);
   napi_value buf;
@@ -557,9 +577,11 @@ napi_value HashCall(napi_env env, napi_callback_info info, bool vector) {
                                                : "poseidon(ctx, arity, n, inputsBuffer(n*arity*32))");
     return nullptr;
   }
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
   std::vector<uint8_t> out((size_t)n * 32 + 32);
-  int rc = vector ? zkfl_vector_hash_batch(ctx_box(ctx), width, n, static_cast<const uint8_t*>(in), out.data())
-                  : zkfl_poseidon_batch(ctx_box(ctx), width, n, static_cast<const uint8_t*>(in), out.data());
+  int rc = vector ? zkfl_vector_hash_batch(c, width, n, static_cast<const uint8_t*>(in), out.data())
+                  : zkfl_poseidon_batch(c, width, n, static_cast<const uint8_t*>(in), out.data());
   if (rc) return throw_err(env, rc);
   napi_value buf;
   void* p;
@@ -583,8 +605,10 @@ napi_value MerkleBuild(napi_env env, napi_callback_info info) {
     return nullptr;
   }
   const size_t nodes = ((size_t)2 << depth) - 1;
+  zkfl_ctx* c = ctx_arg(env, argv[0]);
+  if (!c) return nullptr;
   std::vector<uint8_t> out(nodes * 32);
-  int rc = zkfl_merkle_build(ctx_box(ctx), static_cast<const uint8_t*>(in), len / 32, depth, out.data());
+  int rc = zkfl_merkle_build(c, static_cast<const uint8_t*>(in), len / 32, depth, out.data());
   if (rc) return throw_err(env, rc);
   napi_value buf;
   void* p;
