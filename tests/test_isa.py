@@ -59,6 +59,21 @@ def test_accumulation_kernels_do_not_spill(acc):
         assert r["group_segment_fixed_size"] == 8192, (name, r)  # two 4 KB LDS-DMA buffers per wave
 
 
+def test_accumulation_census(acc):
+    """The main loops hold the point formula's products exactly (G1 madd: 6 products x 162 + 2
+    squares x 126 + the Y3 sum 243 = 1467 v_mad_u64_u32; G2 per lane 2187), and the G1 formula's
+    other instructions stay within the budget the paired products brought (round 5: 2,345 -> 2,211
+    VALU instructions, the 17 column joins of each paired product gone)."""
+    for name, lines in acc.items():
+        g2 = "Fq2Pair29" in name
+        cz = isa_check.census(lines, 2187 if g2 else 1467)
+        assert cz["formula"]["mad64"] == (2187 if g2 else 1467), name
+        assert cz["formula"]["mul_lo"] == 81, name  # 9 Montgomery m per reduction, 9 reductions per lane
+        if not g2:
+            assert cz["formula"]["valu"] <= 2250, (name, cz["formula"])
+            assert cz["formula"]["add64"] <= 180, (name, cz["formula"])  # joins of unpaired products only
+
+
 def test_no_function_clobbers_its_return_address():
     """Round-3 G2 ceremony hang (commit 68f6c67), root cause found on the CPU from the pre-fix code
     object: the outlined smul_xyzz<Fq2Ops> / smul_aff<Fq2Ops> (333 / 276 KB, past the +-128 KB

@@ -105,8 +105,10 @@ _ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
 _TARGET = re.compile(r"<[^>+]+\+0x([0-9a-f]+)>")
 
 
-def lds_dma_hazards(lines: list[str]) -> list[str]:
-    """ds_read_b128 instructions reachable with an LDS DMA possibly in flight (see module doc)."""
+def _cfg(lines: list[str]):
+    """(ins, blocks, succs): the kernel's instructions as (offset from its start, text), its basic
+    blocks as [start, end) instruction index ranges, and each block's successor blocks (branch
+    targets from the disassembly's <sym+0xOFF> annotations)."""
     ins = []  # (offset from the kernel start, text)
     base = None
     for ln in lines:
@@ -141,6 +143,12 @@ def lds_dma_hazards(lines: list[str]) -> list[str]:
         last = e - 1
         nxt = succ_of.get(last, [e] if e < len(ins) else [])
         succs.append([block_of[x] for x in nxt if x in block_of])
+    return ins, blocks, succs
+
+
+def lds_dma_hazards(lines: list[str]) -> list[str]:
+    """ds_read_b128 instructions reachable with an LDS DMA possibly in flight (see module doc)."""
+    ins, blocks, succs = _cfg(lines)
     wait0 = re.compile(r"^s_waitcnt\b.*\bvmcnt\(0\)")
 
     def transfer(k: int, pending: bool, report: list[str] | None) -> bool:
@@ -168,6 +176,120 @@ def lds_dma_hazards(lines: list[str]) -> list[str]:
     for k in range(len(blocks)):
         transfer(k, entry[k], bad)
     return bad
+
+
+# VALU instruction classes of the census (first match wins); everything else starting with v_ is
+# "valu other", ds_ LDS, global_/buffer_ VMEM, s_ scalar
+_CLASSES = (
+    ("mad64", ("v_mad_u64_u32",)),                                  # the limb products
+    ("mul_lo", ("v_mul_lo_u32",)),                                  # Montgomery m = c * n' mod 2^29
+    ("add64", ("v_lshl_add_u64", "v_add_co_u32", "v_addc_co_u32", "v_add_u64")),  # column joins / sums
+    ("shift64", ("v_lshrrev_b64", "v_lshlrev_b64", "v_alignbit_b32")),  # column carries, limb repacking
+    ("mask", ("v_and_b32", "v_bfe_u32", "v_and_or_b32", "v_bfi_b32")),  # 29-bit limb masks
+    ("add32", ("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_add3_u32", "v_sub_co", "v_subb", "v_add_lshl")),
+    ("logic", ("v_or", "v_xor", "v_lshl", "v_lshr", "v_ashr", "v_not", "v_bitop3", "v_perm")),
+    ("cmp_sel", ("v_cmp", "v_cndmask")),
+    ("mov", ("v_mov",)),
+    ("lane", ("v_readlane", "v_writelane", "v_readfirstlane", "v_permlane")),
+)
+
+
+def _cls(text: str) -> str:
+    op = text.split()[0] if text else ""
+    for name, prefixes in _CLASSES:
+        if op.startswith(prefixes):
+            return name
+    if op.startswith("v_"):
+        return "valu_other"
+    if op.startswith("ds_"):
+        return "lds"
+    if op.startswith(("global_", "buffer_", "scratch_")):
+        return "vmem"
+    return "salu"
+
+
+_VALU = tuple(n for n, _ in _CLASSES) + ("valu_other",)
+
+
+def census(lines: list[str], formula_mads: int) -> dict:
+    """Instruction census of an accumulation kernel's main loop (the innermost back edge whose
+    blocks hold the most v_mad_u64_u32).  formula_mads: the mads of one point addition as written (G1 madd:
+    6 products x 162 + 2 squares x 126 + the Y3 product sum 243 = 1467); the loop blocks with mads
+    whose counts sum to exactly that are the formula's ("formula"), other blocks with mads are the
+    special cases (P == 0: the doubling, "cold"), blocks with a global store are the run ends
+    ("emit": executed when any lane of the wave closes a bucket run), mad-free blocks before the
+    first formula block are the loop head ("head": key / index loads, the LDS read of the
+    prefetched base and its 8 x 32 -> 9 x 29 repacking, the zero tests), the rest "other".  The
+    per-entry path is head + formula."""
+    import itertools
+    ins, blocks, succs = _cfg(lines)
+    cnt = []
+    for s, e in blocks:
+        c: dict[str, int] = {}
+        for i in range(s, e):
+            k = _cls(ins[i][1])
+            c[k] = c.get(k, 0) + 1
+        c["stores"] = sum(1 for i in range(s, e) if ins[i][1].startswith(("global_store", "buffer_store")))
+        cnt.append(c)
+    # the main loop: the back edge whose block range holds the most mads
+    best = None
+    for k, ss in enumerate(succs):
+        for t in ss:
+            if t <= k:
+                m = sum(cnt[j].get("mad64", 0) for j in range(t, k + 1))
+                if best is None or (m, t - k) > (best[0], best[1] - best[2]):  # most mads, then innermost
+                    best = (m, t, k)
+    assert best, "no loop"
+    _, lo, hi = best
+    loop = list(range(lo, hi + 1))
+    withmad = [j for j in loop if cnt[j].get("mad64", 0)]
+    formula = None
+    for r in range(1, len(withmad) + 1):
+        for comb in itertools.combinations(withmad, r):
+            if sum(cnt[j]["mad64"] for j in comb) == formula_mads:
+                formula = list(comb)
+                break
+        if formula:
+            break
+    assert formula, f"no loop blocks hold exactly {formula_mads} mads: {[cnt[j].get('mad64') for j in withmad]}"
+    first = min(formula)
+    rows = []
+    for j in loop:
+        c = cnt[j]
+        if j in formula:
+            kind = "formula"
+        elif c.get("mad64"):
+            kind = "cold"
+        elif c["stores"]:
+            kind = "emit"
+        elif j < first:
+            kind = "head"
+        else:
+            kind = "other"
+        rows.append((ins[blocks[j][0]][0], kind, c))
+
+    def total(kinds):
+        t: dict[str, int] = {}
+        for _, kind, c in rows:
+            if kind in kinds:
+                for k, v in c.items():
+                    t[k] = t.get(k, 0) + v
+        t["valu"] = sum(t.get(k, 0) for k in _VALU)
+        return t
+    return {"blocks": rows, "path": total(("head", "formula")), "formula": total(("formula",)),
+            "head": total(("head",)), "emit": total(("emit",)), "cold": total(("cold",))}
+
+
+def print_census(name: str, cz: dict) -> None:
+    print(f"{name}: main-loop census (per lane, per accumulated entry on the path head + formula)")
+    keys = _VALU + ("lds", "vmem")
+    print("   block      kind     valu " + " ".join(f"{k:>9s}" for k in keys))
+    for off, kind, c in cz["blocks"]:
+        v = sum(c.get(k, 0) for k in _VALU)
+        print(f"   +0x{off:<7x} {kind:8s} {v:5d} " + " ".join(f"{c.get(k, 0):9d}" for k in keys))
+    for part in ("head", "formula", "path", "emit"):
+        t = cz[part]
+        print(f"   {part:8s} valu {t['valu']:5d}: " + ", ".join(f"{k} {t[k]}" for k in keys if t.get(k)))
 
 
 def functions(so: str) -> dict[str, list[str]]:
@@ -223,6 +345,8 @@ def main() -> int:
         for b in bad:
             print("   ", b)
         rc |= bool(bad)
+    for name, lines in ks.items():  # the formula's mads: G1 madd 1467; G2 per lane (lane pairs) 2187
+        print_census(name[:60], census(lines, 2187 if "Fq2Pair29" in name else 1467))
     for name, r in resources(so, r"k_msm_(accumulate|stitch|wsum)|k_assemble").items():
         print(name[:60], r)
     for name, lines in functions(so).items():
