@@ -76,6 +76,30 @@ struct PairHost {
   static V mulsum2(const V& a, const V& b, const V& c, const V& d) {
     return {f29_mulsum2(a.l[0], b.l[0], c.l[0], d.l[0]), f29_mulsum2(a.l[1], b.l[1], c.l[1], d.l[1])};
   }
+  struct V2 {
+    V a, b;
+  };
+  // two independent products / product sums (the device policy runs them through f29_mont2)
+  static V2 mul2(const V& a, const V& b, const V& c, const V& d) {
+    V2 r;
+    for (int l = 0; l < 2; l++) {
+      const F29x2 t = f29_mul2(a.l[l], b.l[l], c.l[l], d.l[l]);
+      r.a.l[l] = t.a;
+      r.b.l[l] = t.b;
+    }
+    return r;
+  }
+  static V2 mulsum2x2(const V& a, const V& b, const V& c, const V& d, const V& e, const V& f, const V& g,
+                      const V& h) {
+    V2 r;
+    for (int l = 0; l < 2; l++) {
+      const F29 xa[2] = {a.l[l], c.l[l]}, ya[2] = {b.l[l], d.l[l]}, xb[2] = {e.l[l], g.l[l]}, yb[2] = {f.l[l], h.l[l]};
+      const F29x2 t = f29_mont2<2, 2, false, false>(xa, ya, xb, yb);
+      r.a.l[l] = t.a;
+      r.b.l[l] = t.b;
+    }
+    return r;
+  }
   static V mulsum4(const V (&x)[4], const V (&y)[4]) {
     V r;
     for (int h = 0; h < 2; h++) {

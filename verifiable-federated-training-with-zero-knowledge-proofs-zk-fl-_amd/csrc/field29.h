@@ -821,6 +821,29 @@ ZK_HD typename L::V f2_sqr(const typename L::V& a, const uint32_t (&k)[9]) {
   return L::mul(x, L::sel(a, L::ksub(k, a, pa)));  // lane 1: a1, lane 0: a0 + K - a1
 }
 
+// Two independent Fq2 products a b (k_a) and c d (k_c) side by side (L::mulsum2x2, F29_PAIRED)
+template <class L>
+ZK_HD typename L::V2 f2_mul2(const typename L::V& a, const typename L::V& b, const uint32_t (&ka)[9],
+                             const typename L::V& c, const typename L::V& d, const uint32_t (&kc)[9]) {
+  using V = typename L::V;
+  const V pa = L::swap(a), pc = L::swap(c);
+  const V zero = L::zero();
+  return L::mulsum2x2(a, L::even(b), L::sel(pa, L::ksub(ka, zero, pa)), L::odd(b), c, L::even(d),
+                      L::sel(pc, L::ksub(kc, zero, pc)), L::odd(d));
+}
+
+// Two independent Fq2 squares (f2_sqr each) side by side (L::mul2, F29_PAIRED)
+template <class L>
+ZK_HD typename L::V2 f2_sqr2(const typename L::V& a, const uint32_t (&ka)[9], const typename L::V& c,
+                             const uint32_t (&kc)[9]) {
+  using V = typename L::V;
+  const V pa = L::swap(a), pc = L::swap(c);
+  V x = L::add(pa, L::sel(pa, a)), z = L::add(pc, L::sel(pc, c));
+  L::norm(x);
+  L::norm(z);
+  return L::mul2(x, L::sel(a, L::ksub(ka, a, pa)), z, L::sel(c, L::ksub(kc, c, pc)));
+}
+
 // A B - Y D over Fq2 (a normalized A < kA, Y < kY; B, D normalized): four products per lane
 //   lane 0: A0 B0 + (kA - A1) B1 + (kY - Y0) D0 + Y1 D1
 //   lane 1: A1 B0 + A0 B1 + (kY - Y1) D0 + (kY - Y0) D1
@@ -880,6 +903,29 @@ ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typenam
   using V = typename L::V;
   if (L::is_zero(ax) && L::is_zero(ay)) return p;
   if (L::is_zero(p.ZZ)) return {ax, ay, L::one(), L::one()};
+#if F29_PAIRED
+  // the same products, two independent ones at a time: U2 | S2, PP | RR, PPP | Q, ZZ3 | ZZZ3; the
+  // result returned as one aggregate (see f29_madd_signed)
+  const typename L::V2 us = f2_mul2<L>(ax, p.ZZ, P29::K2_1, ay, p.ZZZ, P29::K2_1);
+  V P = L::ksub(P29::K7_1, us.a, p.X);
+  V R = L::ksub(P29::K7_1, us.b, p.Y);
+  L::norm(P);
+  L::norm(R);
+  const typename L::V2 sq = f2_sqr2<L>(P, P29::K9_1, R, P29::K9_1);
+  if (L::is_zero3(sq.a)) {
+    if (L::is_zero3(sq.b)) return f2_dbl<L>({ax, ay, L::one(), L::one()});
+    return f2_inf<L>();
+  }
+  const V PP = sq.a, RR = sq.b;
+  const typename L::V2 pq = f2_mul2<L>(PP, P, P29::K3_1, PP, p.X, P29::K3_1);
+  const V PPP = pq.a, Q = pq.b;
+  const typename L::V2 zz = f2_mul2<L>(p.ZZ, PP, P29::K3_1, p.ZZZ, PPP, P29::K3_1);
+  V X3 = L::ksub3(P29::K4_3, RR, PPP, Q, Q);
+  L::norm(X3);
+  V QX = L::ksub(P29::K7_1, Q, X3);
+  L::norm(QX);
+  return {X3, f2_mulsub<L>(R, QX, P29::K9_1, p.Y, PPP, P29::K7_1), zz.a, zz.b};
+#else
   const V U2 = f2_mul<L>(ax, p.ZZ, P29::K2_1);
   const V S2 = f2_mul<L>(ay, p.ZZZ, P29::K2_1);
   V P = L::ksub(P29::K7_1, U2, p.X);
@@ -903,6 +949,7 @@ ZK_HD G2P29<L> f2_madd(const G2P29<L>& p, const typename L::V& ax, const typenam
   r.ZZ = f2_mul<L>(p.ZZ, PP, P29::K3_1);
   r.ZZZ = f2_mul<L>(p.ZZZ, PPP, P29::K3_1);
   return r;
+#endif
 }
 
 // add-2008-s.  U1, U2, S1, S2 = (ZZ or ZZZ) (X or Y) < p + (2 + 3) 6.7/169 p = 1.2p;
@@ -989,6 +1036,14 @@ struct Pair29Dev {
   }
   static ZK_DEV V mulsum2(const V& a, const V& b, const V& c, const V& d) { return f29_mulsum2(a, b, c, d); }
   static ZK_DEV V mulsum4(const V (&x)[4], const V (&y)[4]) { return f29_mulsum4(x, y); }
+  using V2 = F29x2;
+  // two independent products / product sums side by side (f29_mont2: one accumulator each, no joins)
+  static ZK_DEV V2 mul2(const V& a, const V& b, const V& c, const V& d) { return f29_mul2(a, b, c, d); }
+  static ZK_DEV V2 mulsum2x2(const V& a, const V& b, const V& c, const V& d, const V& e, const V& f, const V& g,
+                             const V& h) {
+    const F29 xa[2] = {a, c}, ya[2] = {b, d}, xb[2] = {e, g}, yb[2] = {f, h};
+    return f29_mont2<2, 2, false, false>(xa, ya, xb, yb);
+  }
 };
 
 // Compute type of the G2 MSM kernels: Fq2 on lane pairs, 29-bit limbs (storage Affine/XYZZ<Fq2Ops>)

@@ -85,19 +85,22 @@ namespace zkfl {
 // Compute type -> storage: how the point kernels read and write the stored points.  G1 and plain
 // Fq2 hold a point per lane; Fq2PairOps holds it across a lane pair (component h of every
 // coordinate in lane 2k+h), reading and writing Affine/XYZZ<Fq2Ops> memory.
+// PIECES: 16-B LDS-DMA pieces of one lane's share of a base record; REC: Affine<S> slots per stored
+// base record (the record stride of the window table).
 template <class F>
 struct MsmIO {
   using S = F;
   static constexpr int LANES = 1;
+  static constexpr int PIECES = 4, REC = 1;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return p[i]; }
   // the 16-B piece q < 4 of this lane's share of base i, and a share rebuilt from its pieces
   // (G1: the whole 64-B point; the LDS-DMA prefetch of k_msm_accumulate)
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
     return reinterpret_cast<const uint4*>(p + i) + q;
   }
-  static ZK_DEV Affine<F> from_pieces(const uint4 (&u)[4]) {
+  static ZK_DEV Affine<F> from_pieces(const uint32_t (&w)[4 * PIECES]) {
     Affine<F> a;
-    memcpy(&a, u, sizeof(a));
+    memcpy(&a, w, sizeof(a));
     return a;
   }
   static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return p[i]; }
@@ -107,6 +110,7 @@ template <>
 struct MsmIO<Fq2PairOps> {
   using S = Fq2Ops;
   static constexpr int LANES = 2;
+  static constexpr int PIECES = 4, REC = 1;
   static ZK_DEV Affine<Fq2PairOps> ld_aff(const Affine<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
     const uint32_t h = pair_half();
@@ -116,10 +120,13 @@ struct MsmIO<Fq2PairOps> {
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
     return reinterpret_cast<const uint4*>(p + i) + 2 * pair_half() + (q & 1) + (q >> 1) * 4;
   }
-  static ZK_DEV Affine<Fq2PairOps> from_pieces(const uint4 (&u)[4]) {
+  static ZK_DEV Affine<Fq2PairOps> from_pieces(const uint32_t (&w)[4 * PIECES]) {
     Affine<Fq2PairOps> a;
-    memcpy(&a.x, &u[0], 32);
-    memcpy(&a.y, &u[2], 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      a.x.v[k] = w[k];
+      a.y.v[k] = w[8 + k];
+    }
     return a;
   }
   static ZK_DEV XYZZ<Fq2PairOps> ld(const XYZZ<S>* p, size_t i) {
@@ -141,13 +148,14 @@ template <class F>
 struct MsmIOSameLayout {
   using S = FqOps;
   static constexpr int LANES = 1;
+  static constexpr int PIECES = 4, REC = 1;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return reinterpret_cast<const Affine<F>*>(p)[i]; }
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
     return reinterpret_cast<const uint4*>(p + i) + q;
   }
-  static ZK_DEV Affine<F> from_pieces(const uint4 (&u)[4]) {
+  static ZK_DEV Affine<F> from_pieces(const uint32_t (&w)[4 * PIECES]) {
     Affine<F> a;
-    memcpy(&a, u, sizeof(a));
+    memcpy(&a, w, sizeof(a));
     return a;
   }
   static ZK_DEV XYZZ<F> ld(const XYZZ<S>* p, size_t i) { return reinterpret_cast<const XYZZ<F>*>(p)[i]; }
@@ -159,21 +167,51 @@ template <>
 struct MsmIO<FqOpsLazy> : MsmIOSameLayout<FqOpsLazy> {};
 // G1 in 29-bit limbs (field29.h): the same 8 x 32-bit storage, converted on every load / store
 // (stored values < 2^256, in the 2^261 Montgomery domain)
+// (MSM_G1_PACKED: the bases as 128-B records of x, y in nine 29-bit limbs each, k_msm_pack29)
 template <>
 struct MsmIO<FqOps29> {
   using S = FqOps;
   static constexpr int LANES = 1;
+  static constexpr int PIECES = MSM_G1_PACKED ? 5 : 4, REC = MSM_G1_PACKED ? 2 : 1;
   static ZK_DEV Affine<FqOps29> ld_aff(const Affine<S>* p, size_t i) {
+#if MSM_G1_PACKED
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p + REC * i);
+    Affine<FqOps29> a;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      a.x.v[k] = w[k];
+      a.y.v[k] = w[9 + k];
+    }
+    return a;
+#else
     const Affine<S> a = p[i];
     return {f29_pack(a.x.v), f29_pack(a.y.v)};
+#endif
   }
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
-    return reinterpret_cast<const uint4*>(p + i) + q;
+    return reinterpret_cast<const uint4*>(p + REC * i) + q;
   }
-  static ZK_DEV Affine<FqOps29> from_pieces(const uint4 (&u)[4]) {
-    Affine<S> a;
-    memcpy(&a, u, sizeof(a));
-    return {f29_pack(a.x.v), f29_pack(a.y.v)};
+  // the record's words as read from LDS (word by word: a memcpy through HIP's uint4 was lowered to
+  // byte permutes, ~45 VALU instructions per entry)
+  static ZK_DEV Affine<FqOps29> from_pieces(const uint32_t (&w)[4 * PIECES]) {
+    Affine<FqOps29> a;
+#if MSM_G1_PACKED
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      a.x.v[k] = w[k];
+      a.y.v[k] = w[9 + k];
+    }
+#else
+    uint32_t x[8], y[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      x[k] = w[k];
+      y[k] = w[8 + k];
+    }
+    a.x = f29_pack(x);
+    a.y = f29_pack(y);
+#endif
+    return a;
   }
   static ZK_DEV XYZZ<FqOps29> ld(const XYZZ<S>* p, size_t i) {
     const XYZZ<S> a = p[i];
@@ -198,6 +236,7 @@ template <>
 struct MsmIO<Fq2Pair29> {
   using S = Fq2Ops;
   static constexpr int LANES = 2;
+  static constexpr int PIECES = 4, REC = 1;
   static ZK_DEV Affine<Fq2Pair29> ld_aff(const Affine<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
     const uint32_t h = pair_half();
@@ -206,11 +245,14 @@ struct MsmIO<Fq2Pair29> {
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
     return reinterpret_cast<const uint4*>(p + i) + 2 * pair_half() + (q & 1) + (q >> 1) * 4;
   }
-  static ZK_DEV Affine<Fq2Pair29> from_pieces(const uint4 (&u)[4]) {
-    Fq x, y;
-    memcpy(&x, &u[0], 32);
-    memcpy(&y, &u[2], 32);
-    return {f29_pack(x.v), f29_pack(y.v)};
+  static ZK_DEV Affine<Fq2Pair29> from_pieces(const uint32_t (&w)[4 * PIECES]) {
+    uint32_t x[8], y[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      x[k] = w[k];
+      y[k] = w[8 + k];
+    }
+    return {f29_pack(x), f29_pack(y)};
   }
   static ZK_DEV XYZZ<Fq2Pair29> ld(const XYZZ<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
@@ -250,6 +292,29 @@ static __global__ void __launch_bounds__(256) k_msm_to_m29(Fq* __restrict__ a, s
 #pragma unroll
   for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
   a[i] = fp_mul(a[i], c);
+}
+// MSM_G1_PACKED: n expanded G1 bases (64-B records, 2^256 domain) -> 128-B records of x, y in nine
+// 29-bit limbs each, 2^261 domain (the layout MsmIO<FqOps29> reads), words 18..31 zero
+static __global__ void __launch_bounds__(256) k_msm_pack29(const Affine<FqOps>* __restrict__ in, size_t n,
+                                                          uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fq c;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
+  const Affine<FqOps> a = in[i];
+  const F29 x = f29_pack(fp_mul(a.x, c).v), y = f29_pack(fp_mul(a.y, c).v);
+  uint32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    w[k] = x.v[k];
+    w[9 + k] = y.v[k];
+  }
+#pragma unroll
+  for (int k = 18; k < 32; k++) w[k] = 0;
+  uint4* o = reinterpret_cast<uint4*>(out + 32 * i);
+#pragma unroll
+  for (int q = 0; q < 8; q++) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 // MSM_G2_F29 (default): lane pairs in 29-bit limbs (Fq2Pair29); 0: 32-bit limbs (Fq2PairOps).
 #ifndef MSM_G2_F29
@@ -621,11 +686,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   // native 4 x u32 vector type: with HIP's uint4 struct the reads below were lowered to 32
   // ds_read_u16 plus ~100 byte-reassembly instructions per entry (gfx950, ROCm 7.2)
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  __shared__ v4u pf[2][4][64];
+  constexpr int NP = IO::PIECES;
+  __shared__ v4u pf[2][NP][64];
   const uint32_t ln = threadIdx.x;
   auto fetch = [&](uint32_t idx, int b) {
 #pragma unroll
-    for (int q = 0; q < 4; q++)
+    for (int q = 0; q < NP; q++)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)IO::piece(bases, idx, q),
                                        (__attribute__((address_space(3))) void*)&pf[b][q][0], 16, 0, 0);
   };
@@ -641,11 +707,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
     // longer connects these reads to the global_load_lds writes and dropped the vmcnt wait on the
     // first iteration (wrong first base, found by the GPU proof tests) -- so wait explicitly
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint4 u[4];
+    uint32_t u[4 * NP];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {  // ds_read_b128
+    for (int q = 0; q < NP; q++) {  // ds_read_b128
       const v4u x = pf[b][q][ln];
-      u[q] = make_uint4(x.x, x.y, x.z, x.w);
+      u[4 * q] = x.x;
+      u[4 * q + 1] = x.y;
+      u[4 * q + 2] = x.z;
+      u[4 * q + 3] = x.w;
     }
     const Affine<F> a = IO::from_pieces(u);
     if (p + 1 < p1) fetch(v1 & 0x7FFFFFFFu, b ^ 1);
@@ -915,7 +984,8 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
 template <class F>
 hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n) {
   b.n = n;
-  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * MSM_W * sizeof(Affine<F>)));
+  using IO = MsmIO<typename MsmCompute<F>::type>;
+  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * MSM_W * IO::REC * sizeof(Affine<F>)));
   return hipSuccess;
 }
 
@@ -937,8 +1007,19 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
     ZK_CHECK(hipMalloc(&b.sidx, b.n * sizeof(uint32_t)));
     ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
-  if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
   using FC = typename MsmCompute<F>::type;
+  if constexpr (MsmIO<FC>::REC == 2) {  // MSM_G1_PACKED: expand into a temporary table, then pack
+    const size_t m = b.n * MSM_W;
+    if (!m) return hipGetLastError();
+    Affine<F>* tmp = nullptr;
+    ZK_CHECK(hipMallocAsync(reinterpret_cast<void**>(&tmp), m * sizeof(Affine<F>), st));
+    hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, tmp);
+    hipLaunchKernelGGL(k_msm_pack29, dim3(zk_grid(m, 256)), dim3(256), 0, st, tmp, m,
+                       reinterpret_cast<uint32_t*>(b.bases_w));
+    ZK_CHECK(hipFreeAsync(tmp, st));
+    return hipGetLastError();
+  }
+  if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
   if constexpr (std::is_same<FC, FqOps29>::value || std::is_same<FC, Fq2Pair29>::value) {
     const size_t nfq = b.n * MSM_W * (sizeof(Affine<F>) / sizeof(Fq));
     if (nfq)

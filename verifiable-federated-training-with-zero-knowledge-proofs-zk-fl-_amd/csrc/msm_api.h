@@ -55,9 +55,18 @@ static_assert(!MSM_SORT_ROCPRIM || MSM_C <= 16, "rocPRIM digit sort: c <= 16");
 // XYZZ only.  Measured on MI355X: correct (50 GPU parity tests, metric-size proofs equal the C
 // oracle) but 347 vs 421 proofs/s -- 2,818 VALU instructions per entry against 2,509 for the XYZZ
 // kernel (profiles/r03_affine_v2_kernels_counters.txt)
+// 1: G1 expanded bases stored pre-packed for the 29-bit engine -- x and y as nine 29-bit limbs in
+// the 2^261 Montgomery domain (72 B) padded to a 128-B record, one L2 line per base, fetched as
+// five 16-B LDS-DMA pieces -- so the accumulation does no 8 x 32 -> 9 x 29 repacking per entry.
+// A 64-B record already costs a whole 128-B line per gather: twice the HBM
+// footprint of the window table, the same HBM traffic.  0: 64-B records in 8 x 32-bit limbs.
+#ifndef MSM_G1_PACKED
+#define MSM_G1_PACKED 0
+#endif
 #ifndef MSM_G1_AFFINE
 #define MSM_G1_AFFINE 0
 #endif
+static_assert(!(MSM_G1_PACKED && MSM_G1_AFFINE), "the batch-affine rounds read 64-B base records");
 #ifndef MSM_G1_L
 #if MSM_G1_AFFINE
 #define MSM_G1_L 32
