@@ -365,6 +365,31 @@ def test_resident_batch_and_errors(gpu_ctx):
     key.close()
 
 
+def test_batch_equals_single_proofs(gpu_ctx):
+    """A 12-proof batch of a small key over 3 slots (the one-stream chain, every slot's later proofs
+    graph-replayed; with ZKFL_FOLD=1 the folded s pi_A + r pi_B1 MSM, zkfl_key::bRS) must equal the
+    same proofs taken alone (the latency schedule, the GLV scalar multiplications) byte for byte,
+    and one of them the oracle's."""
+    from zkfl import clients, native, zkey
+    b, zk = _setup(gpu_ctx, "balance_unified", 8, 3, 4)
+    key = native.ProvingKey(gpu_ctx, zk)
+    wt = []
+    for cid in (1, 2, 3, 4):
+        c = clients.Client(cid, 8, 4, 3, clients.JsLcg(777 + cid))
+        wt.append(zkey.wtns_bytes(ow.evaluate(b, c.balance_input())))
+    ws = [key.upload(x) for x in wt]
+    order = [i % 4 for i in range(12)]
+    rs = b"".join(_le(1000 + 7 * j) + _le(2000 + 11 * j) for j in range(12))
+    batch = key.prove_batch([ws[i] for i in order], rs)
+    for j, i in enumerate(order):
+        assert batch[j] == key.prove(wt[i], rs[64 * j:64 * j + 64])[0], j
+    z = og.parse_zkey(zk)
+    assert batch[5] == og.proof_bytes(og.prove(z, zkey.read_wtns(wt[order[5]]), r=1000 + 35, s=2000 + 55))
+    for w in ws:
+        w.close()
+    key.close()
+
+
 def test_node_snarkjs_cli_prove(gpu_ctx, tmp_path):
     """`node snarkjs_shim.js groth16 prove zkey wtns proof.json public.json` — the reference's
     execSync line (tests/full_system_simulation.mjs:773-776) through N-API -> C ABI -> HIP."""

@@ -18,10 +18,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=16)
     ap.add_argument("--slots", type=int, default=8)
+    ap.add_argument("--weak", type=int, default=0, help="also the weak leg with this many rounds (as bench.py)")
+    ap.add_argument("--repeat", type=int, default=1, help="run the leg(s) this many times in one process")
     args = ap.parse_args()
     from zkfl import native
     ctx = native.Context(0)
-    s, _ = bench.c5_leg(ctx, 0, 1, args.rounds, args.slots, None, 0)
+    for it in range(args.repeat):
+        s, w = bench.c5_leg(ctx, 0, 1, args.rounds, args.slots, None, args.weak)
+        if w is not None or args.repeat > 1:
+            for tag, x in (("strong", s), ("weak", w)):
+                if x is not None:
+                    print(f"  pass {it} {tag}: {x['value']:.2f} proofs/s, host CPU {x['host_cpu_ms_per_proof']} ms "
+                          f"per proof, {x['host_cpu_cores_busy']} cores busy", flush=True)
     print(f"{os.environ.get('ZKFL_LIB', 'in-tree')}: {s['value']:.2f} proofs/s (host CPU "
           f"{s['host_cpu_ms_per_proof']} ms per proof, {s['host_cpu_cores_busy']} cores busy)", flush=True)
 

@@ -212,14 +212,15 @@ _VALU = tuple(n for n, _ in _CLASSES) + ("valu_other",)
 
 
 def census(lines: list[str], formula_mads: int) -> dict:
-    """Instruction census of an accumulation kernel's main loop (the innermost back edge whose
-    blocks hold the most v_mad_u64_u32).  formula_mads: the mads of one point addition as written (G1 madd:
-    6 products x 162 + 2 squares x 126 + the Y3 product sum 243 = 1467); the loop blocks with mads
+    """Instruction census of an accumulation kernel's main loop (the innermost loop that holds the
+    point formula).  formula_mads: the mads of one point addition as written (G1 madd:
+    6 products x 162 + 2 squares x 126 + the Y3 product sum 243 = 1467); the loop's blocks with mads
     whose counts sum to exactly that are the formula's ("formula"), other blocks with mads are the
     special cases (P == 0: the doubling, "cold"), blocks with a global store are the run ends
-    ("emit": executed when any lane of the wave closes a bucket run), mad-free blocks before the
-    first formula block are the loop head ("head": key / index loads, the LDS read of the
-    prefetched base and its 8 x 32 -> 9 x 29 repacking, the zero tests), the rest "other".  The
+    ("emit": executed when any lane of the wave closes a bucket run), mad-free blocks on every path
+    from the loop header to the formula are the loop head ("head": key / index loads, the LDS read
+    of the prefetched base and its 8 x 32 -> 9 x 29 repacking, the zero tests), the rest "other"
+    (the run ends' bookkeeping, the latch).  The
     per-entry path is head + formula."""
     import itertools
     ins, blocks, succs = _cfg(lines)
@@ -231,27 +232,54 @@ def census(lines: list[str], formula_mads: int) -> dict:
             c[k] = c.get(k, 0) + 1
         c["stores"] = sum(1 for i in range(s, e) if ins[i][1].startswith(("global_store", "buffer_store")))
         cnt.append(c)
-    # the main loop: the back edge whose block range holds the most mads
+    # the main loop: the innermost back edge whose blocks contain the formula (a subset of its
+    # blocks with mads summing to formula_mads exactly)
+    def formula_in(blks):
+        withmad = [j for j in blks if cnt[j].get("mad64", 0)]
+        for r in range(1, len(withmad) + 1):
+            for comb in itertools.combinations(withmad, r):
+                if sum(cnt[j]["mad64"] for j in comb) == formula_mads:
+                    return list(comb)
+        return None
+    preds: list[list[int]] = [[] for _ in blocks]
+    for k, ss in enumerate(succs):
+        for t in ss:
+            preds[t].append(k)
+
+    def natural_loop(t, k):  # the header t and every block that reaches the latch k without passing t
+        body, work = {t, k}, [k]
+        while work:
+            x = work.pop()
+            for p in preds[x]:
+                if p not in body:
+                    body.add(p)
+                    work.append(p)
+        return sorted(body)
+    # dominators (iterative): an edge k -> t is a back edge when t dominates k (the compiler may
+    # place a loop's latch before its header, so address order does not tell)
+    nb = len(blocks)
+    dom = [set(range(nb)) for _ in range(nb)]
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for x in range(1, nb):
+            ps = [dom[p] for p in preds[x]]
+            d = (set.intersection(*ps) if ps else set()) | {x}
+            if d != dom[x]:
+                dom[x], changed = d, True
     best = None
     for k, ss in enumerate(succs):
         for t in ss:
-            if t <= k:
-                m = sum(cnt[j].get("mad64", 0) for j in range(t, k + 1))
-                if best is None or (m, t - k) > (best[0], best[1] - best[2]):  # most mads, then innermost
-                    best = (m, t, k)
-    assert best, "no loop"
-    _, lo, hi = best
-    loop = list(range(lo, hi + 1))
-    withmad = [j for j in loop if cnt[j].get("mad64", 0)]
-    formula = None
-    for r in range(1, len(withmad) + 1):
-        for comb in itertools.combinations(withmad, r):
-            if sum(cnt[j]["mad64"] for j in comb) == formula_mads:
-                formula = list(comb)
-                break
-        if formula:
-            break
-    assert formula, f"no loop blocks hold exactly {formula_mads} mads: {[cnt[j].get('mad64') for j in withmad]}"
+            if t in dom[k]:
+                body = natural_loop(t, k)
+                if best is None or len(body) < len(best[0]):
+                    f = formula_in(body)
+                    if f:
+                        best = (body, f)
+    assert best, f"no loop holds {formula_mads} mads in a subset of its blocks"
+    loop, formula = best
+    header = next(t for t in loop if all(t in dom[j] for j in loop))
     first = min(formula)
     rows = []
     for j in loop:
@@ -262,7 +290,7 @@ def census(lines: list[str], formula_mads: int) -> dict:
             kind = "cold"
         elif c["stores"]:
             kind = "emit"
-        elif j < first:
+        elif j in dom[first]:  # on every path from the loop header to the formula
             kind = "head"
         else:
             kind = "other"

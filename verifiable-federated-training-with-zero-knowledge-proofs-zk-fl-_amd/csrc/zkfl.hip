@@ -627,6 +627,37 @@ __global__ void __launch_bounds__(128) k_assemble_c(const G1P* __restrict__ res,
   }
 }
 
+// Folded keys (key_folds_rs): the scalars of the s pi_A + r pi_B1 MSM over bRS -- element i of the
+// witness-and-extras vector x = (w_0 .. w_{nVars-1}, 1, r, s, -rs) times s, then times r:
+// sw[i] = s x_i, sw[nVars + 4 + i] = r x_i (standard form, as the witness)
+__global__ void __launch_bounds__(256) k_rs_scale(const Fr* __restrict__ w, const Fr* __restrict__ extra, uint32_t nV,
+                                                  Fr* __restrict__ sw) {
+  ZK_WT(WT_SET_EXTRA);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, total = nV + 4;
+  if (i >= total) return;
+  const Fr x = fp_to_mont(i < nV ? w[i] : extra[i - nV]);  // x R
+  sw[i] = fp_mul(x, extra[2]);                              // x R s / R = x s
+  sw[total + i] = fp_mul(x, extra[1]);
+}
+
+// The assembly of a folded key: res[3] = s pi_A + r pi_B1 (the bRS MSM), so pi_c = C' + H + res[3]
+// needs one addition and its affine conversion; pi_a and pi_b are converted beside it.
+__global__ void __launch_bounds__(192) k_assemble_f(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                    uint32_t* __restrict__ proof) {
+  ZK_WT(WT_ASSEMBLE);
+  ZK_LIGHT();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 2, q = lane & 3;
+  if (wave == 0 && g == 0) {
+    const G1Q C = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
+  } else if (wave == 2 && lane == 0) {
+    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
+  }
+}
+
 // Parts of a split proof (zkfl_groth16_prove_part_batch / zkfl_groth16_assemble): a shard's MSM
 // results as XYZZ points, every coordinate in standard form (so the parts cross process boundaries
 // in a defined encoding without an inversion per point): A' (32 words) | B1' (32) | B2' (64: each
@@ -811,6 +842,7 @@ struct ProofSlot {
   MsmScratch<Fq2Ops> g2s;
   MsmTail<Fq2Ops> g2t;
   Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs (= h + n: the extra slots follow h)
+  Fr* sw = nullptr;     // folded keys: [2 (nVars + 4)] scalars s w | s extra | r w | r extra (k_rs_scale)
   Fr* abc = nullptr;  // [3n]
   Fr* abc_head = nullptr;  // [ceil(K / ABC_L)] ABC segmented-sum partials
   Fr* abc_tail = nullptr;
@@ -878,6 +910,11 @@ struct zkfl_key {
   // the extra pointer = the slot's h vector, whose extra slots 1, r, s, -rs follow it).  bC / bH
   // stay for the parity hook (zkfl_debug_prove_parts returns C and H apart).
   MsmBases<FqOps> bCH;
+  // Small keys (key_folds_rs): s pi_A + r pi_B1 as ONE more MSM instead of the assembly's GLV scalar
+  // multiplications -- A's bases (with alpha1, delta1) then B1's (beta1, delta1), scalars s w | r w
+  // (k_rs_scale): sum = s (alpha + sum w A + r delta) + r (beta + sum w B1 + s delta).
+  MsmBases<FqOps> bRS;
+  bool fold = false;
   // the parity hook's zeros (zkfl_debug_prove_parts, first call): with C and H merged it runs the
   // C + H MSM twice, once with a zero h (C alone) and once with a zero witness (H alone), so the key
   // holds no separate C and H bases (they were ~0.5 GB of expanded bases per key at 2^18)
@@ -927,7 +964,7 @@ void slot_release(ProofSlot* s) {
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
   void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_parts,
-                  s->w_stage};  // extra lives in h
+                  s->w_stage, s->sw};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -975,7 +1012,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ProofSlot* s = new ProofSlot();
   *out = s;
   const size_t nV = k->nVars, n = k->n;
-  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n, k->bCH.n});
+  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n, k->bCH.n, k->bRS.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
   // One stream per slot by default: a slot's proof is a serial chain and throughput comes from
@@ -993,8 +1030,10 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * MSM_W * sizeof(uint32_t), st));
   }
 #endif
-  // tail 3 is H's; with C and H merged only the parity hook uses it, for the C + H MSM
-  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), std::max(k->bH.n, k->bCH.n)};
+  // tail 3 is H's; with C and H merged the parity hook uses it for the C + H MSM, a folded key
+  // for s pi_A + r pi_B1
+  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n),
+                          std::max({k->bH.n, k->bCH.n, k->bRS.n})};
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
@@ -1004,6 +1043,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     s->nnz_alias = true;
   }
   if (graph_mode()) ZK_CHECK(hipMalloc(&s->w_stage, nV * 32));
+  if (k->fold) ZK_CHECK(hipMalloc(&s->sw, 2 * (nV + 4) * 32));
   ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
   s->extra = s->h + n;
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
@@ -1114,6 +1154,7 @@ void key_release(zkfl_key* k) {
   msm_bases_free_g1(k->bC);
   msm_bases_free_g1(k->bH);
   msm_bases_free_g1(k->bCH);
+  msm_bases_free_g1(k->bRS);
   msm_bases_free_g2(k->bB2);
   if (k->dbg_zero) (void)hipFree(k->dbg_zero);
   ntt_plan_free(k->ntt);
@@ -1190,6 +1231,19 @@ bool lowlat_fast_wsum() {
 // shorter-chain reduction in batches too: their proofs are chains of small latency-bound kernels
 // that leave most of the GPU idle (config-5 wave trace: SIMD share 0.135 with a wave resident 99%
 // of the time), so the reduction's extra waves are free and its shorter chain is not.
+// ZKFL_FOLD=1 (an A/B knob, off): small keys (domain <= 2^ZKFL_FOLD_LOGN, default 2^16) fold the
+// assembly's scalar multiplications s pi_A + r pi_B1 into one more MSM (zkfl_key::bRS): k_assemble's
+// four 128-bit GLV multiplications in one wave are ~0.8 ms of a small proof's ~3.4 ms of kernels,
+// the extra MSM (A's and B1's bases, 2 x nVars scalars) a sort, an accumulation and a fourth tail.
+// Bit-exact, but config 5 measured 2,095 vs 2,165 proofs/s without it (3 same-box alternations,
+// profiles/r05_ab_c5_fold_wait.log): under 16 proofs in flight the assembly overlaps other chains,
+// the extra launches and tail work do not.
+bool key_folds_rs(int logn, uint32_t nshards) {
+  static const int on = getenv("ZKFL_FOLD") ? atoi(getenv("ZKFL_FOLD")) : 0;
+  static const int lim = getenv("ZKFL_FOLD_LOGN") ? atoi(getenv("ZKFL_FOLD_LOGN")) : 16;
+  return on && MSM_MERGE_CH && nshards == 1 && logn <= lim;
+}
+
 bool small_key_fast_wsum(const zkfl_key* k) {
   static const int logn = getenv("ZKFL_FAST_WSUM_LOGN") ? atoi(getenv("ZKFL_FAST_WSUM_LOGN")) : 16;
   return lowlat_fast_wsum() && k->logn <= logn;
@@ -1410,11 +1464,13 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   int pp = prof->begin("prove", st);
   const bool lowlat_path =
       lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT;
+  // a folded key's s pi_A + r pi_B1 MSM (tail 3, res[3]) instead of the assembly's scalar multiplications
+  const bool fold = k->fold && !lowlat_path && MSM_MERGE_CH && plain == 0 && s->sw;
   {
     // the tails this chain accumulates into: G1 A, B1, C (+ H), [H]; G2 B2 when it shares B1's sort
     // on this stream (a separate G2 stream's msm_run empties its own).  The condition is the body's
     // `share` below: a slot with a second stream under serialized profiling shares too.
-    const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1) ? 3 : 4;
+    const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1 && !fold) ? 3 : 4;
     const bool g2 = lowlat_path || (k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32));
     ProofStart ps = {};
     auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
@@ -1426,7 +1482,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     };
     for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, MSM_NB * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
     if (g2) add(s->g2t.buckets, MSM_NB * sizeof(G2P), s->g2t.nnz, s->g2t.live);
-    uint32_t* res3 = MSM_MERGE_CH && plain != 1 ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
+    uint32_t* res3 = MSM_MERGE_CH && plain != 1 && !fold ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
     if (s->w_stage && d_w == s->w_stage) {  // graph replay (enqueue_proof): stage the witness here
       ps.w_src_host = reinterpret_cast<const uint64_t*>(s->pinned + W_PTR_OFF);
       ps.w_dst = reinterpret_cast<uint4*>(s->w_stage);
@@ -1452,7 +1508,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   const bool split_ch = MSM_MERGE_CH && plain == 1;
   if (split_ch && !k->dbg_zero) return fail(ZKFL_E_ARG, "parity hook: zeros not allocated");
   const uint32_t* Z = (const uint32_t*)k->dbg_zero;
-  const int ntails = merge ? 3 : 4;
+  const int ntails = merge && !fold ? 3 : 4;
   // Stage order.  Every slot runs the same chain, so under load the slots move as a convoy: the
   // accumulations fill the GPU one at a time, and the slots that leave them together reach ABC +
   // NTT together -- the wave timeline (tools/wtrace.py) showed stretches of ~4 ms with no
@@ -1480,6 +1536,12 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   if (light_first) {
     const int rc = abc_ntt();
     if (rc) return rc;
+  }
+  if (fold) {
+    const uint32_t nV4 = k->nVars + 4;
+    hipLaunchKernelGGL(k_rs_scale, dim3((nV4 + 255) / 256), dim3(256), 0, st, d_w, s->extra, k->nVars, s->sw);
+    HIP_TRY(msm_accumulate_g1(k->bRS, sA, s->g1t[3], (const uint32_t*)s->sw, nullptr, st, prof, "msm_accumulate_g1"),
+            "msm rs");
   }
   HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   if (share) {
@@ -1526,8 +1588,12 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
-    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
-                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
+    if (fold)
+      hipLaunchKernelGGL(k_assemble_f, dim3(1), dim3(192), 0, st, s->res, s->resB2, proof_out(s));
+    else
+      hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
+                         reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64),
+                         proof_out(s));
     prof->end(pa, st, 1.0);
   }
   prof->end(pp, st, 1.0);
@@ -1602,8 +1668,25 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
   return ZKFL_OK;
 }
 
-int wait_slot(ProofSlot* s) {
-  HIP_TRY(hipEventSynchronize(s->ev_done), "sync");
+// Host wait for a device event.  hipEventSynchronize on these (non-blocking-sync) events spins a
+// host core for the whole wait: it was most of config 5's host CPU per proof (0.55-0.57 ms, 1.2
+// cores busy at ~2,100 proofs/s).  A batch (poll = true) polls instead, sleeping ZKFL_WAIT_US
+// (default 50) microseconds between queries: 0.13-0.16 ms per proof, 0.3 cores, throughput within
+// the spread (2,091 vs 2,095 proofs/s, 3 same-box alternations, profiles/r05_ab_c5_fold_wait.log);
+// the scheduler refills a freed slot up to that much later, ~0.1% of an M step.  A proof alone (the
+// latency path) keeps the spin.  ZKFL_WAIT_US=0 spins everywhere.
+static hipError_t host_wait(hipEvent_t ev, bool poll) {
+  static const int us = getenv("ZKFL_WAIT_US") ? atoi(getenv("ZKFL_WAIT_US")) : 50;
+  if (us <= 0 || !poll) return hipEventSynchronize(ev);
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+  }
+}
+
+int wait_slot(ProofSlot* s, bool poll = false) {
+  HIP_TRY(host_wait(s->ev_done, poll), "sync");
   if (s->out_proof) memcpy(s->out_proof, s->pinned, 256);
   if (s->out_part) memcpy(s->out_part, s->pinned + 512, PART_WORDS * 4);
   s->busy = false;
@@ -1650,7 +1733,7 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     rc = get_slot(J.key, cursor[c].second++, &s);
     if (rc) break;
     if (s->busy) {
-      rc = wait_slot(s);
+      rc = wait_slot(s, n > 1);
       if (rc) break;
     }
     s->job = i;
@@ -1673,7 +1756,7 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
   for (auto& kc : cursor)
     for (ProofSlot* s : kc.first->slots)
       if (s->busy) {
-        int r2 = wait_slot(s);
+        int r2 = wait_slot(s, n > 1);
         if (rc == ZKFL_OK) rc = r2;
       }
   return rc;
@@ -1991,6 +2074,7 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
   k->nPub = nPub;
   k->n = dom;
   k->logn = logn;
+  k->fold = key_folds_rs(logn, nshards);
   k->nC = nC;
   k->K = ncoef;
   k->shard = shard;
@@ -2086,7 +2170,7 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
       o.sidx.swap(c.sidx);
       o.sidx.insert(o.sidx.end(), h.sidx.begin(), h.sidx.end());
     };
-    enum { QA, QB1, QB2, QC, QH, QCH, NQ };
+    enum { QA, QB1, QB2, QC, QH, QCH, QRS, NQ };
     std::vector<Img> im(NQ);
     {
       std::vector<std::thread> th;
@@ -2101,6 +2185,13 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
         th.emplace_back([&] { image(im[QH], 64, z.secH, dom, 0, {}, h_identity); });
       }
       for (auto& t : th) t.join();
+    }
+    if (k->fold) {  // s pi_A + r pi_B1: A's image then B1's, B1's scalars behind the first nVars + 4
+      Img& o = im[QRS];
+      o.img = im[QA].img;
+      o.img.insert(o.img.end(), im[QB1].img.begin(), im[QB1].img.end());
+      o.sidx = im[QA].sidx;
+      for (uint32_t x : im[QB1].sidx) o.sidx.push_back(x + X + 4);
     }
     mark("bases_host");
     std::vector<void*> d_imgs;
@@ -2122,6 +2213,8 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && im[QB1].sidx == im[QB2].sidx && !im[QB1].sidx.empty();
     if (e == hipSuccess && MSM_MERGE_CH) e = upload(k->bCH, im[QCH], false, X);
+    // every index of the folded map addresses the scalar vector sw itself (no extra slots)
+    if (e == hipSuccess && k->fold) e = upload(k->bRS, im[QRS], false, 2 * (X + 4));
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bC, im[QC], false, X);
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bH, im[QH], h_identity, 0xFFFFFFFFu);
     const hipError_t es = hipStreamSynchronize(st);
@@ -2477,7 +2570,7 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
     WitPipe::Set& b = P->set[g % 3];
     const size_t l0 = g * pk.G, m = std::min(pk.G, pk.jobs.size() - l0), nw = pk.key->nVars;
     const size_t npub = pk.key->nPub;
-    HIP_TRY(hipEventSynchronize(b.ev), "witness set reuse");  // its group of 3 groups ago
+    HIP_TRY(host_wait(b.ev, true), "witness set reuse");  // its group of 3 groups ago
     for (size_t j = 0; j < m; j++) {
       const uint8_t* in = nullptr;
       int r = get_input(pk.jobs[l0 + j], &in);
