@@ -365,12 +365,15 @@ def test_resident_batch_and_errors(gpu_ctx):
     key.close()
 
 
-def test_batch_equals_single_proofs(gpu_ctx):
+@pytest.mark.parametrize("pairs", ["0", "1"])
+def test_batch_equals_single_proofs(gpu_ctx, monkeypatch, pairs):
     """A 12-proof batch of a small key over 3 slots (the one-stream chain, every slot's later proofs
-    graph-replayed; with ZKFL_FOLD=1 the folded s pi_A + r pi_B1 MSM, zkfl_key::bRS) must equal the
-    same proofs taken alone (the latency schedule, the GLV scalar multiplications) byte for byte,
-    and one of them the oracle's."""
+    graph-replayed; with ZKFL_FOLD=1 the folded s pi_A + r pi_B1 MSM, zkfl_key::bRS; with
+    ZKFL_PAIRS=1 two proofs per chain, ProofPair: pair sorts over 2 NB bucket keys, per-half
+    reductions) must equal the same proofs taken alone (the latency schedule, the GLV scalar
+    multiplications) byte for byte, and one of them the oracle's."""
     from zkfl import clients, native, zkey
+    monkeypatch.setenv("ZKFL_PAIRS", pairs)
     b, zk = _setup(gpu_ctx, "balance_unified", 8, 3, 4)
     key = native.ProvingKey(gpu_ctx, zk)
     wt = []

@@ -435,9 +435,15 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
 // Zero digits are dropped (the accumulation reads only the first nnz pairs).  The order inside
 // a bucket is arbitrary: a bucket's sum does not depend on it, and the proof is affine.
 // ---------------------------------------------------------------------------
+// Proof pairs (P = 2, small keys: msm_sort_pair): the digits of two proofs' scalars over the same
+// bases sort as ONE problem with 2 NB bucket keys, proof p's buckets at p NB ("virtual bases"
+// i + p n); the accumulation and stitching run unchanged over the doubled key range and the bucket
+// reduction takes each half apart (msm_tails_pair).  The high bins stay MSM_SORT_HB: a pair sorts
+// one more low bit inside each (MSM_SORT_LB + 1).
 constexpr int MSM_SORT_T = 256;           // threads per block in count / scatter
 constexpr int MSM_SORT_LB = MSM_SORT_LOW_BITS;       // key bits sorted inside a high bin
 constexpr int MSM_SORT_NL = 1 << MSM_SORT_LB;        // low counters per high-bin workgroup
+static_assert(MSM_C <= 16, "proof pairs: 2 NB bucket keys in a u16");
 constexpr int MSM_SORT_HB = MSM_NB >> MSM_SORT_LB;   // high bins
 constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
 static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 512 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
@@ -446,10 +452,22 @@ constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin wor
 static_assert(MSM_SORT_BINT >= MSM_SORT_NL && MSM_SORT_BINT <= 1024, "bins: one thread per low counter");
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
-// Signed digits of base i's scalar: fn(key, val) for every non-zero digit (as k_msm_digits).
-template <class Fn>
-ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra,
-                           const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t i, Fn&& fn) {
+// The scalars of one sort: proof p's scalar vector and extra slots (p < P)
+struct MsmScalars {
+  const uint32_t* sc[2];
+  const uint32_t* ex[2];
+};
+
+// Signed digits of virtual base v (base i = v mod n of proof p = v / n): fn(key, val) for every
+// non-zero digit, key = bucket + p NB (as k_msm_digits for P = 1).
+template <int P, class Fn>
+ZK_DEV void msm_for_digits(const MsmScalars& S, const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t n,
+                           size_t v, Fn&& fn) {
+  const uint32_t p = P > 1 && v >= n ? 1u : 0u;
+  const size_t i = v - p * n;
+  const uint32_t* __restrict__ scalars = P > 1 && p ? S.sc[1] : S.sc[0];
+  const uint32_t* __restrict__ extra = P > 1 && p ? S.ex[1] : S.ex[0];
+  const uint32_t koff = p * MSM_NB;
   const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
   const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
   const uint4* sp = reinterpret_cast<const uint4*>(src);
@@ -464,24 +482,25 @@ ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t*
     if (carry) d -= (1 << MSM_C);
     if (d != 0) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      fn(mag - 1, (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u));
+      fn(koff + mag - 1, (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u));
     }
   }
 }
 
-static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint32_t* __restrict__ scalars,
-                                                                   const uint32_t* __restrict__ extra,
-                                                                   const uint32_t* __restrict__ sidx,
-                                                                   uint32_t extra_start, size_t n, size_t per_blk,
-                                                                   uint32_t* __restrict__ cnt) {
+// n: bases per proof; the blocks cover the P n virtual bases
+template <int P>
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const MsmScalars S, const uint32_t* __restrict__ sidx,
+                                                            uint32_t extra_start, size_t n, size_t per_blk,
+                                                            uint32_t* __restrict__ cnt) {
   ZK_WT(WT_SORT_COUNT);
   ZK_LIGHT();
+  constexpr int LB = MSM_SORT_LB + P - 1;
   __shared__ uint32_t h[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
   __syncthreads();
-  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> MSM_SORT_LB], 1u); });
+    msm_for_digits<P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
   __syncthreads();
   if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
@@ -536,19 +555,21 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* _
   }
 }
 
-static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
-    const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra, const uint32_t* __restrict__ sidx,
-    uint32_t extra_start, size_t n, size_t per_blk, const uint32_t* __restrict__ cnt, uint16_t* __restrict__ keys,
-    uint32_t* __restrict__ vals) {
+template <int P>
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const MsmScalars S, const uint32_t* __restrict__ sidx,
+                                                              uint32_t extra_start, size_t n, size_t per_blk,
+                                                              const uint32_t* __restrict__ cnt,
+                                                              uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   ZK_WT(WT_SORT_SCATTER);
   ZK_LIGHT();
+  constexpr int LB = MSM_SORT_LB + P - 1;
   __shared__ uint32_t cur[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
-  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t val) {
-      const uint32_t p = atomicAdd(&cur[key >> MSM_SORT_LB], 1u);
+    msm_for_digits<P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t val) {
+      const uint32_t p = atomicAdd(&cur[key >> LB], 1u);
       keys[p] = (uint16_t)key;
       vals[p] = val;
     });
@@ -557,19 +578,19 @@ static __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(
 // One workgroup per high bin: [bin_start[b], bin_start[b+1]) of (tk, tv) -> buckets in (ko, vo).
 // BINT threads per workgroup (MSM_SORT_BINT).  A 256-thread variant for small MSMs measured
 // neutral on config 5 (1906.7 vs 1894.0 proofs/s, 3 alternations, profiles/r04_ab_c5_small_keys.log).
-template <int BINT>
+template <int BINT, int NL = MSM_SORT_NL>
 __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
                                                       const uint16_t* __restrict__ tk,
                                                       const uint32_t* __restrict__ tv,
                                                       uint16_t* __restrict__ ko,
                                                       uint32_t* __restrict__ vo) {
-  static_assert(BINT >= MSM_SORT_NL && BINT <= 1024, "bins: one thread per low counter");
+  static_assert(BINT >= NL && BINT <= 1024 && NL >= 64, "bins: one thread per low counter");
   ZK_WT(WT_SORT_BINS);
   ZK_LIGHT();
-  __shared__ uint32_t c[MSM_SORT_NL];
+  __shared__ uint32_t c[NL];
   const uint32_t b0 = bin_start[blockIdx.x], b1 = bin_start[blockIdx.x + 1], t = threadIdx.x;
   if (b0 == b1) return;
-  if (t < MSM_SORT_NL) c[t] = 0;
+  if (t < NL) c[t] = 0;
   __syncthreads();
 #if MSM_SORT_STAGE
   // a bin that fits is read from memory once: its pairs wait in LDS for the placing loop
@@ -582,15 +603,15 @@ __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restric
       sk[p - b0] = key;
       sv[p - b0] = tv[p];
     }
-    atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
+    atomicAdd(&c[key & (NL - 1)], 1u);
   }
 #else
-  for (uint32_t p = b0 + t; p < b1; p += BINT) atomicAdd(&c[tk[p] & (MSM_SORT_NL - 1)], 1u);
+  for (uint32_t p = b0 + t; p < b1; p += BINT) atomicAdd(&c[tk[p] & (NL - 1)], 1u);
 #endif
   __syncthreads();
   // exclusive scan of the low counters by the first waves (wave scan + wave totals)
   uint32_t v = 0, x = 0;
-  if (t < MSM_SORT_NL) {
+  if (t < NL) {
     v = c[t];
     x = v;
 #pragma unroll
@@ -599,10 +620,10 @@ __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restric
       if ((t & 63) >= (uint32_t)o) x += y;
     }
   }
-  __shared__ uint32_t wt[MSM_SORT_NL / 64];
-  if (t < MSM_SORT_NL && (t & 63) == 63) wt[t >> 6] = x;
+  __shared__ uint32_t wt[NL / 64];
+  if (t < NL && (t & 63) == 63) wt[t >> 6] = x;
   __syncthreads();
-  if (t < MSM_SORT_NL) {
+  if (t < NL) {
     uint32_t base = b0;
     for (uint32_t w = 0; w < (t >> 6); w++) base += wt[w];
     c[t] = base + x - v;
@@ -616,7 +637,7 @@ __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restric
     const uint16_t key = tk[p];
     const uint32_t val = tv[p];
 #endif
-    const uint32_t q = atomicAdd(&c[key & (MSM_SORT_NL - 1)], 1u);
+    const uint32_t q = atomicAdd(&c[key & (NL - 1)], 1u);
     ko[q] = key;
     vo[q] = val;
   }
@@ -1094,8 +1115,10 @@ uint32_t msm_tail_l0(size_t cap) {
   return l < 1 ? 1u : l > 255 ? 255u : l;
 }
 
+// pairs = 2: the tail of a proof pair (msm_sort_pair): cap = both proofs' bases, 2 NB buckets and
+// reduction scratch per half
 template <class F>
-hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
+hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int pairs = 1) {
   const size_t m = cap * MSM_W;
   t.target = std::min<uint32_t>(msm_resident_chunks<F>(), 0xFFFFFFu);
   t.l0 = msm_tail_l0<F>(cap);
@@ -1111,9 +1134,10 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap) {
     ZK_CHECK(hipMalloc(&t.item_key[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(uint32_t)));
     ZK_CHECK(hipMalloc(&t.item_val[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(XYZZ<F>)));
   }
-  ZK_CHECK(hipMalloc(&t.buckets, MSM_NB * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&t.red_a, 4 * MSM_RB * sizeof(XYZZ<F>)));  // <= 2 level-1 blocks (fast: 128 lanes)
-  ZK_CHECK(hipMalloc(&t.red_s, 4 * MSM_RB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.buckets, pairs * MSM_NB * sizeof(XYZZ<F>)));
+  // <= 2 level-1 blocks (fast: 128 lanes) per half
+  ZK_CHECK(hipMalloc(&t.red_a, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.red_s, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.nnz, sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&t.live, MSM_LIVE_LEVELS * sizeof(uint32_t)));
   return hipSuccess;
@@ -1157,32 +1181,42 @@ hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
 
 // digits (+ nnz) -> sort by bucket into pl.keys_out / pl.vals_out (the first *nnz pairs).  With the
 // rocPRIM sort *nnz must be zero on entry; the bucket sort writes it.
-template <class F>
-hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
-                    const uint32_t* d_extra, hipStream_t st) {
-  if (b.n > pl.cap) return hipErrorInvalidValue;
+// The bucket sort of P proofs' digits over the same bases (P = 2: a proof pair, keys + p NB).
+template <int P, class F>
+hipError_t msm_sort_p(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const MsmScalars& S, hipStream_t st) {
+  const size_t nv = P * b.n;  // virtual bases
+  if (nv > pl.cap) return hipErrorInvalidValue;
   if (b.n == 0) return hipSuccess;
-#if !MSM_SORT_ROCPRIM
   // count / scan / scatter / bins (see k_msm_bin_count); keys_in/vals_in hold the high-bin order
-  const size_t per_blk = (b.n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
+  const size_t per_blk = (nv + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
                              ? (size_t)MSM_SORT_T
-                             : ((b.n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
-  const uint32_t nblk = (uint32_t)((b.n + per_blk - 1) / per_blk);
+                             : ((nv + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
+  const uint32_t nblk = (uint32_t)((nv + per_blk - 1) / per_blk);
   if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
   uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
   uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
-  hipLaunchKernelGGL(k_msm_bin_count, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx, b.extra_start,
-                     b.n, per_blk, cnt);
+  hipLaunchKernelGGL(k_msm_bin_count<P>, dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n, per_blk,
+                     cnt);
   hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
   if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
     pl.ko_sorted = 1;
-    hipLaunchKernelGGL(k_msm_bin_scatter, dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
-                       b.extra_start, b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
-    hipLaunchKernelGGL(k_msm_bin_sort<MSM_SORT_BINT>, dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st, bin_start,
-                       pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+    hipLaunchKernelGGL(k_msm_bin_scatter<P>, dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
+                       per_blk, cnt, pl.keys_in, pl.vals_in);
+    hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, (MSM_SORT_NL << (P - 1))>), dim3(MSM_SORT_HB),
+                       dim3(MSM_SORT_BINT), 0, st, bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
   }
   return hipGetLastError();
+}
+
+template <class F>
+hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
+                    const uint32_t* d_extra, hipStream_t st) {
+#if !MSM_SORT_ROCPRIM
+  const MsmScalars S = {{d_scalars, nullptr}, {d_extra, nullptr}};
+  return msm_sort_p<1>(b, pl, nnz, S, st);
 #else
+  if (b.n > pl.cap) return hipErrorInvalidValue;
+  if (b.n == 0) return hipSuccess;
   const size_t m = b.n * MSM_W;
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
@@ -1199,11 +1233,12 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
 // Accumulation (level 0: fixed chunks, closed runs straight into the buckets, open runs as items)
 // over sorted (bucket, entry) pairs and t.nnz.  The pairs may come from another MSM with the same
 // scalars and base index map (B1's sort serves B2: msm_sort once, accumulate on both curves).
+// pairs = 2: the pairs of a proof pair's sort (msm_sort_p<2>: up to 2 n W entries)
 template <class F>
 hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, MsmTail<F>& t,
-                                 hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
+                                 hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr, int pairs = 1) {
   if (b.n == 0) return hipSuccess;
-  const size_t m = b.n * MSM_W;
+  const size_t m = pairs * b.n * MSM_W;
   size_t chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) chunks = std::min<size_t>(chunks, t.target);  // lanes of msm_chunk_len(nnz, target)
   if (chunks > t.max_chunks) return hipErrorInvalidValue;
@@ -1247,13 +1282,12 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
 // the two weighted-reduction levels, the last writing outs[i].  fast: the latency schedule's
 // reduction (MSM_WSUM_Q_FAST: shorter dependent chain, more waves).
 template <class F>
-hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast = false) {
+hipError_t msm_stitch(MsmTail<F>* const* t, int n, hipStream_t st) {
   if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
-  constexpr int TW = sizeof(typename F::T) == 32 ? MSM_G1_TAIL_WAVES : MSM_G2_TAIL_WAVES;
   constexpr int SW = sizeof(typename F::T) == 32 ? MSM_G1_STITCH_WAVES : MSM_G2_TAIL_WAVES;
-  const MsmTailArgs<F> ta = msm_tail_args<F>(t, outs, n);
+  const MsmTailArgs<F> ta = msm_tail_args<F>(t, nullptr, n);
   size_t N = 0;
   for (int i = 0; i < n; i++) N = std::max(N, t[i]->item_cap[0]);
   N = std::max<size_t>(N, 2);
@@ -1271,7 +1305,17 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
     N = 2 * lanes;
     cur ^= 1;
   }
+  return hipGetLastError();
+}
+
+// The two weighted-reduction levels of n bucket sets (ta: buckets, red_a, red_s, out of each)
+template <class F>
+hipError_t msm_wsum(const MsmTailArgs<F>& ta, int n, hipStream_t st, bool fast) {
+  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
   if (ZK_KNOCKOUT & 16) return hipGetLastError();
+  using FC = typename MsmCompute<F>::type;
+  constexpr int LN = MsmIO<FC>::LANES;
+  constexpr int TW = sizeof(typename F::T) == 32 ? MSM_G1_TAIL_WAVES : MSM_G2_TAIL_WAVES;
   constexpr int Q0 = msm_wsum_q0<F>(), QF = MSM_WSUM_Q_FAST;
   if (fast) {
     hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, QF>), dim3(MSM_NB / (MSM_RB * QF), n), dim3(MSM_RB * LN), 0, st, ta);
@@ -1281,6 +1325,31 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
     hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, Q0>), dim3(1, n), dim3(msm_wsum_rb<false, Q0>() * LN), 0, st, ta);
   }
   return hipGetLastError();
+}
+
+template <class F>
+hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast = false) {
+  ZK_CHECK(msm_stitch(t, n, st));
+  return msm_wsum(msm_tail_args<F>(t, outs, n), n, st, fast);
+}
+
+// Tails of n proof-pair MSMs (msm_sort_pair, msm_tail_alloc(.., 2)): the stitching levels over each
+// pair's 2 NB buckets as one MSM, then the reduction of each half apart: outs[2 i + h] = the sum of
+// pair i's proof h.
+template <class F>
+hipError_t msm_tails_pair(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) {
+  if (2 * n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  ZK_CHECK(msm_stitch(t, n, st));
+  MsmTailArgs<F> ta = {};
+  for (int i = 0; i < n; i++)
+    for (int h = 0; h < 2; h++) {
+      const int y = 2 * i + h;
+      ta.buckets[y] = t[i]->buckets + (size_t)h * MSM_NB;
+      ta.red_a[y] = t[i]->red_a + (size_t)h * MSM_TAIL_RED;
+      ta.red_s[y] = t[i]->red_s + (size_t)h * MSM_TAIL_RED;
+      ta.out[y] = outs[y];
+    }
+  return msm_wsum(ta, 2 * n, st, fast);
 }
 
 template <class F>
@@ -1307,6 +1376,19 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
   }                                                                                                      \
   void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
   hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap) { return msm_tail_alloc(t, cap); }          \
+  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap) { return msm_tail_alloc(t, cap, 2); }  \
+  hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0,  \
+                                 const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st) { \
+    const MsmScalars S = {{sc0, sc1}, {ex0, ex1}};                                                       \
+    return msm_sort_p<2>(b, s, nnz, S, st);                                                              \
+  }                                                                                                      \
+  hipError_t msm_tails_pair_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) { \
+    return msm_tails_pair(t, outs, n, st, fast);                                                         \
+  }                                                                                                      \
+  hipError_t msm_accumulate_sorted_pair_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, \
+                                              MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag) { \
+    return msm_accumulate_sorted(b, keys, vals, t, st, prof, tag, 2);                                    \
+  }                                                                                                      \
   void msm_tail_free_##SUF(MsmTail<F>& t) { msm_tail_free(t); }                                          \
   hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc, \
                                   const uint32_t* ex, hipStream_t st, Profiler* prof, const char* tag) { \

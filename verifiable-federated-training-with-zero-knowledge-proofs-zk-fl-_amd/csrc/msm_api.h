@@ -190,7 +190,8 @@ inline uint32_t msm_target_arg(const MsmTail<F>& t) {
   return (t.l0 << 24) | (t.target & 0xFFFFFFu);
 }
 
-constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs of a proof)
+constexpr int MSM_TAIL_MAX = 6;  // MSM tails per batched launch (the 4 G1 MSMs of a proof; 3 pairs' halves)
+constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket set (<= 2 level-1 blocks of 128 lanes)
 
 #define ZKFL_MSM_DECLARE(SUF, F)                                                                    \
   hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                       \
@@ -215,7 +216,15 @@ constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs 
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st,     \
                              bool fast = false);                                                      \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \
-                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
+                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag); \
+  /* proof pairs (small keys): two proofs' digits over the same bases as one sort with 2 NB bucket  \
+     keys into a pair tail (cap = both proofs' bases); its tails reduce each half: outs[2 i + h] */ \
+  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap);                                  \
+  hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0, \
+                                 const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st); \
+  hipError_t msm_tails_pair_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast); \
+  hipError_t msm_accumulate_sorted_pair_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, \
+                                              MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag);
 
 ZKFL_MSM_DECLARE(g1, FqOps)
 ZKFL_MSM_DECLARE(g2, Fq2Ops)

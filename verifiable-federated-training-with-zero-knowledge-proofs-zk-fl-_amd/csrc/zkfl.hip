@@ -290,6 +290,67 @@ __global__ void __launch_bounds__(256) k_proof_start(const uint32_t* __restrict_
   if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ps.live[y][threadIdx.x] = 0;
 }
 
+// A proof pair's first kernel (ProofPair): both witnesses staged from the addresses the host left
+// in the pair's pinned buffer, both proofs' augmentation scalars and r, s, GLV halves (d_rs: r0 s0 |
+// r1 s1 | ks0[4] | ks1[4], the layout k_assemble reads with blockIdx.x = proof), res[3] and res[8]
+// = infinity (the merged C + H), and the pair tails emptied (blockIdx.y = tail).
+struct PairStart {
+  const uint32_t* rs_host[2];   // r, s, GLV halves of proof p (RS_WORDS words, pinned)
+  const uint64_t* w_src_host[2];
+  uint4* w_dst[2];
+  uint32_t w_nvec;
+  Fr* extra[2];
+  uint32_t* d_rs;
+  uint32_t* res;
+  uint4* buckets[4];
+  uint32_t nvec[4];
+  uint32_t* nnz[4];
+  uint32_t* live[4];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_pair_start(const PairStart ps) {
+  ZK_WT(WT_SET_EXTRA);
+  ZK_LIGHT();
+  const int y = blockIdx.y;
+  {
+    __shared__ const uint4* src[2];
+    if (threadIdx.x < 2) src[threadIdx.x] = reinterpret_cast<const uint4*>(*ps.w_src_host[threadIdx.x]);
+    __syncthreads();
+    const size_t nb = (size_t)gridDim.x * gridDim.y * blockDim.x, tot = 2 * (size_t)ps.w_nvec;
+    for (size_t i = ((size_t)y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < tot; i += nb) {
+      const int q = i >= ps.w_nvec;
+      const size_t j = i - (size_t)q * ps.w_nvec;
+      ps.w_dst[q][j] = src[q][j];
+    }
+  }
+  if (y == 0 && blockIdx.x == 2 && threadIdx.x < 2 * RS_WORDS) {
+    const int q = threadIdx.x >= RS_WORDS, w = threadIdx.x - q * RS_WORDS;
+    ps.d_rs[w < 16 ? 16 * q + w : 32 + 32 * q + (w - 16)] = ps.rs_host[q][w];
+  }
+  if (y == 0 && blockIdx.x == 0 && threadIdx.x < 2) {
+    const int q = threadIdx.x;
+    const Fr* rs = reinterpret_cast<const Fr*>(ps.rs_host[q]);
+    Fr one = fp_zero<FrP>();
+    one.v[0] = 1u;
+    const Fr r = rs[0], s = rs[1];
+    ps.extra[q][0] = one;
+    ps.extra[q][1] = r;
+    ps.extra[q][2] = s;
+    ps.extra[q][3] = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
+  }
+  if (y == 0 && blockIdx.x == 1 && threadIdx.x < 2 * sizeof(G1P) / 4) {
+    const int q = threadIdx.x >= sizeof(G1P) / 4;
+    ps.res[(3 + 5 * q) * sizeof(G1P) / 4 + threadIdx.x - q * sizeof(G1P) / 4] = 0u;  // res[3], res[8]: ZZ = 0
+  }
+  if (y >= ps.n) return;
+  uint4* b = ps.buckets[y];
+  const size_t nv = ps.nvec[y];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
+    b[i] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ps.nnz[y] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ps.live[y][threadIdx.x] = 0;
+}
+
 template <class F>
 __device__ void store_affine_std(const Affine<F>& a, uint32_t* out);
 
@@ -887,6 +948,35 @@ struct ProofSlot {
   uint8_t* out_part = nullptr;    // split proofs: where the 768 part bytes go (nullable)
 };
 
+// Two proofs of one small key through ONE chain of launches (batches with ZKFL_PAIRS=1,
+// zkfl_key::pairs; an A/B knob, see key_pairs).  The idea: config 5's 16 proofs in flight are
+// chains of ~37 small kernels whose summed kernel time (3.1 ms per proof,
+// profiles/r05_c5_kernels_8slots.csv) is well under the ~7.5 ms a chain takes under load, and more
+// chains (slots) than 8 per key oversubscribe the hardware queues (10 slots: 1,167 vs 2,139
+// proofs/s), so half the launches per proof should have paid.  A pair sorts both proofs' digits as
+// one problem with 2 NB bucket keys (msm_sort_pair: proof p's buckets at p NB), so the accumulations
+// and stitching levels run once for both; only the bucket reductions take the halves apart
+// (msm_tails_pair), and ABC / NTT stay per proof.  Pair k runs on slot k's stream (no more streams,
+// no more hardware queues), its per-proof vectors in two stream-less half slots.
+struct ProofPair {
+  ProofSlot* slot = nullptr;      // the key's slot whose stream this pair uses (not owned)
+  ProofSlot* half[2] = {nullptr, nullptr};  // per-proof vectors: abc, h | extra, witness stage (owned)
+  hipEvent_t ev_done = nullptr;
+  MsmScratch<FqOps> g1s;          // the pair sorts (A, B1 = B2, C + H), 2 x the bases each
+  MsmTail<FqOps> g1t[3];          // A, B1, C + H pair tails (2 NB buckets)
+  MsmTail<Fq2Ops> g2t;            // B2's pair tail; counts with B1's nnz
+  G1P* res = nullptr;             // [2][5]: proof p's A', B1', C' + H, (infinity), unused
+  G2P* resB2 = nullptr;           // [2]
+  uint32_t* d_rs = nullptr;       // r0 s0 | r1 s1 (16 words each), then GLV halves [2][4] (k_assemble's ks)
+  uint8_t* pinned = nullptr;      // proofs (2 x 256) | r, s, GLV halves (2 x 256 at 512) | witness addresses (at 1024)
+  hipGraph_t g = nullptr;         // the pair chain, captured on the pair's second use
+  hipGraphExec_t ex = nullptr;
+  uint32_t direct = 0;
+  bool busy = false;
+  uint8_t* out_proof[2] = {nullptr, nullptr};
+};
+constexpr size_t PAIR_RS_OFF = 512, PAIR_RS_STRIDE = 256, PAIR_W_OFF = 1024;
+
 #ifndef ZK_NO_SHARE_B
 #define ZK_NO_SHARE_B 0  // 1: B2 sorts its own digits (A/B builds)
 #endif
@@ -922,6 +1012,7 @@ struct zkfl_key {
   bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
+  std::vector<ProofPair*> pairs;  // proof pairs of batches (small keys), pair k on slot k's stream
   int max_slots = 3;
   // Split proofs (zkfl_zkey_load_shard): this key holds base i of every query only when
   // i % nshards == shard, and the alpha/beta/delta augmentation bases only on shard 0, so its
@@ -992,6 +1083,24 @@ void slot_release(ProofSlot* s) {
 }
 
 int graph_mode();
+
+void pair_release(ProofPair* pr) {
+  if (!pr) return;
+  if (pr->slot && pr->slot->st_main) (void)hipStreamSynchronize(pr->slot->st_main);
+  if (pr->ex) (void)hipGraphExecDestroy(pr->ex);
+  if (pr->g) (void)hipGraphDestroy(pr->g);
+  for (ProofSlot* h : pr->half) slot_release(h);
+  msm_scratch_free_g1(pr->g1s);
+  for (auto& t : pr->g1t) msm_tail_free_g1(t);
+  pr->g2t.nnz = nullptr;  // g1t[1]'s
+  msm_tail_free_g2(pr->g2t);
+  void* ptrs[] = {pr->res, pr->resB2, pr->d_rs};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (pr->pinned) (void)hipHostFree(pr->pinned);
+  if (pr->ev_done) (void)hipEventDestroy(pr->ev_done);
+  delete pr;
+}
 
 // Release a slot's latency-schedule streams and events (made again on its next batch of one).
 void slot_drop_lowlat(ProofSlot* s) {
@@ -1076,6 +1185,73 @@ int get_slot(zkfl_key* k, size_t idx, ProofSlot** out) {
   return ZKFL_OK;
 }
 
+// A pair's per-proof vectors: a slot without streams or MSM structures
+hipError_t half_create(zkfl_key* k, ProofSlot** out) {
+  ProofSlot* s = new ProofSlot();
+  *out = s;
+  const size_t n = k->n;
+  ZK_CHECK(hipMalloc(&s->w_stage, (size_t)k->nVars * 32));
+  ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));
+  s->extra = s->h + n;
+  ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
+  const size_t abc_chunks = (k->K + ABC_L - 1) / ABC_L + 1;
+  ZK_CHECK(hipMalloc(&s->abc_head, abc_chunks * 32));
+  ZK_CHECK(hipMalloc(&s->abc_tail, abc_chunks * 32));
+  return hipSuccess;
+}
+
+hipError_t pair_create(zkfl_key* k, ProofSlot* slot, ProofPair** out) {
+  ProofPair* pr = new ProofPair();
+  *out = pr;
+  pr->slot = slot;
+  for (ProofSlot*& h : pr->half) ZK_CHECK(half_create(k, &h));
+  ZK_CHECK(hipEventCreateWithFlags(&pr->ev_done, hipEventDisableTiming));
+  const size_t cap = std::max<size_t>({k->bA.n, k->bB1.n, k->bCH.n});
+  ZK_CHECK(msm_scratch_alloc_g1(pr->g1s, 2 * cap, k->ctx->st));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[0], 2 * k->bA.n));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[1], 2 * k->bB1.n));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[2], 2 * k->bCH.n));
+  ZK_CHECK(msm_tail_alloc_pair_g2(pr->g2t, 2 * k->bB2.n));
+  ZK_CHECK(hipFree(pr->g2t.nnz));  // B2 counts with B1's nnz (the same sort)
+  pr->g2t.nnz = pr->g1t[1].nnz;
+  ZK_CHECK(hipMalloc(&pr->res, 10 * sizeof(G1P)));
+  ZK_CHECK(hipMalloc(&pr->resB2, 2 * sizeof(G2P)));
+  ZK_CHECK(hipMalloc(&pr->d_rs, 2 * 64 + 8 * sizeof(GlvScalar)));
+  ZK_CHECK(hipHostMalloc(&pr->pinned, 2048, hipHostMallocCoherent));
+  return hipStreamSynchronize(k->ctx->st);
+}
+
+// ZKFL_PAIRS=1 (an A/B knob, off; read per batch): batches of a small key run their proofs two at a
+// time through one chain (ProofPair).  Bit-exact (the GPU suite passes with it on), but config 5
+// measured 1,714 vs 2,154 proofs/s at 8 slots per key, and 2,098 / 2,158 at 4 pair slots against
+// 2,133 at 8 single slots (profiles/r05_ab_c5_pairs.log): the launches a pair saves do not set the
+// pace -- about 16 proofs in flight do, however they are grouped.
+bool key_pairs(const zkfl_key* k) {
+  const char* e = getenv("ZKFL_PAIRS");
+  const int on = e ? atoi(e) : 0;
+  static const int lim = getenv("ZKFL_PAIRS_LOGN") ? atoi(getenv("ZKFL_PAIRS_LOGN")) : 16;
+  return on && MSM_MERGE_CH && !ZK_KNOCKOUT && k->share_b && k->nshards == 1 && k->logn <= lim &&
+         !k->ctx->prof.on && !k->ctx->prof.serialize;
+}
+
+int get_pair(zkfl_key* k, size_t idx, ProofPair** out) {
+  const size_t want = idx % (size_t)k->max_slots;
+  while (k->pairs.size() <= want) {
+    ProofSlot* slot = nullptr;
+    int rc = get_slot(k, k->pairs.size(), &slot);
+    if (rc) return rc;
+    ProofPair* pr = nullptr;
+    hipError_t e = pair_create(k, slot, &pr);
+    if (e != hipSuccess) {
+      pair_release(pr);
+      return hip_fail(e, "proof pair allocation");
+    }
+    k->pairs.push_back(pr);
+  }
+  *out = k->pairs[want];
+  return ZKFL_OK;
+}
+
 }  // namespace
 
 // Witnesses of the single-key full-prove entry points, computed G (= the key's slots) jobs at a
@@ -1147,6 +1323,8 @@ void key_release(zkfl_key* k) {
   if (!k) return;
   wpipe_release(k->wpipe);
   k->wpipe = nullptr;
+  for (ProofPair* pr : k->pairs) pair_release(pr);
+  k->pairs.clear();
   for (ProofSlot* s : k->slots) slot_release(s);
   k->slots.clear();
   msm_bases_free_g1(k->bA);
@@ -1693,6 +1871,121 @@ int wait_slot(ProofSlot* s, bool poll = false) {
   return ZKFL_OK;
 }
 
+// The chain of a proof pair (ProofPair) on its slot's stream: the witnesses staged by k_pair_start,
+// ABC + NTT per proof, then A, B1 (+ B2 on B1's pairs) and C + H each as one pair MSM, the G2 and G1
+// tails with per-half reductions (small keys: the short-chain reduction), and k_assemble over both
+// proofs (blockIdx.x = proof) into the pair's pinned buffer.
+int enqueue_pair_body(zkfl_ctx* ctx, zkfl_key* k, ProofPair* pr) {
+  Profiler* prof = &ctx->prof;
+  hipStream_t st = pr->slot->st_main;
+  {
+    PairStart ps = {};
+    for (int q = 0; q < 2; q++) {
+      ps.rs_host[q] = reinterpret_cast<const uint32_t*>(pr->pinned + PAIR_RS_OFF + q * PAIR_RS_STRIDE);
+      ps.w_src_host[q] = reinterpret_cast<const uint64_t*>(pr->pinned + PAIR_W_OFF + 8 * q);
+      ps.w_dst[q] = reinterpret_cast<uint4*>(pr->half[q]->w_stage);
+      ps.extra[q] = pr->half[q]->extra;
+    }
+    ps.w_nvec = (uint32_t)((size_t)k->nVars * 32 / sizeof(uint4));
+    ps.d_rs = pr->d_rs;
+    ps.res = reinterpret_cast<uint32_t*>(pr->res);
+    auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
+      ps.buckets[ps.n] = static_cast<uint4*>(buckets);
+      ps.nvec[ps.n] = (uint32_t)(bytes / sizeof(uint4));
+      ps.nnz[ps.n] = nnz;
+      ps.live[ps.n] = live;
+      ps.n++;
+    };
+    for (auto& t : pr->g1t) add(t.buckets, 2 * MSM_NB * sizeof(G1P), t.nnz, t.live);
+    add(pr->g2t.buckets, 2 * MSM_NB * sizeof(G2P), pr->g2t.nnz, pr->g2t.live);
+    hipLaunchKernelGGL(k_pair_start, dim3(64, ps.n), dim3(256), 0, st, ps);
+  }
+  for (ProofSlot* h : pr->half) {
+    const int rc = enqueue_abc_ntt(k, h, h->w_stage, st, prof);
+    if (rc) return rc;
+  }
+  const uint32_t *W0 = (const uint32_t*)pr->half[0]->w_stage, *W1 = (const uint32_t*)pr->half[1]->w_stage;
+  const uint32_t *E0 = (const uint32_t*)pr->half[0]->extra, *E1 = (const uint32_t*)pr->half[1]->extra;
+  const uint32_t *H0 = (const uint32_t*)pr->half[0]->h, *H1 = (const uint32_t*)pr->half[1]->h;
+  const bool fast = small_key_fast_wsum(k);
+  HIP_TRY(msm_sort_pair_g1(k->bA, pr->g1s, pr->g1t[0].nnz, W0, E0, W1, E1, st), "pair A sort");
+  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bA, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[0], st, prof,
+                                   "msm_accumulate_g1"), "pair A");
+  HIP_TRY(msm_sort_pair_g1(k->bB1, pr->g1s, pr->g1t[1].nnz, W0, E0, W1, E1, st), "pair B sort");
+  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bB1, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[1], st, prof,
+                                   "msm_accumulate_g1"), "pair B1");
+  HIP_TRY(msm_accumulate_sorted_pair_g2(k->bB2, pr->g1s.keys_out, pr->g1s.vals_out, pr->g2t, st, prof,
+                                   "msm_accumulate_g2"), "pair B2");
+  {
+    MsmTail<Fq2Ops>* t2 = &pr->g2t;
+    G2P* o2[2] = {pr->resB2, pr->resB2 + 1};
+    HIP_TRY(msm_tails_pair_g2(&t2, o2, 1, st, fast), "pair B2 tail");
+  }
+  HIP_TRY(msm_sort_pair_g1(k->bCH, pr->g1s, pr->g1t[2].nnz, W0, H0, W1, H1, st), "pair C+H sort");
+  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bCH, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[2], st, prof,
+                                   "msm_accumulate_g1"), "pair C+H");
+  {
+    MsmTail<FqOps>* tl[3] = {&pr->g1t[0], &pr->g1t[1], &pr->g1t[2]};
+    G1P* outs[6] = {pr->res + 0, pr->res + 5, pr->res + 1, pr->res + 6, pr->res + 2, pr->res + 7};
+    HIP_TRY(msm_tails_pair_g1(tl, outs, 3, st, fast), "pair tails");
+  }
+  if (!(ZK_KNOCKOUT & 1))
+    hipLaunchKernelGGL(k_assemble, dim3(2), dim3(192), 0, st, pr->res, pr->resB2,
+                       reinterpret_cast<const GlvScalar*>(pr->d_rs + 32), reinterpret_cast<uint32_t*>(pr->pinned));
+  return ZKFL_OK;
+}
+
+// Two jobs of one key through one pair chain: r, s (+ GLV halves) and the witness addresses into the
+// pinned buffer, then the chain -- kernel by kernel on the pair's first use, from its graph after.
+int enqueue_pair(zkfl_ctx* ctx, zkfl_key* k, ProofPair* pr, const Fr* const w[2], const uint32_t* const rs[2]) {
+  for (int q = 0; q < 2; q++) {
+    uint8_t* r = pr->pinned + PAIR_RS_OFF + q * PAIR_RS_STRIDE;
+    memcpy(r, rs[q], 64);
+    GlvScalar* ks = reinterpret_cast<GlvScalar*>(r + 64);
+    glv_split(rs[q] + 8, ks[0], ks[1]);  // s -> s1, s2 (pi_A)
+    glv_split(rs[q], ks[2], ks[3]);      // r -> r1, r2 (B1)
+    const uint64_t src = reinterpret_cast<uint64_t>(w[q]);
+    memcpy(pr->pinned + PAIR_W_OFF + 8 * q, &src, sizeof(src));
+  }
+  hipStream_t st = pr->slot->st_main;
+  if (graph_mode() && pr->direct > 0 && !pr->ex) {
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "begin capture");
+    const int rc = enqueue_pair_body(ctx, k, pr);
+    const hipError_t ec = hipStreamEndCapture(st, &pr->g);
+    if (rc) {
+      if (pr->g) (void)hipGraphDestroy(pr->g);
+      pr->g = nullptr;
+      return rc;
+    }
+    HIP_TRY(ec, "end capture");
+    const hipError_t ei = hipGraphInstantiate(&pr->ex, pr->g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(pr->g);
+      pr->g = nullptr;
+      pr->ex = nullptr;
+      return hip_fail(ei, "graph instantiate");
+    }
+  }
+  if (pr->ex) {
+    HIP_TRY(hipGraphLaunch(pr->ex, st), "graph launch");
+  } else {
+    pr->direct++;
+    const int rc = enqueue_pair_body(ctx, k, pr);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(pr->ev_done, st), "event");
+  HIP_TRY(hipGetLastError(), "launch");
+  return ZKFL_OK;
+}
+
+int wait_pair(ProofPair* pr, bool poll) {
+  HIP_TRY(host_wait(pr->ev_done, poll), "sync");
+  for (int q = 0; q < 2; q++)
+    if (pr->out_proof[q]) memcpy(pr->out_proof[q], pr->pinned + 256 * q, 256);
+  pr->busy = false;
+  return ZKFL_OK;
+}
+
 // One proof of a batch: a device-resident witness, complete once w_ready is (nullptr: already).
 // Jobs of one batch may use different keys.
 struct Job {
@@ -1711,7 +2004,40 @@ struct Job {
 template <class GetJob>
 int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-  std::vector<std::pair<zkfl_key*, size_t>> cursor;  // per key: proofs issued in this batch
+  struct PerKey {
+    zkfl_key* key;
+    size_t issued = 0, pairs = 0;  // proofs issued on single slots / pairs issued in this batch
+    bool pend = false;             // a job waiting for its partner (proof pairs)
+    Job pj;
+    size_t pi = 0;
+    uint32_t prs[16];
+  };
+  std::vector<PerKey> cursor;
+  // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
+  // 1: A and B before ABC / NTT, 2: overlapped)
+  static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
+  // A/B knob: ZKFL_LOWLAT_BATCH=1 runs every proof of a batch on the low-latency schedule
+  static const bool lowlat_batch = getenv("ZKFL_LOWLAT_BATCH") && atoi(getenv("ZKFL_LOWLAT_BATCH")) != 0;
+  auto single = [&](PerKey& pk, size_t i, const Job& J, const uint32_t* rsl) -> int {
+    ProofSlot* s = nullptr;
+    int rc = get_slot(J.key, pk.issued++, &s);
+    if (rc) return rc;
+    if (s->busy) {
+      rc = wait_slot(s, n > 1);
+      if (rc) return rc;
+    }
+    s->job = i;
+    s->out_proof = J.part_out ? nullptr : J.proof_out;
+    s->out_part = J.part_out;
+    if (J.w_ready) {
+      hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
+      if (e != hipSuccess) return hip_fail(e, "wait for the witness group");
+    }
+    rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, (n == 1 || lowlat_batch) ? lowlat : 0);
+    if (rc) return rc;
+    s->busy = true;
+    return ZKFL_OK;
+  };
   int rc = ZKFL_OK;
   for (size_t i = 0; i < n && rc == ZKFL_OK; i++) {
     Job J;
@@ -1727,38 +2053,62 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     rc = get_rs(J.rs, rsl);
     if (rc) break;
     size_t c = 0;
-    while (c < cursor.size() && cursor[c].first != J.key) c++;
-    if (c == cursor.size()) cursor.push_back({J.key, 0});
-    ProofSlot* s = nullptr;
-    rc = get_slot(J.key, cursor[c].second++, &s);
-    if (rc) break;
-    if (s->busy) {
-      rc = wait_slot(s, n > 1);
+    while (c < cursor.size() && cursor[c].key != J.key) c++;
+    if (c == cursor.size()) {
+      cursor.emplace_back();
+      cursor.back().key = J.key;
+    }
+    PerKey& pk = cursor[c];
+    if (n > 1 && !J.part_out && key_pairs(J.key)) {  // two proofs of one key per chain
+      if (!pk.pend) {
+        pk.pend = true;
+        pk.pj = J;
+        pk.pi = i;
+        memcpy(pk.prs, rsl, sizeof(rsl));
+        continue;
+      }
+      ProofPair* pr = nullptr;
+      rc = get_pair(J.key, pk.pairs++, &pr);
       if (rc) break;
+      if (pr->busy) {
+        rc = wait_pair(pr, true);
+        if (rc) break;
+      }
+      for (const Job* x : {&pk.pj, &J})
+        if (x->w_ready) {
+          hipError_t e = hipStreamWaitEvent(pr->slot->st_main, x->w_ready, 0);
+          if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
+        }
+      if (rc) break;
+      pr->out_proof[0] = pk.pj.proof_out;
+      pr->out_proof[1] = J.proof_out;
+      const Fr* w[2] = {pk.pj.w, J.w};
+      const uint32_t* rsp[2] = {pk.prs, rsl};
+      rc = enqueue_pair(ctx, J.key, pr, w, rsp);
+      if (rc) break;
+      pr->busy = true;
+      pk.pend = false;
+      continue;
     }
-    s->job = i;
-    s->out_proof = J.part_out ? nullptr : J.proof_out;
-    s->out_part = J.part_out;
-    if (J.w_ready) {
-      hipError_t e = hipStreamWaitEvent(s->st_main, J.w_ready, 0);
-      if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
-    }
-    // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
-    // 1: A and B before ABC / NTT, 2: overlapped)
-    static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
-    // A/B knob: ZKFL_LOWLAT_BATCH=1 runs every proof of a batch on the low-latency schedule
-    static const bool lowlat_batch = getenv("ZKFL_LOWLAT_BATCH") && atoi(getenv("ZKFL_LOWLAT_BATCH")) != 0;
-    if (rc == ZKFL_OK)
-      rc = enqueue_proof(ctx, J.key, s, J.w, rsl, J.part_out ? 2 : 0, (n == 1 || lowlat_batch) ? lowlat : 0);
-    if (rc) break;
-    s->busy = true;
+    rc = single(pk, i, J, rsl);
   }
-  for (auto& kc : cursor)
-    for (ProofSlot* s : kc.first->slots)
+  for (auto& pk : cursor)  // a key's odd last job runs alone
+    if (rc == ZKFL_OK && pk.pend) {
+      rc = single(pk, pk.pi, pk.pj, pk.prs);
+      pk.pend = false;
+    }
+  for (auto& pk : cursor) {
+    for (ProofSlot* s : pk.key->slots)
       if (s->busy) {
         int r2 = wait_slot(s, n > 1);
         if (rc == ZKFL_OK) rc = r2;
       }
+    for (ProofPair* pr : pk.key->pairs)
+      if (pr->busy) {
+        int r2 = wait_pair(pr, n > 1);
+        if (rc == ZKFL_OK) rc = r2;
+      }
+  }
   return rc;
 }
 
@@ -2383,6 +2733,11 @@ int zkfl_key_set_slots(zkfl_key* key, int slots) {
   for (ProofSlot* s : key->slots) {
     if (s->busy) return fail(ZKFL_E_ARG, "slots busy");
   }
+  for (ProofPair* pr : key->pairs) {
+    if (pr->busy) return fail(ZKFL_E_ARG, "slots busy");
+  }
+  for (ProofPair* pr : key->pairs) pair_release(pr);  // pair k lives on slot k's stream
+  key->pairs.clear();
   while ((int)key->slots.size() > slots) {
     slot_release(key->slots.back());
     key->slots.pop_back();
@@ -2551,7 +2906,9 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
       uint32_t nw = 0, nin = 0, np = 0;
       wprog_info(pk.prog, &nw, &nin, &np);
       pk.n_in = nin;
-      pk.G = (size_t)k->max_slots;
+      // one group = the proofs a key holds in flight (pairs hold two per slot): the witness sets'
+      // reuse (enqueue_group) relies on it
+      pk.G = (size_t)k->max_slots * (n > 1 && key_pairs(k) ? 2 : 1);
       ks.push_back(pk);
     }
     kidx[i] = c;
