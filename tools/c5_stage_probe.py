@@ -65,6 +65,8 @@ def main():
     for nm in keys:
         for w in res[nm]:
             w.close()
+        progs[nm].close()
+        keys[nm].close()  # its slot streams would hold hardware queues beside the c5 leg's own keys
     s, _ = bench.c5_leg(ctx, 0, 1, args.rounds, args.slots, None, 0)
     print(f"witness {n / tw:.1f} /s | proofs (one key at a time, {args.slots} slots) {n / tp:.1f} /s | "
           f"proofs (per-round batches of 8) {n / tr2:.1f} /s | full c5 {s['value']:.1f} proofs/s", flush=True)
