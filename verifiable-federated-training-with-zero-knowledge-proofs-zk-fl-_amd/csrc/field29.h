@@ -205,25 +205,34 @@ ZK_HD void f29_keep(uint64_t& a) {
 #endif
 }
 
-template <int NP>
+// NACC: accumulators per column (chains a lone wave can issue from; the latency-bound kernels --
+// k_assemble's quad operations -- take 4, the throughput kernels 2: every extra chain costs one
+// 64-bit join per column)
+template <int NP, int NACC = (F29_SPLIT ? 2 : 1)>
 ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
+  static_assert(NACC == 1 || NACC == 2 || NACC == 4, "accumulators per column");
   uint32_t m[9];
   F29 r;
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 17; k++) {
-    uint64_t acc[2] = {carry, 0};
+    uint64_t acc[NACC];
+    acc[0] = carry;
+#pragma unroll
+    for (int q = 1; q < NACC; q++) acc[q] = 0;
     int t = 0;
     const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
 #pragma unroll
     for (int i = lo; i <= hi; i++) {
 #pragma unroll
-      for (int j = 0; j < NP; j++) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)x[j].v[i] * y[j].v[k - i];
-      if (i < k) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)m[i] * P29::P[k - i];  // m_k is not known yet
+      for (int j = 0; j < NP; j++) acc[(t++) % NACC] += (uint64_t)x[j].v[i] * y[j].v[k - i];
+      if (i < k) acc[(t++) % NACC] += (uint64_t)m[i] * P29::P[k - i];  // m_k is not known yet
     }
-    f29_keep(acc[0]);
-    f29_keep(acc[1]);
-    uint64_t c = acc[0] + acc[1];
+#pragma unroll
+    for (int q = 0; q < NACC; q++) f29_keep(acc[q]);
+    uint64_t c = acc[0];
+    if (NACC == 4) c = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    else if (NACC == 2) c = acc[0] + acc[1];
     if (k < 9) {
       m[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
       c += (uint64_t)m[k] * P29::P[0];
@@ -240,6 +249,13 @@ ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
 ZK_HD F29 f29_mul(const F29& a, const F29& b) {
   const F29 x[1] = {a}, y[1] = {b};
   return f29_mont<1>(x, y);
+}
+
+// The same product with ACC accumulators per column (latency-bound single-wave kernels)
+template <int ACC>
+ZK_HD F29 f29_mul_acc(const F29& a, const F29& b) {
+  const F29 x[1] = {a}, y[1] = {b};
+  return f29_mont<1, ACC>(x, y);
 }
 
 // Montgomery square a^2 2^-261 of a NORMALIZED a (every limb < 2^29): the cross products

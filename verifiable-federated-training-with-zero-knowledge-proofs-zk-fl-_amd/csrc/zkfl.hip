@@ -403,7 +403,14 @@ ZK_DEV void pick4_words(int q, const uint32_t (&a)[N], const uint32_t (&b)[N], c
 
 struct Q29 {
   using T = F29;
-  static ZK_DEV T mul(const T& a, const T& b) { return f29_canon_sub<1>(f29_mul(a, b)); }
+  // ZKFL_Q29_ACC: accumulators per product column of the assembly's quad operations (an A/B knob:
+  // one wave alone on its SIMD might issue from more chains; 4 measured 2,075 vs 2,106 config-5
+  // proofs/s and 4.05 vs 4.00 ms alone, 3 same-box alternations, profiles/r05_ab_q29_acc.log: the
+  // extra joins cost what the shorter spine saves)
+#ifndef ZKFL_Q29_ACC
+#define ZKFL_Q29_ACC 2
+#endif
+  static ZK_DEV T mul(const T& a, const T& b) { return f29_canon_sub<1>(f29_mul_acc<ZKFL_Q29_ACC>(a, b)); }
   static ZK_DEV T add(const T& a, const T& b) {
     T r = f29_add_lazy(a, b);
     f29_norm(r);
@@ -2906,9 +2913,11 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
       uint32_t nw = 0, nin = 0, np = 0;
       wprog_info(pk.prog, &nw, &nin, &np);
       pk.n_in = nin;
-      // one group = the proofs a key holds in flight (pairs hold two per slot): the witness sets'
-      // reuse (enqueue_group) relies on it
-      pk.G = (size_t)k->max_slots * (n > 1 && key_pairs(k) ? 2 : 1);
+      // one group >= the proofs a key holds in flight (pairs hold two per slot): the witness sets'
+      // reuse (enqueue_group) relies on it.  ZKFL_WIT_GROUP=m: m times that (a witness launch
+      // serves m x as many witnesses; its kernels are latency-bound, so they take about as long)
+      static const int wg = getenv("ZKFL_WIT_GROUP") ? std::max(1, atoi(getenv("ZKFL_WIT_GROUP"))) : 1;
+      pk.G = (size_t)k->max_slots * (n > 1 && key_pairs(k) ? 2 : 1) * wg;
       ks.push_back(pk);
     }
     kidx[i] = c;
