@@ -23,13 +23,14 @@ MASK = (1 << 29) - 1
 
 
 # F29_PAIRED=1: the point formulas take their independent products two at a time (f29_mont2) --
-# the same values, checked with the same cases
-@pytest.fixture(scope="module", params=[0, 1], ids=["single", "paired"])
+# the same values, checked with the same cases; F29_TRIPLE=1 (default) the madd's three-chain products
+@pytest.fixture(scope="module", params=[(0, 0), (1, 0), (1, 1)], ids=["single", "paired", "triple"])
 def f29(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     out = str(tmp_path_factory.mktemp("f29") / "f29_check")
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17", f"-DF29_PAIRED={request.param}",
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17", f"-DF29_PAIRED={request.param[0]}",
+                    f"-DF29_TRIPLE={request.param[1]}",
                     "-I" + os.path.join(PKG, "csrc"), "-o", out,
                     os.path.join(ROOT, "tools", "f29_check.cpp")], check=True, capture_output=True)
 

@@ -122,9 +122,13 @@ def test_msm_g1_matches_oracle_pippenger(gpu_ctx):
     assert _g1_std(gpu_ctx.msm_g1(bases, _scal(ss))) == bn.msm(pts, ss)
 
 
+# every case at both window widths a key can take (csrc/msm_api.h msm_pick_c: 14 bits for small
+# keys, 16 for large ones; ZKFL_MSM_C forces one)
+@pytest.mark.parametrize("width", [14, 16])
 @pytest.mark.parametrize("case", ["zeros", "ones", "small", "neg", "dup", "cancel", "inf_base", "max", "binedge",
-                                  "binedge17"])
-def test_msm_g1_edge_cases(gpu_ctx, case):
+                                  "binedge17", "binedge14"])
+def test_msm_g1_edge_cases(gpu_ctx, monkeypatch, case, width):
+    monkeypatch.setenv("ZKFL_MSM_C", str(width))
     rnd = random.Random(zlib.crc32(case.encode()))
     n = 3000
     ks = [rnd.randrange(1, R) for _ in range(n)]
@@ -153,6 +157,10 @@ def test_msm_g1_edge_cases(gpu_ctx, case):
         # the signed-digit boundary 2^16 / 2^16 + 1 and the high-bin edges of 9 low bits
         edge = [1, 2, 511, 512, 513, 65535, 65536, 65537, 131071, 0]
         ss = [sum(rnd.choice(edge) << (17 * j) for j in range(15)) % R for _ in range(n)]
+    elif case == "binedge14":     # 14-bit windows: bucket 2^13 - 1, the signed-digit boundary
+        # 2^13 / 2^13 + 1 and the high-bin edges of 6 low bits
+        edge = [1, 2, 63, 64, 65, 127, 8191, 8192, 8193, 16383, 0]
+        ss = [sum(rnd.choice(edge) << (14 * j) for j in range(19)) % R for _ in range(n)]
     bases = bytearray(_bases_g1(gpu_ctx, ks))
     if case == "inf_base":
         for i in range(0, n, 3):
@@ -172,10 +180,12 @@ def test_msm_g2_identity(gpu_ctx, n):
     assert _g2_std(out) == bn.mul(bn.G2_GEN, _expect(ks, ss))
 
 
+@pytest.mark.parametrize("width", [14, 16])
 @pytest.mark.parametrize("case", ["zeros", "ones", "dup", "cancel", "neg", "inf_base"])
-def test_msm_g2_edge_cases(gpu_ctx, case):
+def test_msm_g2_edge_cases(gpu_ctx, monkeypatch, case, width):
     """G2 runs on lane pairs (csrc/field.h Fq2PairOps): the exceptional additions (P + P inside a
     bucket, P + (-P), infinity bases) and a single-bucket skew must stay pair-uniform."""
+    monkeypatch.setenv("ZKFL_MSM_C", str(width))
     rnd = random.Random(zlib.crc32(case.encode()))
     n = 1500
     ks = [rnd.randrange(1, R) for _ in range(n)]
@@ -365,15 +375,17 @@ def test_resident_batch_and_errors(gpu_ctx):
     key.close()
 
 
-@pytest.mark.parametrize("pairs", ["0", "1"])
-def test_batch_equals_single_proofs(gpu_ctx, monkeypatch, pairs):
+@pytest.mark.parametrize("pairs,width", [("0", "14"), ("1", "14"), ("0", "16"), ("1", "16")])
+def test_batch_equals_single_proofs(gpu_ctx, monkeypatch, pairs, width):
     """A 12-proof batch of a small key over 3 slots (the one-stream chain, every slot's later proofs
     graph-replayed; with ZKFL_FOLD=1 the folded s pi_A + r pi_B1 MSM, zkfl_key::bRS; with
     ZKFL_PAIRS=1 two proofs per chain, ProofPair: pair sorts over 2 NB bucket keys, per-half
     reductions) must equal the same proofs taken alone (the latency schedule, the GLV scalar
-    multiplications) byte for byte, and one of them the oracle's."""
+    multiplications) byte for byte, and one of them the oracle's -- at the small keys' 14-bit
+    windows (the default for this key) and at the large keys' 16."""
     from zkfl import clients, native, zkey
     monkeypatch.setenv("ZKFL_PAIRS", pairs)
+    monkeypatch.setenv("ZKFL_MSM_C", width)
     b, zk = _setup(gpu_ctx, "balance_unified", 8, 3, 4)
     key = native.ProvingKey(gpu_ctx, zk)
     wt = []

@@ -110,8 +110,11 @@ def breakdown(db, out, proofs=6):
     c = sqlite3.connect(db)
     starts = [r[0] for r in c.execute("select start from kernels where name like '%k_proof_start%' or name like '%k_set_extra%' order by start")]
     t0 = starts[-proofs]
-    rows = c.execute("select name, count(*), sum(end-start) from kernels where start >= ? group by name", (t0,)).fetchall()
-    span = c.execute("select max(end) - ? from kernels where start >= ?", (t0, t0)).fetchone()[0]
+    # the pass ends with its last proof's k_assemble (bench.py verifies the proofs afterwards)
+    t1 = c.execute("select max(end) from kernels where name like '%k_assemble(%'").fetchone()[0]
+    rows = c.execute("select name, count(*), sum(end-start) from kernels where start >= ? and end <= ? "
+                     "group by name", (t0, t1)).fetchall()
+    span = t1 - t0
     agg = {}
     for name, cnt, tot in rows:
         k = _short(name)
@@ -130,6 +133,7 @@ def breakdown(db, out, proofs=6):
 
 def _category(name):
     for key, cat in (("k_msm_accumulate<zkfl::FqOps", "acc_g1"), ("k_msm_accumulate<zkfl::Fq2", "acc_g2"),
+                     ("bin_", "sort"),
                      ("stitch", "stitch"), ("wsum", "reduce"), ("rocprim", "sort"),
                      ("k_ntt", "ntt"), ("k_abc", "abc"), ("assemble", "asm")):
         if key in name:
@@ -138,12 +142,12 @@ def _category(name):
 
 
 def timeline(db, out, step_us=10.0):
-    """Samples the window between the first accumulate of the timed region and the start of the
-    serialized roofline pass (its first k_set_extra is the 7th from last)."""
+    """Samples the window between the timed region and the start of the serialized roofline pass
+    (its first k_proof_start is the 6th from last)."""
     c = sqlite3.connect(db)
     ks = c.execute("select name, start, end from kernels order by start").fetchall()
-    sx = [k[1] for k in ks if "k_set_extra" in k[0]]
-    t_end = sx[-7]
+    sx = [k[1] for k in ks if "k_proof_start" in k[0]]
+    t_end = sx[-6]
     t_begin = sx[len(sx) // 4]  # skip warmup-ish quarter
     cats = {}
     for name, s0, e0 in ks:

@@ -197,6 +197,13 @@ ZK_HD F29 f29_below256(const F29& a) {
 #ifndef F29_PAIRED
 #define F29_PAIRED 1
 #endif
+// 1 (default): the madd's last products as a triple and a pair (f29_mont3), so no product of the
+// G1 madd joins split columns: formula 2,211 -> 2,194 VALU per entry (tools/isa_check.py census);
+// the G1 accumulation 1.5807 vs 1.5901 ms per proof alone (2 traced runs each), 429 vs 427 proofs/s
+// (4 same-box alternations, profiles/r05_ab_triple.log)
+#ifndef F29_TRIPLE
+#define F29_TRIPLE 1
+#endif
 ZK_HD void f29_keep(uint64_t& a) {
 #ifdef __HIP_DEVICE_COMPILE__
   asm volatile("" : "+v"(a));
@@ -367,6 +374,61 @@ ZK_HD F29x2 f29_mont2(const F29 (&xa)[NA], const F29 (&ya)[NA], const F29 (&xb)[
   return r;
 }
 
+// Three independent product sums side by side (as f29_mont2, no squares): one accumulator each per
+// column, so three chains and no joins.  Used by the madd for PPP | Q | ZZ3 (F29_TRIPLE).
+struct F29x3 {
+  F29 a, b, c;
+};
+template <int NA, int NB, int NC>
+ZK_HD F29x3 f29_mont3(const F29 (&xa)[NA], const F29 (&ya)[NA], const F29 (&xb)[NB], const F29 (&yb)[NB],
+                      const F29 (&xc)[NC], const F29 (&yc)[NC]) {
+  uint32_t ma[9], mb[9], mc[9];
+  F29x3 r;
+  uint64_t ca = 0, cb = 0, cc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t a = ca, b = cb, c = cc;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 8) continue;
+#pragma unroll
+      for (int q = 0; q < NA; q++) a += (uint64_t)xa[q].v[i] * ya[q].v[j];
+#pragma unroll
+      for (int q = 0; q < NB; q++) b += (uint64_t)xb[q].v[i] * yb[q].v[j];
+#pragma unroll
+      for (int q = 0; q < NC; q++) c += (uint64_t)xc[q].v[i] * yc[q].v[j];
+      if (i < k) {
+        a += (uint64_t)ma[i] * P29::P[j];
+        b += (uint64_t)mb[i] * P29::P[j];
+        c += (uint64_t)mc[i] * P29::P[j];
+      }
+    }
+    f29_keep(a);
+    f29_keep(b);
+    f29_keep(c);
+    if (k < 9) {
+      ma[k] = ((uint32_t)a * P29::NINV) & P29::MASK;
+      mb[k] = ((uint32_t)b * P29::NINV) & P29::MASK;
+      mc[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
+      a += (uint64_t)ma[k] * P29::P[0];
+      b += (uint64_t)mb[k] * P29::P[0];
+      c += (uint64_t)mc[k] * P29::P[0];
+    } else {
+      r.a.v[k - 9] = (uint32_t)a & P29::MASK;
+      r.b.v[k - 9] = (uint32_t)b & P29::MASK;
+      r.c.v[k - 9] = (uint32_t)c & P29::MASK;
+    }
+    ca = a >> 29;
+    cb = b >> 29;
+    cc = c >> 29;
+  }
+  r.a.v[8] = (uint32_t)ca;
+  r.b.v[8] = (uint32_t)cb;
+  r.c.v[8] = (uint32_t)cc;
+  return r;
+}
+
 // {a b, c d} (two independent products, f29_mont2)
 ZK_HD F29x2 f29_mul2(const F29& a, const F29& b, const F29& c, const F29& d) {
   const F29 xa[1] = {a}, ya[1] = {b}, xb[1] = {c}, yb[1] = {d};
@@ -519,6 +581,20 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
     }
     return f29_inf();
   }
+#if F29_TRIPLE
+  // PPP | Q | ZZ3 as three chains, then ZZZ3 | Y3 (Y3's two products in one accumulator): no
+  // column joins at all
+  const F29 x3a[1] = {P}, x3b[1] = {p.X}, x3c[1] = {p.ZZ}, y3[1] = {PP};
+  const F29x3 t3 = f29_mont3<1, 1, 1>(x3a, y3, x3b, y3, x3c, y3);
+  const F29 PPP = t3.a, Q = t3.b;
+  F29 X3 = f29_ksub3(P29::K4_3, RR, PPP, Q, Q);
+  f29_norm(X3);
+  const F29 QX = f29_ksub(P29::K6_1, Q, X3);
+  const F29 nY = f29_ksub(P29::K7_1, f29_zero(), p.Y);
+  const F29 xz[1] = {p.ZZZ}, yz[1] = {PPP}, xy[2] = {R, nY}, yy[2] = {QX, PPP};
+  const F29x2 zy = f29_mont2<1, 2, false, false>(xz, yz, xy, yy);
+  return {X3, zy.b, t3.c, zy.a};
+#else
   const F29x2 pq = f29_mul2(P, PP, p.X, PP);
   const F29 PPP = pq.a, Q = pq.b;
   const F29x2 zz = f29_mul2(p.ZZ, PP, p.ZZZ, PPP);
@@ -529,6 +605,7 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
   // the result as one aggregate: a named XYZZ filled member by member here kept two coordinates in
   // scratch memory (its slot merged with the early returns' through a pointer phi)
   return {X3, f29_mulsum2(R, QX, nY, PPP), zz.a, zz.b};
+#endif
 #else
   const F29 U2 = f29_mul(a.x, p.ZZ);
   const F29 S2 = f29_mul(a.y, p.ZZZ);

@@ -8,8 +8,8 @@
 //
 // MI355X design:
 //  * Bases are fixed per proving key, so at key-load time every base P_i is expanded into
-//    W window copies 2^(c j) P_i (affine, Montgomery; c = MSM_C bits, W = ceil(255 / c): 16 x 16
-//    or 15 x 17), laid out [i][j] (64 B / 128 B each).  One MSM is then a single bucket set:
+//    W window copies 2^(c j) P_i (affine, Montgomery; c bits per key, msm_pick_c: 16 x 16 or
+//    19 x 14 for small keys, W = ceil(255 / c)), laid out [i][j] (64 B / 128 B each).  One MSM is then a single bucket set:
 //    every (i, j) with a non-zero signed c-bit digit d_ij lands in bucket |d_ij|-1 (2^(c-1)
 //    buckets), no per-window bucket reduction and no window combination.  288 GB of HBM makes
 //    the Wx base expansion (~2 GB for the 2^18-constraint training circuit) free.
@@ -332,36 +332,37 @@ struct MsmCompute<Fq2Ops> {
 // ---------------------------------------------------------------------------
 // Key-load-time window expansion: out[i*W + j] = 2^(c j) * in[i]  (affine)
 // ---------------------------------------------------------------------------
-template <class F>
+template <class F, int C>
 __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__ in, size_t n, Affine<F>* __restrict__ out) {
+  constexpr int W = msm_w_of(C);
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   using T = typename F::T;
   Affine<F> p = in[i];
   if (aff_is_inf(p)) {
-    for (int j = 0; j < MSM_W; j++) out[i * MSM_W + j] = p;
+    for (int j = 0; j < W; j++) out[i * W + j] = p;
     return;
   }
   // Keep the W window copies in XYZZ in the output slots' scratch (global), with a
   // Montgomery batch inversion of their ZZZ over the 16 copies.
   XYZZ<F> acc = xyzz_from_affine<F>(p);
-  T pref[MSM_W];
-  XYZZ<F> pts[MSM_W];
-  for (int j = 0; j < MSM_W; j++) {
+  T pref[W];
+  XYZZ<F> pts[W];
+  for (int j = 0; j < W; j++) {
     pts[j] = acc;
     pref[j] = (j == 0) ? acc.ZZZ : F::mul(pref[j - 1], acc.ZZZ);
-    if (j + 1 < MSM_W)
-      for (int k = 0; k < MSM_C; k++) acc = xyzz_dbl<F>(acc);
+    if (j + 1 < W)
+      for (int k = 0; k < C; k++) acc = xyzz_dbl<F>(acc);
   }
-  T inv = F::inv(pref[MSM_W - 1]);
-  for (int j = MSM_W - 1; j >= 0; j--) {
+  T inv = F::inv(pref[W - 1]);
+  for (int j = W - 1; j >= 0; j--) {
     T iZZZ = (j == 0) ? inv : F::mul(inv, pref[j - 1]);
     if (j > 0) inv = F::mul(inv, pts[j].ZZZ);
     T iZ = F::mul(pts[j].ZZ, iZZZ);
     Affine<F> a;
     a.x = F::mul(pts[j].X, F::sqr(iZ));
     a.y = F::mul(pts[j].Y, iZZZ);
-    out[i * MSM_W + j] = a;
+    out[i * W + j] = a;
   }
 }
 
@@ -370,22 +371,25 @@ __global__ void __launch_bounds__(64) k_msm_expand(const Affine<F>* __restrict__
 // ---------------------------------------------------------------------------
 // Window j of a 256-bit scalar (8 x 32-bit words): bits [c j, c j + c) (j is unrolled, so the
 // word index and shifts are constants).
+template <int C>
 ZK_DEV uint32_t msm_window(const uint32_t (&s)[8], int j) {
-  const int b = MSM_C * j, w = b >> 5, sh = b & 31;
+  const int b = C * j, w = b >> 5, sh = b & 31;
   uint32_t x = s[w] >> sh;
-  if (sh + MSM_C > 32 && w + 1 < 8) x |= s[w + 1] << (32 - sh);
-  return x & ((1u << MSM_C) - 1u);
+  if (sh + C > 32 && w + 1 < 8) x |= s[w + 1] << (32 - sh);
+  return x & ((1u << C) - 1u);
 }
 
 // Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31, written
 // window-major (position j*n + i: consecutive lanes store consecutive words; the sort that
 // follows does not care about the input order).  Also counts the non-zero digits into *nnz
 // (the sorted prefix the accumulation covers).
-static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
+template <int C>
+__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
                                                            const uint32_t* __restrict__ extra,
                                                            const uint32_t* __restrict__ sidx, uint32_t extra_start,
                                                            size_t n, uint16_t* __restrict__ keys,
                                                            uint32_t* __restrict__ vals, uint32_t* __restrict__ nnz) {
+  constexpr int W = msm_w_of(C), NB = msm_nb_of(C);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cnt = 0;
   if (i < n) {
@@ -396,11 +400,11 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
     uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     uint32_t carry = 0;
 #pragma unroll
-    for (int j = 0; j < MSM_W; j++) {
-      uint32_t raw = msm_window(s, j);
+    for (int j = 0; j < W; j++) {
+      uint32_t raw = msm_window<C>(s, j);
       int32_t d = (int32_t)(raw + carry);
-      if (d > MSM_NB) {
-        d -= (1 << MSM_C);
+      if (d > NB) {
+        d -= (1 << C);
         carry = 1;
       } else {
         carry = 0;
@@ -409,7 +413,7 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
       if (d != 0) {
         const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
         key = mag - 1;
-        val = (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u);
+        val = (uint32_t)(i * W + j) | (d < 0 ? 0x80000000u : 0u);
         cnt++;
       }
       keys[(size_t)j * n + i] = (uint16_t)key;
@@ -441,15 +445,20 @@ static __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __res
 // reduction takes each half apart (msm_tails_pair).  The high bins stay MSM_SORT_HB: a pair sorts
 // one more low bit inside each (MSM_SORT_LB + 1).
 constexpr int MSM_SORT_T = 256;           // threads per block in count / scatter
-constexpr int MSM_SORT_LB = MSM_SORT_LOW_BITS;       // key bits sorted inside a high bin
-constexpr int MSM_SORT_NL = 1 << MSM_SORT_LB;        // low counters per high-bin workgroup
-static_assert(MSM_C <= 16, "proof pairs: 2 NB bucket keys in a u16");
-constexpr int MSM_SORT_HB = MSM_NB >> MSM_SORT_LB;   // high bins
+constexpr int MSM_SORT_HB = 1 << MSM_SORT_HIGH_BITS; // high bins (every window width)
+// key bits sorted inside a high bin of a P-proof sort at window width C, and its low counters
+template <int C, int P>
+constexpr int msm_sort_lb() {
+  return C - 1 - MSM_SORT_HIGH_BITS + P - 1;
+}
+template <int C, int P>
+constexpr int msm_sort_nl() {
+  return 1 << msm_sort_lb<C, P>();
+}
 constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
-static_assert(MSM_SORT_NL >= 64 && MSM_SORT_NL <= 512 && MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
+static_assert(MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
 constexpr int MSM_SORT_BT = 1024;         // threads of the scan workgroup
 constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin workgroup
-static_assert(MSM_SORT_BINT >= MSM_SORT_NL && MSM_SORT_BINT <= 1024, "bins: one thread per low counter");
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
 // The scalars of one sort: proof p's scalar vector and extra slots (p < P)
@@ -460,14 +469,16 @@ struct MsmScalars {
 
 // Signed digits of virtual base v (base i = v mod n of proof p = v / n): fn(key, val) for every
 // non-zero digit, key = bucket + p NB (as k_msm_digits for P = 1).
-template <int P, class Fn>
+template <int C, int P, class Fn>
 ZK_DEV void msm_for_digits(const MsmScalars& S, const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t n,
                            size_t v, Fn&& fn) {
+  static_assert(P == 1 || C <= 16, "proof pairs: 2 NB bucket keys in a u16");
+  constexpr int W = msm_w_of(C), NB = msm_nb_of(C);
   const uint32_t p = P > 1 && v >= n ? 1u : 0u;
   const size_t i = v - p * n;
   const uint32_t* __restrict__ scalars = P > 1 && p ? S.sc[1] : S.sc[0];
   const uint32_t* __restrict__ extra = P > 1 && p ? S.ex[1] : S.ex[0];
-  const uint32_t koff = p * MSM_NB;
+  const uint32_t koff = p * NB;
   const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
   const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
   const uint4* sp = reinterpret_cast<const uint4*>(src);
@@ -475,32 +486,32 @@ ZK_DEV void msm_for_digits(const MsmScalars& S, const uint32_t* __restrict__ sid
   const uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t carry = 0;
 #pragma unroll
-  for (int j = 0; j < MSM_W; j++) {
-    const uint32_t raw = msm_window(s, j);
+  for (int j = 0; j < W; j++) {
+    const uint32_t raw = msm_window<C>(s, j);
     int32_t d = (int32_t)(raw + carry);
-    carry = d > MSM_NB ? 1u : 0u;
-    if (carry) d -= (1 << MSM_C);
+    carry = d > NB ? 1u : 0u;
+    if (carry) d -= (1 << C);
     if (d != 0) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      fn(koff + mag - 1, (uint32_t)(i * MSM_W + j) | (d < 0 ? 0x80000000u : 0u));
+      fn(koff + mag - 1, (uint32_t)(i * W + j) | (d < 0 ? 0x80000000u : 0u));
     }
   }
 }
 
 // n: bases per proof; the blocks cover the P n virtual bases
-template <int P>
+template <int C, int P>
 __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const MsmScalars S, const uint32_t* __restrict__ sidx,
                                                             uint32_t extra_start, size_t n, size_t per_blk,
                                                             uint32_t* __restrict__ cnt) {
   ZK_WT(WT_SORT_COUNT);
   ZK_LIGHT();
-  constexpr int LB = MSM_SORT_LB + P - 1;
+  constexpr int LB = msm_sort_lb<C, P>();
   __shared__ uint32_t h[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
   __syncthreads();
   const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
+    msm_for_digits<C, P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
   __syncthreads();
   if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
@@ -555,20 +566,20 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* _
   }
 }
 
-template <int P>
+template <int C, int P>
 __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const MsmScalars S, const uint32_t* __restrict__ sidx,
                                                               uint32_t extra_start, size_t n, size_t per_blk,
                                                               const uint32_t* __restrict__ cnt,
                                                               uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   ZK_WT(WT_SORT_SCATTER);
   ZK_LIGHT();
-  constexpr int LB = MSM_SORT_LB + P - 1;
+  constexpr int LB = msm_sort_lb<C, P>();
   __shared__ uint32_t cur[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
   const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t val) {
+    msm_for_digits<C, P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t val) {
       const uint32_t p = atomicAdd(&cur[key >> LB], 1u);
       keys[p] = (uint16_t)key;
       vals[p] = val;
@@ -578,7 +589,7 @@ __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const MsmScalars
 // One workgroup per high bin: [bin_start[b], bin_start[b+1]) of (tk, tv) -> buckets in (ko, vo).
 // BINT threads per workgroup (MSM_SORT_BINT).  A 256-thread variant for small MSMs measured
 // neutral on config 5 (1906.7 vs 1894.0 proofs/s, 3 alternations, profiles/r04_ab_c5_small_keys.log).
-template <int BINT, int NL = MSM_SORT_NL>
+template <int BINT, int NL>
 __global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
                                                       const uint16_t* __restrict__ tk,
                                                       const uint32_t* __restrict__ tv,
@@ -800,6 +811,7 @@ struct MsmTailArgs {
   XYZZ<S>* out[MSM_TAIL_MAX];
   uint32_t* live[MSM_TAIL_MAX];
   uint32_t target[MSM_TAIL_MAX];
+  int c;  // window bits of every MSM in the batch
 };
 
 // Zero the buckets (ZZ = 0: infinity) and the nnz counter of every tail in the batch: one launch
@@ -810,7 +822,7 @@ __global__ void __launch_bounds__(256) k_msm_tail_reset(const MsmTailArgs<S> ta)
   ZK_LIGHT();
   const int y = blockIdx.y;
   uint4* b = reinterpret_cast<uint4*>(ta.buckets[y]);
-  constexpr size_t nv = MSM_NB * sizeof(XYZZ<S>) / sizeof(uint4);
+  const size_t nv = (size_t)msm_nb_of(ta.c) * sizeof(XYZZ<S>) / sizeof(uint4);
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
     b[i] = make_uint4(0, 0, 0, 0);
   if (blockIdx.x == 0 && threadIdx.x == 0) *const_cast<uint32_t*>(ta.nnz[y]) = 0;
@@ -917,21 +929,26 @@ constexpr int msm_wsum_q0() {
   return sizeof(typename S::T) == 32 ? MSM_G1_WSUM_Q : MSM_G2_WSUM_Q;
 }
 // Q0 of the latency schedule's reduction (one proof alone, msm_tails(..., fast = true)): 128
-// level-0 blocks (4 buckets per lane at c = 16), a 128-lane level 1 -- about 45 dependent point
-// operations on the chain instead of ~70, for ~1.8x the reduction's (small) work
-constexpr int MSM_WSUM_Q_FAST = MSM_NB / (MSM_RB * 128);  // 128 level-0 blocks: 4 at c = 16, 8 at c = 17
-// lanes of a reduction block: level 0 one wave (MSM_RB), level 1 one lane per level-0 block
-template <bool L0, int Q0>
-constexpr int msm_wsum_rb() {
-  return L0 || MSM_NB / (MSM_RB * Q0) <= MSM_RB ? MSM_RB : MSM_NB / (MSM_RB * Q0);
+// level-0 blocks (4 buckets per lane at c = 16, 1 at c = 14), a 128-lane level 1 -- about 45
+// dependent point operations on the chain instead of ~70, for ~1.8x the reduction's (small) work
+template <int C>
+constexpr int msm_wsum_q_fast() {
+  return msm_nb_of(C) / (MSM_RB * 128);
 }
-static_assert(MSM_NB % (MSM_RB * MSM_G1_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G1_WSUM_Q) <= MSM_RB &&
-                  MSM_NB % (MSM_RB * MSM_G2_WSUM_Q) == 0 && MSM_NB / (MSM_RB * MSM_G2_WSUM_Q) <= MSM_RB &&
-                  MSM_NB % (MSM_RB * MSM_WSUM_Q_FAST) == 0 && msm_wsum_rb<false, MSM_WSUM_Q_FAST>() <= 2 * MSM_RB,
-              "two reduction levels cover the buckets; red_a / red_s hold 2 x the level-1 block");
-template <class F, int MINW, bool L0, int Q0, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__((msm_wsum_rb<L0, Q0>() * MsmIO<F>::LANES)) __attribute__((amdgpu_waves_per_eu(MINW)))
+// lanes of a reduction block: level 0 one wave (MSM_RB), level 1 one lane per level-0 block
+template <bool L0, int Q0, int C>
+constexpr int msm_wsum_rb() {
+  return L0 || msm_nb_of(C) / (MSM_RB * Q0) <= MSM_RB ? MSM_RB : msm_nb_of(C) / (MSM_RB * Q0);
+}
+template <int Q0, int C>
+constexpr bool msm_wsum_fits() {
+  return Q0 >= 1 && msm_nb_of(C) % (MSM_RB * Q0) == 0 && msm_wsum_rb<false, Q0, C>() <= 2 * MSM_RB;
+}
+template <class F, int MINW, bool L0, int Q0, int C, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__((msm_wsum_rb<L0, Q0, C>() * MsmIO<F>::LANES)) __attribute__((amdgpu_waves_per_eu(MINW)))
 k_msm_wsum(const MsmTailArgs<S> ta) {
+  static_assert(msm_wsum_fits<Q0, C>(), "two reduction levels cover the buckets; red_a / red_s hold 2 x the level-1 block");
+  constexpr int NB = msm_nb_of(C);
   ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
   ZK_LIGHT();
   // One kernel per level (template L0): level 0 keeps only the running sums R, W live through its
@@ -939,9 +956,9 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
   const int yb = blockIdx.y;
   const XYZZ<S>* __restrict__ in_a = L0 ? ta.buckets[yb] : ta.red_a[yb];
   const XYZZ<S>* __restrict__ in_s = L0 ? ta.buckets[yb] : ta.red_s[yb];
-  constexpr int B0 = MSM_NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
-  constexpr int RB = msm_wsum_rb<L0, Q0>();
-  constexpr int N = L0 ? MSM_NB : B0, Q = L0 ? Q0 : 1;
+  constexpr int B0 = NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
+  constexpr int RB = msm_wsum_rb<L0, Q0, C>();
+  constexpr int N = L0 ? NB : B0, Q = L0 ? Q0 : 1;
   constexpr int log2g = L0 ? 0 : __builtin_ctz((unsigned)(Q0 * MSM_RB));
   XYZZ<S>* __restrict__ out_a = L0 ? ta.red_a[yb] : ta.out[yb];
   XYZZ<S>* __restrict__ out_s = L0 ? ta.red_s[yb] : ta.red_s[yb] + RB;
@@ -1002,11 +1019,23 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
 // ---------------------------------------------------------------------------
 // Host-side plan
 // ---------------------------------------------------------------------------
+// fn(std::integral_constant<int, C>) for the window width c of a base set (MSM_C or MSM_C_SMALL:
+// the widths whose kernels are instantiated)
+template <class Fn>
+hipError_t msm_with_c(int c, Fn&& fn) {
+  if (c == MSM_C) return fn(std::integral_constant<int, MSM_C>());
+  if constexpr (MSM_C_SMALL != MSM_C)
+    if (c == MSM_C_SMALL) return fn(std::integral_constant<int, MSM_C_SMALL>());
+  return hipErrorInvalidValue;
+}
+
 template <class F>
-hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n) {
+hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n, int c) {
+  if (c != MSM_C && c != MSM_C_SMALL) return hipErrorInvalidValue;
   b.n = n;
+  b.c = c;
   using IO = MsmIO<typename MsmCompute<F>::type>;
-  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * MSM_W * IO::REC * sizeof(Affine<F>)));
+  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * msm_w_of(c) * IO::REC * sizeof(Affine<F>)));
   return hipSuccess;
 }
 
@@ -1029,20 +1058,27 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
     ZK_CHECK(hipMemcpyAsync(b.sidx, h_sidx, b.n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   using FC = typename MsmCompute<F>::type;
+  const size_t m = b.n * msm_w_of(b.c);
+  auto expand = [&](Affine<F>* out) {
+    return msm_with_c(b.c, [&](auto cc) {
+      hipLaunchKernelGGL((k_msm_expand<F, decltype(cc)::value>), dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases,
+                         b.n, out);
+      return hipSuccess;
+    });
+  };
   if constexpr (MsmIO<FC>::REC == 2) {  // MSM_G1_PACKED: expand into a temporary table, then pack
-    const size_t m = b.n * MSM_W;
     if (!m) return hipGetLastError();
     Affine<F>* tmp = nullptr;
     ZK_CHECK(hipMallocAsync(reinterpret_cast<void**>(&tmp), m * sizeof(Affine<F>), st));
-    hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, tmp);
+    ZK_CHECK(expand(tmp));
     hipLaunchKernelGGL(k_msm_pack29, dim3(zk_grid(m, 256)), dim3(256), 0, st, tmp, m,
                        reinterpret_cast<uint32_t*>(b.bases_w));
     ZK_CHECK(hipFreeAsync(tmp, st));
     return hipGetLastError();
   }
-  if (b.n) hipLaunchKernelGGL(k_msm_expand<F>, dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases, b.n, b.bases_w);
+  if (b.n) ZK_CHECK(expand(b.bases_w));
   if constexpr (std::is_same<FC, FqOps29>::value || std::is_same<FC, Fq2Pair29>::value) {
-    const size_t nfq = b.n * MSM_W * (sizeof(Affine<F>) / sizeof(Fq));
+    const size_t nfq = m * (sizeof(Affine<F>) / sizeof(Fq));
     if (nfq)
       hipLaunchKernelGGL(k_msm_to_m29, dim3(zk_grid(nfq, 256)), dim3(256), 0, st, reinterpret_cast<Fq*>(b.bases_w), nfq);
   }
@@ -1050,9 +1086,10 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
 }
 
 template <class F>
-hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
+hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, int c, hipStream_t st) {
   s.cap = cap;
-  const size_t m = cap * MSM_W;
+  s.c = c;
+  const size_t m = cap * msm_w_of(c);
   ZK_CHECK(hipMalloc(&s.keys_in, m * sizeof(uint16_t)));
   ZK_CHECK(hipMalloc(&s.keys_out, m * sizeof(uint16_t)));
   ZK_CHECK(hipMalloc(&s.vals_in, m * sizeof(uint32_t)));
@@ -1065,7 +1102,7 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, hipStream_t st) {
 #endif
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
   if constexpr (std::is_same<F, FqOps>::value)
-    if (MSM_G1_AFFINE) ZK_CHECK(msm_aff_alloc(s.aff, cap));
+    if (MSM_G1_AFFINE) ZK_CHECK(msm_aff_alloc(s.aff, m));
   return hipSuccess;
 }
 
@@ -1118,8 +1155,10 @@ uint32_t msm_tail_l0(size_t cap) {
 // pairs = 2: the tail of a proof pair (msm_sort_pair): cap = both proofs' bases, 2 NB buckets and
 // reduction scratch per half
 template <class F>
-hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int pairs = 1) {
-  const size_t m = cap * MSM_W;
+hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int c, int pairs = 1) {
+  if (c != MSM_C && c != MSM_C_SMALL) return hipErrorInvalidValue;
+  t.c = c;
+  const size_t m = cap * msm_w_of(c);
   t.target = std::min<uint32_t>(msm_resident_chunks<F>(), 0xFFFFFFu);
   t.l0 = msm_tail_l0<F>(cap);
   // the batch-affine rounds write their items with the fixed AFF_L: the stitching levels must count
@@ -1134,7 +1173,7 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int pairs = 1) {
     ZK_CHECK(hipMalloc(&t.item_key[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(uint32_t)));
     ZK_CHECK(hipMalloc(&t.item_val[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(XYZZ<F>)));
   }
-  ZK_CHECK(hipMalloc(&t.buckets, pairs * MSM_NB * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.buckets, pairs * msm_nb_of(c) * sizeof(XYZZ<F>)));
   // <= 2 level-1 blocks (fast: 128 lanes) per half
   ZK_CHECK(hipMalloc(&t.red_a, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.red_s, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
@@ -1152,9 +1191,11 @@ void msm_tail_free(MsmTail<F>& t) {
   t = MsmTail<F>();
 }
 
+// (one window width per batch: msm_tails_* reject a batch that mixes them)
 template <class F>
 MsmTailArgs<F> msm_tail_args(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n) {
   MsmTailArgs<F> ta = {};
+  ta.c = n > 0 ? t[0]->c : MSM_C;
   for (int i = 0; i < n; i++) {
     for (int k = 0; k < 2; k++) {
       ta.key[i][k] = t[i]->item_key[k];
@@ -1173,8 +1214,15 @@ MsmTailArgs<F> msm_tail_args(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n) 
 
 // Empty buckets and zero nnz for n tails (before their accumulations).
 template <class F>
+bool msm_tails_one_c(MsmTail<F>* const* t, int n) {
+  for (int i = 1; i < n; i++)
+    if (t[i]->c != t[0]->c) return false;
+  return true;
+}
+
+template <class F>
 hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
-  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  if (n < 1 || n > MSM_TAIL_MAX || !msm_tails_one_c(t, n)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_msm_tail_reset<F>, dim3(128, n), dim3(256), 0, st, msm_tail_args<F>(t, nullptr, n));
   return hipGetLastError();
 }
@@ -1193,19 +1241,24 @@ hipError_t msm_sort_p(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, co
                              : ((nv + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
   const uint32_t nblk = (uint32_t)((nv + per_blk - 1) / per_blk);
   if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
+  if (b.c != pl.c) return hipErrorInvalidValue;
   uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
   uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
-  hipLaunchKernelGGL(k_msm_bin_count<P>, dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n, per_blk,
-                     cnt);
-  hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
-  if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
-    pl.ko_sorted = 1;
-    hipLaunchKernelGGL(k_msm_bin_scatter<P>, dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
-                       per_blk, cnt, pl.keys_in, pl.vals_in);
-    hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, (MSM_SORT_NL << (P - 1))>), dim3(MSM_SORT_HB),
-                       dim3(MSM_SORT_BINT), 0, st, bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
-  }
-  return hipGetLastError();
+  return msm_with_c(b.c, [&](auto cc) {
+    constexpr int C = decltype(cc)::value, NL = msm_sort_nl<C, P>();
+    static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
+    hipLaunchKernelGGL((k_msm_bin_count<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
+                       per_blk, cnt);
+    hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
+    if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
+      pl.ko_sorted = 1;
+      hipLaunchKernelGGL((k_msm_bin_scatter<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start,
+                         b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
+      hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
+                         bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+    }
+    return hipGetLastError();
+  });
 }
 
 template <class F>
@@ -1215,14 +1268,17 @@ hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, cons
   const MsmScalars S = {{d_scalars, nullptr}, {d_extra, nullptr}};
   return msm_sort_p<1>(b, pl, nnz, S, st);
 #else
-  if (b.n > pl.cap) return hipErrorInvalidValue;
+  if (b.n > pl.cap || b.c != pl.c) return hipErrorInvalidValue;
   if (b.n == 0) return hipSuccess;
-  const size_t m = b.n * MSM_W;
+  const size_t m = b.n * msm_w_of(b.c);
   size_t need = 0;
   ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
   if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_msm_digits, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars, d_extra, b.sidx,
-                     b.extra_start, b.n, pl.keys_in, pl.vals_in, nnz);
+  ZK_CHECK(msm_with_c(b.c, [&](auto cc) {
+    hipLaunchKernelGGL(k_msm_digits<decltype(cc)::value>, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars,
+                       d_extra, b.sidx, b.extra_start, b.n, pl.keys_in, pl.vals_in, nnz);
+    return hipSuccess;
+  }));
   if (!(ZK_KNOCKOUT & 2))
     ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
                                        st));
@@ -1238,7 +1294,8 @@ template <class F>
 hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, MsmTail<F>& t,
                                  hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr, int pairs = 1) {
   if (b.n == 0) return hipSuccess;
-  const size_t m = pairs * b.n * MSM_W;
+  if (b.c != t.c) return hipErrorInvalidValue;
+  const size_t m = pairs * b.n * msm_w_of(b.c);
   size_t chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) chunks = std::min<size_t>(chunks, t.target);  // lanes of msm_chunk_len(nnz, target)
   if (chunks > t.max_chunks) return hipErrorInvalidValue;
@@ -1283,7 +1340,7 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
 // reduction (MSM_WSUM_Q_FAST: shorter dependent chain, more waves).
 template <class F>
 hipError_t msm_stitch(MsmTail<F>* const* t, int n, hipStream_t st) {
-  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  if (n < 1 || n > MSM_TAIL_MAX || !msm_tails_one_c(t, n)) return hipErrorInvalidValue;
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int SW = sizeof(typename F::T) == 32 ? MSM_G1_STITCH_WAVES : MSM_G2_TAIL_WAVES;
@@ -1316,15 +1373,20 @@ hipError_t msm_wsum(const MsmTailArgs<F>& ta, int n, hipStream_t st, bool fast) 
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int TW = sizeof(typename F::T) == 32 ? MSM_G1_TAIL_WAVES : MSM_G2_TAIL_WAVES;
-  constexpr int Q0 = msm_wsum_q0<F>(), QF = MSM_WSUM_Q_FAST;
-  if (fast) {
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, QF>), dim3(MSM_NB / (MSM_RB * QF), n), dim3(MSM_RB * LN), 0, st, ta);
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, QF>), dim3(1, n), dim3(msm_wsum_rb<false, QF>() * LN), 0, st, ta);
-  } else {
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, Q0>), dim3(MSM_NB / (MSM_RB * Q0), n), dim3(MSM_RB * LN), 0, st, ta);
-    hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, Q0>), dim3(1, n), dim3(msm_wsum_rb<false, Q0>() * LN), 0, st, ta);
-  }
-  return hipGetLastError();
+  return msm_with_c(ta.c, [&](auto cc) {
+    constexpr int C = decltype(cc)::value, NB = msm_nb_of(C);
+    constexpr int Q0 = msm_wsum_q0<F>(), QF = msm_wsum_q_fast<C>();
+    if (fast) {
+      hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, QF, C>), dim3(NB / (MSM_RB * QF), n), dim3(MSM_RB * LN), 0, st, ta);
+      hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, QF, C>), dim3(1, n), dim3(msm_wsum_rb<false, QF, C>() * LN), 0, st,
+                         ta);
+    } else {
+      hipLaunchKernelGGL((k_msm_wsum<FC, TW, true, Q0, C>), dim3(NB / (MSM_RB * Q0), n), dim3(MSM_RB * LN), 0, st, ta);
+      hipLaunchKernelGGL((k_msm_wsum<FC, TW, false, Q0, C>), dim3(1, n), dim3(msm_wsum_rb<false, Q0, C>() * LN), 0, st,
+                         ta);
+    }
+    return hipGetLastError();
+  });
 }
 
 template <class F>
@@ -1341,10 +1403,11 @@ hipError_t msm_tails_pair(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hip
   if (2 * n > MSM_TAIL_MAX) return hipErrorInvalidValue;
   ZK_CHECK(msm_stitch(t, n, st));
   MsmTailArgs<F> ta = {};
+  ta.c = t[0]->c;
   for (int i = 0; i < n; i++)
     for (int h = 0; h < 2; h++) {
       const int y = 2 * i + h;
-      ta.buckets[y] = t[i]->buckets + (size_t)h * MSM_NB;
+      ta.buckets[y] = t[i]->buckets + (size_t)h * msm_nb_of(ta.c);
       ta.red_a[y] = t[i]->red_a + (size_t)h * MSM_TAIL_RED;
       ta.red_s[y] = t[i]->red_s + (size_t)h * MSM_TAIL_RED;
       ta.out[y] = outs[y];
@@ -1365,18 +1428,20 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
 // Non-template entry points (one translation unit per curve: msm_g1.hip / msm_g2.hip).
 #define ZKFL_MSM_DEFINE(SUF, F)                                                                          \
   hipError_t zk_wtrace_bind_##SUF(const WtBuf& b) { return zk_wtrace_bind_tu(b); }                      \
-  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n) { return msm_bases_alloc(b, n); }           \
+  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n, int c) { return msm_bases_alloc(b, n, c); } \
   hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,          \
                                  uint32_t extra_start, hipStream_t st) {                                 \
     return msm_bases_set(b, src, h_sidx, extra_start, st);                                               \
   }                                                                                                      \
   void msm_bases_free_##SUF(MsmBases<F>& b) { msm_bases_free(b); }                                       \
-  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st) {                     \
-    return msm_scratch_alloc(s, cap, st);                                                                \
+  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, int c, hipStream_t st) {              \
+    return msm_scratch_alloc(s, cap, c, st);                                                             \
   }                                                                                                      \
   void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
-  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap) { return msm_tail_alloc(t, cap); }          \
-  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap) { return msm_tail_alloc(t, cap, 2); }  \
+  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap, int c) { return msm_tail_alloc(t, cap, c); } \
+  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap, int c) {                               \
+    return msm_tail_alloc(t, cap, c, 2);                                                                 \
+  }                                                                                                      \
   hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0,  \
                                  const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st) { \
     const MsmScalars S = {{sc0, sc1}, {ex0, ex1}};                                                       \

@@ -338,8 +338,9 @@ __global__ void __launch_bounds__(AFF_WG) __attribute__((amdgpu_waves_per_eu(MIN
   if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
 }
 
-inline hipError_t msm_aff_alloc(MsmAffScratch& s, size_t cap_bases) {
-  s.lanes = (cap_bases * MSM_W + AFF_L - 1) / AFF_L;
+// entries: the most (base, window) pairs one accumulation covers (cap x W)
+inline hipError_t msm_aff_alloc(MsmAffScratch& s, size_t entries) {
+  s.lanes = (entries + AFF_L - 1) / AFF_L;
   s.wgs = (s.lanes + AFF_WG - 1) / AFF_WG;
   s.lanes = s.wgs * AFF_WG;
   if (s.wgs > (size_t)AFF_ROOT_T * AFF_ROOT_K) return hipErrorInvalidValue;
@@ -367,7 +368,7 @@ inline void msm_aff_free(MsmAffScratch& s) {
 template <int MINW>
 hipError_t msm_aff_accumulate(const MsmBases<FqOps>& b, const uint16_t* keys, const uint32_t* vals,
                               MsmTail<FqOps>& t, const MsmAffScratch& s, hipStream_t st) {
-  const size_t lanes = (b.n * MSM_W + AFF_L - 1) / AFF_L;
+  const size_t lanes = (b.n * msm_w_of(b.c) + AFF_L - 1) / AFF_L;
   const uint32_t wgs = (uint32_t)((lanes + AFF_WG - 1) / AFF_WG);
   if (wgs > s.wgs || lanes > t.max_chunks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_aff_prep1, dim3(wgs), dim3(AFF_WG), 0, st, keys, vals, b.bases_w, t.nnz, s);

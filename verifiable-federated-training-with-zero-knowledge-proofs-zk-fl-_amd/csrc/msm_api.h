@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "curve.h"
 #include "prof.h"
@@ -10,17 +12,33 @@ namespace zkfl {
 
 // Window width c of the signed-digit decomposition.  Scalars are < r < 2^254; with signed digits
 // d in [-(2^(c-1) - 1), 2^(c-1)] the top window absorbs the last carry when c W >= 255, so
-// W = ceil(255 / c): 16 windows at c = 16, 15 at c = 17.  Every base is expanded into its W window
-// copies at key load, so an MSM accumulates one entry per non-zero digit into ONE set of 2^(c-1)
-// buckets; c = 17 cuts the entries of a full-width scalar by 1/16 and doubles the buckets the
-// reduction folds.  Bucket keys are |d| - 1 < 2^(c-1), a u16 for c <= 17.
+// W = ceil(255 / c): 19 windows at c = 14, 16 at c = 16, 15 at c = 17.  Every base is expanded into
+// its W window copies at key load, so an MSM accumulates one entry per non-zero digit into ONE set
+// of 2^(c-1) buckets: a wider window cuts the entries of a full-width scalar and multiplies the
+// buckets the (latency-bound) reduction folds.  Bucket keys are |d| - 1 < 2^(c-1),
+// a u16 for c <= 17.
+// The width is chosen per MSM base set (per proving key: msm_pick_c): MSM_C for large keys, where
+// the accumulation dominates, MSM_C_SMALL for keys of at most MSM_SMALL_C_BASES bases, whose
+// proofs are chains of latency-bound reduction launches (config 5: 2,335 vs 2,152 proofs/s at 14
+// vs 16 bits, the metric key 388 vs 427 -- profiles/r05_ab_window_bits.log).
 #ifndef MSM_WINDOW_BITS
 #define MSM_WINDOW_BITS 16
 #endif
-constexpr int MSM_C = MSM_WINDOW_BITS;     // window bits
-constexpr int MSM_W = (255 + MSM_C - 1) / MSM_C;  // windows covering the 254-bit scalars + the last carry
-constexpr int MSM_NB = 1 << (MSM_C - 1);   // buckets (signed digits)
-static_assert(MSM_C >= 12 && MSM_C <= 17 && MSM_C * MSM_W >= 255, "window width: u16 bucket keys, 254-bit scalars");
+#ifndef MSM_WINDOW_BITS_SMALL
+#define MSM_WINDOW_BITS_SMALL 14
+#endif
+#ifndef MSM_SMALL_C_BASES
+#define MSM_SMALL_C_BASES (1 << 16)
+#endif
+constexpr int MSM_C = MSM_WINDOW_BITS;     // window bits of large keys
+constexpr int MSM_C_SMALL = MSM_WINDOW_BITS_SMALL;
+__host__ __device__ constexpr int msm_w_of(int c) { return (255 + c - 1) / c; }  // windows: 254-bit scalars + the last carry
+__host__ __device__ constexpr int msm_nb_of(int c) { return 1 << (c - 1); }     // buckets (signed digits)
+constexpr int MSM_W = msm_w_of(MSM_C);
+constexpr int MSM_NB = msm_nb_of(MSM_C);
+constexpr int MSM_W_MAX = msm_w_of(MSM_C < MSM_C_SMALL ? MSM_C : MSM_C_SMALL);
+static_assert(MSM_C >= 14 && MSM_C <= 17 && MSM_C_SMALL >= 14 && MSM_C_SMALL <= 16,
+              "window width: u16 bucket keys, >= 64 low counters per high bin of the bucket sort");
 // Knock-out builds for marginal-cost measurements (tools/ko_probe.py; proofs are WRONG, timing
 // only): 1 assembly, 2 digit sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
 // 64 the G1 accumulation kernel.  0 in every real build; a non-zero value only compiles together
@@ -38,10 +56,10 @@ static_assert(MSM_C >= 12 && MSM_C <= 17 && MSM_C * MSM_W >= 255, "window width:
 #endif
 // the rocPRIM path keys zero digits MSM_KEY_NONE = 0xFFFF, a real bucket at c = 17
 static_assert(!MSM_SORT_ROCPRIM || MSM_C <= 16, "rocPRIM digit sort: c <= 16");
-// key bits sorted inside one high bin of the bucket sort (c - 1 - LOW_BITS high bits: 128 high
-// bins at c = 16 with 8, at c = 17 with 9)
-#ifndef MSM_SORT_LOW_BITS
-#define MSM_SORT_LOW_BITS (MSM_C - 8)
+// high key bits of the bucket sort (its high bins, every window width): the low c - 1 - HIGH_BITS
+// bits are sorted inside one high bin (6 at c = 14, 8 at c = 16, 9 at c = 17)
+#ifndef MSM_SORT_HIGH_BITS
+#define MSM_SORT_HIGH_BITS 7
 #endif
 // pairs of one high bin staged in LDS by the bucket sort's bins pass (0: the bin is read twice)
 #ifndef MSM_SORT_STAGE
@@ -128,6 +146,7 @@ constexpr int MSM_LIVE_LEVELS = 32;  // stitching levels with a liveness flag (l
 template <class F>
 struct MsmBases {
   size_t n = 0;                  // number of (compacted) bases incl. augmentation slots
+  int c = MSM_C;                 // window bits (msm_pick_c)
   Affine<F>* bases_w = nullptr;  // [n][W] expanded affine bases (device)
   uint32_t* sidx = nullptr;      // [n] scalar index map (device) or nullptr
   uint32_t extra_start = 0xFFFFFFFFu;
@@ -153,6 +172,7 @@ struct MsmAffScratch {
 template <class F>
 struct MsmScratch {
   size_t cap = 0;                // max number of bases served
+  int c = MSM_C;                 // window bits of the base sets served
   uint16_t* keys_in = nullptr;
   uint16_t* keys_out = nullptr;
   uint32_t* vals_in = nullptr;
@@ -168,6 +188,7 @@ struct MsmScratch {
 template <class F>
 struct MsmTail {
   size_t max_chunks = 0;        // ceil(cap * W / L)
+  int c = MSM_C;                // window bits of the MSMs it serves
   // stitching items (ping-pong): 2 per chunk / per stitching lane, sorted by bucket
   uint32_t* item_key[2] = {nullptr, nullptr};   // bucket | MSM_ITEM_DUMMY
   XYZZ<F>* item_val[2] = {nullptr, nullptr};
@@ -190,17 +211,26 @@ inline uint32_t msm_target_arg(const MsmTail<F>& t) {
   return (t.l0 << 24) | (t.target & 0xFFFFFFu);
 }
 
+// Window bits for a base set of n bases; ZKFL_MSM_C=<MSM_C | MSM_C_SMALL> forces one (tests, A/B)
+inline int msm_pick_c(size_t n) {
+  if (const char* e = getenv("ZKFL_MSM_C")) {
+    const int c = atoi(e);
+    if (c == MSM_C || c == MSM_C_SMALL) return c;
+  }
+  return n <= (size_t)MSM_SMALL_C_BASES ? MSM_C_SMALL : MSM_C;
+}
+
 constexpr int MSM_TAIL_MAX = 6;  // MSM tails per batched launch (the 4 G1 MSMs of a proof; 3 pairs' halves)
 constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket set (<= 2 level-1 blocks of 128 lanes)
 
 #define ZKFL_MSM_DECLARE(SUF, F)                                                                    \
-  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n);                                       \
+  hipError_t msm_bases_alloc_##SUF(MsmBases<F>& b, size_t n, int c);                                \
   hipError_t msm_bases_set_##SUF(MsmBases<F>& b, const Affine<F>* src, const uint32_t* h_sidx,      \
                                  uint32_t extra_start, hipStream_t st);                              \
   void msm_bases_free_##SUF(MsmBases<F>& b);                                                        \
-  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, hipStream_t st);                 \
+  hipError_t msm_scratch_alloc_##SUF(MsmScratch<F>& s, size_t cap, int c, hipStream_t st);          \
   void msm_scratch_free_##SUF(MsmScratch<F>& s);                                                    \
-  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap);                                       \
+  hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap, int c);                                \
   void msm_tail_free_##SUF(MsmTail<F>& t);                                                          \
   /* digits -> sort -> accumulation into t (the MSM is finished by msm_tails) */                    \
   hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t,            \
@@ -219,7 +249,7 @@ constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket 
                            const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag); \
   /* proof pairs (small keys): two proofs' digits over the same bases as one sort with 2 NB bucket  \
      keys into a pair tail (cap = both proofs' bases); its tails reduce each half: outs[2 i + h] */ \
-  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap);                                  \
+  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap, int c);                           \
   hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0, \
                                  const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st); \
   hipError_t msm_tails_pair_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast); \

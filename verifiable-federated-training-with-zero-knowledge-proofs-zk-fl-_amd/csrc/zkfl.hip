@@ -1017,6 +1017,7 @@ struct zkfl_key {
   // holds no separate C and H bases (they were ~0.5 GB of expanded bases per key at 2^18)
   Fr* dbg_zero = nullptr;
   bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
+  int msm_c = MSM_C;     // window bits of every base set of the key (msm_pick_c of its largest)
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
   std::vector<ProofPair*> pairs;  // proof pairs of batches (small keys), pair k on slot k's stream
@@ -1138,21 +1139,22 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   if (streams > 1) ZK_CHECK(hipStreamCreateWithFlags(&s->st_g2, hipStreamNonBlocking));
   for (hipEvent_t* e : {&s->ev_ready, &s->ev_b2, &s->ev_done})
     ZK_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, st));
+  const int c = k->msm_c;
+  ZK_CHECK(msm_scratch_alloc_g1(s->g1s, cap1, c, st));
 #if ZK_KNOCKOUT & 2
   for (MsmScratch<FqOps>& x : s->g1s_ko) {  // zeroed: an index past a stale sort is base 0
-    ZK_CHECK(msm_scratch_alloc_g1(x, cap1, st));
-    ZK_CHECK(hipMemsetAsync(x.keys_out, 0, cap1 * MSM_W * sizeof(uint16_t), st));
-    ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * MSM_W * sizeof(uint32_t), st));
+    ZK_CHECK(msm_scratch_alloc_g1(x, cap1, c, st));
+    ZK_CHECK(hipMemsetAsync(x.keys_out, 0, cap1 * msm_w_of(c) * sizeof(uint16_t), st));
+    ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * msm_w_of(c) * sizeof(uint32_t), st));
   }
 #endif
   // tail 3 is H's; with C and H merged the parity hook uses it for the C + H MSM, a folded key
   // for s pi_A + r pi_B1
   const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n),
                           std::max({k->bH.n, k->bCH.n, k->bRS.n})};
-  for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i]));
-  ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, st));
-  ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n));
+  for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i], c));
+  ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, c, st));
+  ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n, c));
   if (k->share_b && !s->st_g2 && !ZK_KNOCKOUT) {
     ZK_CHECK(hipFree(s->g2t.nnz));
     s->g2t.nnz = s->g1t[1].nnz;
@@ -1214,11 +1216,12 @@ hipError_t pair_create(zkfl_key* k, ProofSlot* slot, ProofPair** out) {
   for (ProofSlot*& h : pr->half) ZK_CHECK(half_create(k, &h));
   ZK_CHECK(hipEventCreateWithFlags(&pr->ev_done, hipEventDisableTiming));
   const size_t cap = std::max<size_t>({k->bA.n, k->bB1.n, k->bCH.n});
-  ZK_CHECK(msm_scratch_alloc_g1(pr->g1s, 2 * cap, k->ctx->st));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[0], 2 * k->bA.n));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[1], 2 * k->bB1.n));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[2], 2 * k->bCH.n));
-  ZK_CHECK(msm_tail_alloc_pair_g2(pr->g2t, 2 * k->bB2.n));
+  const int c = k->msm_c;
+  ZK_CHECK(msm_scratch_alloc_g1(pr->g1s, 2 * cap, c, k->ctx->st));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[0], 2 * k->bA.n, c));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[1], 2 * k->bB1.n, c));
+  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[2], 2 * k->bCH.n, c));
+  ZK_CHECK(msm_tail_alloc_pair_g2(pr->g2t, 2 * k->bB2.n, c));
   ZK_CHECK(hipFree(pr->g2t.nnz));  // B2 counts with B1's nnz (the same sort)
   pr->g2t.nnz = pr->g1t[1].nnz;
   ZK_CHECK(hipMalloc(&pr->res, 10 * sizeof(G1P)));
@@ -1504,7 +1507,7 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
   for (int i = 0; i < 3; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
-  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
+  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, k->msm_c, st), "B sort scratch");
   hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
   hipEvent_t ev_b = s->ev_lat[0], ev_b2 = s->ev_lat[1], ev_t = s->ev_lat[2];
   const uint32_t* W = (const uint32_t*)d_w;
@@ -1585,8 +1588,8 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
     if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
   for (int i = 0; i < 3; i++)
     if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
-  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, st), "B sort scratch");
-  if (!s->g1s_a.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, st), "A sort scratch");
+  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, k->msm_c, st), "B sort scratch");
+  if (!s->g1s_a.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, k->msm_c, st), "A sort scratch");
   hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
   // ev_lat[0] marks "ready" then (re-recorded on lat0) "B sorted": each wait is enqueued before
   // the next record, so every wait sees the record it was meant for
@@ -1665,8 +1668,9 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
       ps.live[ps.n] = live;
       ps.n++;
     };
-    for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, MSM_NB * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
-    if (g2) add(s->g2t.buckets, MSM_NB * sizeof(G2P), s->g2t.nnz, s->g2t.live);
+    const size_t nb = msm_nb_of(k->msm_c);
+    for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, nb * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
+    if (g2) add(s->g2t.buckets, nb * sizeof(G2P), s->g2t.nnz, s->g2t.live);
     uint32_t* res3 = MSM_MERGE_CH && plain != 1 && !fold ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
     if (s->w_stage && d_w == s->w_stage) {  // graph replay (enqueue_proof): stage the witness here
       ps.w_src_host = reinterpret_cast<const uint64_t*>(s->pinned + W_PTR_OFF);
@@ -1903,8 +1907,9 @@ int enqueue_pair_body(zkfl_ctx* ctx, zkfl_key* k, ProofPair* pr) {
       ps.live[ps.n] = live;
       ps.n++;
     };
-    for (auto& t : pr->g1t) add(t.buckets, 2 * MSM_NB * sizeof(G1P), t.nnz, t.live);
-    add(pr->g2t.buckets, 2 * MSM_NB * sizeof(G2P), pr->g2t.nnz, pr->g2t.live);
+    const size_t nb = msm_nb_of(k->msm_c);
+    for (auto& t : pr->g1t) add(t.buckets, 2 * nb * sizeof(G1P), t.nnz, t.live);
+    add(pr->g2t.buckets, 2 * nb * sizeof(G2P), pr->g2t.nnz, pr->g2t.live);
     hipLaunchKernelGGL(k_pair_start, dim3(64, ps.n), dim3(256), 0, st, ps);
   }
   for (ProofSlot* h : pr->half) {
@@ -2127,8 +2132,8 @@ hipError_t msm_run_any(const MsmBases<Fq2Ops>& b, MsmScratch<Fq2Ops>& s, MsmTail
                        G2P* o, hipStream_t st, Profiler* p) {
   return msm_run_g2(b, s, t, sc, nullptr, o, st, p, "msm_accumulate_g2");
 }
-hipError_t bases_alloc_any(MsmBases<FqOps>& b, size_t n) { return msm_bases_alloc_g1(b, n); }
-hipError_t bases_alloc_any(MsmBases<Fq2Ops>& b, size_t n) { return msm_bases_alloc_g2(b, n); }
+hipError_t bases_alloc_any(MsmBases<FqOps>& b, size_t n, int c) { return msm_bases_alloc_g1(b, n, c); }
+hipError_t bases_alloc_any(MsmBases<Fq2Ops>& b, size_t n, int c) { return msm_bases_alloc_g2(b, n, c); }
 hipError_t bases_set_any(MsmBases<FqOps>& b, const G1Aff* src, hipStream_t st) {
   return msm_bases_set_g1(b, src, nullptr, 0xFFFFFFFFu, st);
 }
@@ -2143,12 +2148,16 @@ hipError_t bases_set_map_any(MsmBases<Fq2Ops>& b, const void* src, const uint32_
 }
 void bases_free_any(MsmBases<FqOps>& b) { msm_bases_free_g1(b); }
 void bases_free_any(MsmBases<Fq2Ops>& b) { msm_bases_free_g2(b); }
-hipError_t scratch_alloc_any(MsmScratch<FqOps>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g1(s, n, st); }
-hipError_t scratch_alloc_any(MsmScratch<Fq2Ops>& s, size_t n, hipStream_t st) { return msm_scratch_alloc_g2(s, n, st); }
+hipError_t scratch_alloc_any(MsmScratch<FqOps>& s, size_t n, int c, hipStream_t st) {
+  return msm_scratch_alloc_g1(s, n, c, st);
+}
+hipError_t scratch_alloc_any(MsmScratch<Fq2Ops>& s, size_t n, int c, hipStream_t st) {
+  return msm_scratch_alloc_g2(s, n, c, st);
+}
 void scratch_free_any(MsmScratch<FqOps>& s) { msm_scratch_free_g1(s); }
 void scratch_free_any(MsmScratch<Fq2Ops>& s) { msm_scratch_free_g2(s); }
-hipError_t tail_alloc_any(MsmTail<FqOps>& t, size_t n) { return msm_tail_alloc_g1(t, n); }
-hipError_t tail_alloc_any(MsmTail<Fq2Ops>& t, size_t n) { return msm_tail_alloc_g2(t, n); }
+hipError_t tail_alloc_any(MsmTail<FqOps>& t, size_t n, int c) { return msm_tail_alloc_g1(t, n, c); }
+hipError_t tail_alloc_any(MsmTail<Fq2Ops>& t, size_t n, int c) { return msm_tail_alloc_g2(t, n, c); }
 void tail_free_any(MsmTail<FqOps>& t) { msm_tail_free_g1(t); }
 void tail_free_any(MsmTail<Fq2Ops>& t) { msm_tail_free_g2(t); }
 
@@ -2164,9 +2173,10 @@ int run_msm_primitive(zkfl_ctx* ctx, const uint8_t* bases, const uint8_t* scalar
   XYZZ<F>* d_r = nullptr;
   uint32_t* d_o = nullptr;
   int rc = ZKFL_OK;
-  hipError_t e = bases_alloc_any(mb, n);
-  if (e == hipSuccess) e = scratch_alloc_any(ms, n, st);
-  if (e == hipSuccess) e = tail_alloc_any(mt, n);
+  const int c = msm_pick_c(n);
+  hipError_t e = bases_alloc_any(mb, n, c);
+  if (e == hipSuccess) e = scratch_alloc_any(ms, n, c, st);
+  if (e == hipSuccess) e = tail_alloc_any(mt, n, c);
   if (e == hipSuccess) e = hipMalloc(&d_b, n * sizeof(Affine<F>));
   if (e == hipSuccess) e = hipMalloc(&d_s, n * 32);
   if (e == hipSuccess) e = hipMalloc(&d_r, sizeof(XYZZ<F>));
@@ -2551,9 +2561,12 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
       for (uint32_t x : im[QB1].sidx) o.sidx.push_back(x + X + 4);
     }
     mark("bases_host");
+    size_t most = 0;
+    for (const Img& o : im) most = std::max(most, o.sidx.size());
+    k->msm_c = msm_pick_c(most);
     std::vector<void*> d_imgs;
     auto upload = [&](auto& mb, Img& o, bool identity, uint32_t xs) -> hipError_t {
-      hipError_t e = bases_alloc_any(mb, o.sidx.size());
+      hipError_t e = bases_alloc_any(mb, o.sidx.size(), k->msm_c);
       if (e != hipSuccess || o.sidx.empty()) return e;
       void* d_img = nullptr;
       e = hipMalloc(&d_img, o.img.size());
