@@ -349,3 +349,36 @@ def test_g2_madd_chain_stays_in_range(f29):
         for j in range(4):
             acc[j], acc_pts[j] = got[j], exp[j]
             assert from_xyzz2(bn, acc[j]) == exp[j]
+
+
+# Fr in the witness engine's 29-bit form (csrc/fr29.h: canonical x 2^261 mod r in and out)
+RR = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+
+
+def test_fr29_against_big_integers(f29):
+    rng = random.Random(29)
+    vals = [0, 1, 2, RR - 1, RR - 2, (1 << 253) - 1] + [rng.randrange(RR) for _ in range(40)]
+    lines, want = [], []
+    rinv = pow(1 << 261, -1, RR)
+    for i, a in enumerate(vals):
+        b = vals[(7 * i + 3) % len(vals)]
+        lines.append(f"rmul {limbs(a)} {limbs(b)}")
+        want.append(a * b * rinv % RR)
+        lines.append(f"rsqr {limbs(a)}")
+        want.append(a * a * rinv % RR)
+        lines.append(f"radd {limbs(a)} {limbs(b)}")
+        want.append((a + b) % RR)
+        xs = [vals[(i + k) % len(vals)] for k in range(4)]
+        ys = [vals[(3 * i + 5 * k + 1) % len(vals)] for k in range(4)]
+        lines.append("rmulsum4 " + " ".join(limbs(x) for x in xs + ys))
+        want.append(sum(x * y for x, y in zip(xs, ys)) * rinv % RR)
+        lines.append(f"rfromplain {limbs(a)}")
+        want.append(a * (1 << 261) % RR)
+        lines.append(f"rtoplain {limbs(a)}")
+        want.append(a * rinv % RR)
+        lines.append(f"rfrom256 {limbs(a)}")
+        want.append(a * (1 << 5) % RR)
+        lines.append(f"rto256 {limbs(a)}")
+        want.append(a * pow(1 << 5, -1, RR) % RR)
+    got = f29(lines)
+    assert [g[0] for g in got] == want

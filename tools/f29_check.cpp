@@ -3,6 +3,8 @@
 // checked on the CPU against Python big integers.  One operation per stdin line:
 //   mul a b | sqr a | inv a | canon a | aadd x0 y0 x1 y1 | mulsum2 a b c d | below256 a | dbl P | madd P x y | madds P x y neg | add P Q
 //   g2dbl P | g2madd P x y | g2add P Q   (Fq2 values as two elements: c0 c1)
+//   rmul a b | rsqr a | radd a b | rmulsum4 x0 x1 x2 x3 y0 y1 y2 y3 | rfromplain a | rtoplain a |
+//   rfrom256 a | rto256 a   (Fr in the witness engine's 29-bit form, csrc/fr29.h)
 // field elements as 9 comma-separated decimal limbs, points as X Y ZZ ZZZ; the result is
 // printed the same way.
 // Build: hipcc --offload-arch=gfx950 -O1 -std=c++17 -I<pkg>/csrc -o f29_check f29_check.cpp
@@ -13,7 +15,14 @@
 #include <string>
 
 #include "field29.h"
+#include "fr29.h"
 using namespace zkfl;
+
+static Fr as_fr(const F29& a) {
+  Fr r;
+  f29_unpack(r.v, a);
+  return r;
+}
 
 static F29 rd(std::istringstream& in) {
   std::string t;
@@ -143,6 +152,27 @@ int main() {
     if (op == "mul") {
       F29 a = rd(in), b = rd(in);
       wr(f29_mul(a, b));
+    } else if (op == "rmul") {
+      F29 a = rd(in), b = rd(in);
+      wr(fr29_mul(a, b));
+    } else if (op == "rsqr") {
+      wr(fr29_sqr(rd(in)));
+    } else if (op == "radd") {
+      F29 a = rd(in), b = rd(in);
+      wr(fr29_add(a, b));
+    } else if (op == "rmulsum4") {
+      F29 x[4], y[4];
+      for (auto& v : x) v = rd(in);
+      for (auto& v : y) v = rd(in);
+      wr(fr29_mulsum<4>(x, y));
+    } else if (op == "rfromplain") {
+      wr(fr29_from_plain(as_fr(rd(in))));
+    } else if (op == "rtoplain") {
+      wr(f29_pack(fr29_to_plain(rd(in)).v));
+    } else if (op == "rfrom256") {
+      wr(fr29_from_m256(as_fr(rd(in))));
+    } else if (op == "rto256") {
+      wr(f29_pack(fr29_to_m256(rd(in)).v));
     } else if (op == "sqr") {
       wr(f29_sqr(rd(in)));
     } else if (op == "inv") {

@@ -214,8 +214,8 @@ ZK_HD void f29_keep(uint64_t& a) {
 
 // NACC: accumulators per column (chains a lone wave can issue from; the latency-bound kernels --
 // k_assemble's quad operations -- take 4, the throughput kernels 2: every extra chain costs one
-// 64-bit join per column)
-template <int NP, int NACC = (F29_SPLIT ? 2 : 1)>
+// 64-bit join per column).  M: the modulus (P29 = Fq; R29 = Fr, fr29.h) -- MASK, NINV, P[9].
+template <int NP, int NACC = (F29_SPLIT ? 2 : 1), class M = P29>
 ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
   static_assert(NACC == 1 || NACC == 2 || NACC == 4, "accumulators per column");
   uint32_t m[9];
@@ -233,7 +233,7 @@ ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
     for (int i = lo; i <= hi; i++) {
 #pragma unroll
       for (int j = 0; j < NP; j++) acc[(t++) % NACC] += (uint64_t)x[j].v[i] * y[j].v[k - i];
-      if (i < k) acc[(t++) % NACC] += (uint64_t)m[i] * P29::P[k - i];  // m_k is not known yet
+      if (i < k) acc[(t++) % NACC] += (uint64_t)m[i] * M::P[k - i];  // m_k is not known yet
     }
 #pragma unroll
     for (int q = 0; q < NACC; q++) f29_keep(acc[q]);
@@ -241,10 +241,10 @@ ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
     if (NACC == 4) c = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     else if (NACC == 2) c = acc[0] + acc[1];
     if (k < 9) {
-      m[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
-      c += (uint64_t)m[k] * P29::P[0];
+      m[k] = ((uint32_t)c * M::NINV) & M::MASK;
+      c += (uint64_t)m[k] * M::P[0];
     } else {
-      r.v[k - 9] = (uint32_t)c & P29::MASK;
+      r.v[k - 9] = (uint32_t)c & M::MASK;
     }
     carry = c >> 29;
   }
@@ -253,9 +253,10 @@ ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
 }
 
 // Montgomery product a b 2^-261
+template <class M = P29>
 ZK_HD F29 f29_mul(const F29& a, const F29& b) {
   const F29 x[1] = {a}, y[1] = {b};
-  return f29_mont<1>(x, y);
+  return f29_mont<1, (F29_SPLIT ? 2 : 1), M>(x, y);
 }
 
 // The same product with ACC accumulators per column (latency-bound single-wave kernels)
@@ -270,6 +271,7 @@ ZK_HD F29 f29_mul_acc(const F29& a, const F29& b) {
 // instead of 81 (+ the 81 of the reduction).  Column bound: <= 4 cross products < 2^59 and one
 // square < 2^58, plus 9 reduction products < 2^58: 18 x 2^58 < 2^63.  Same value, same
 // Montgomery bound (< p + a^2 / 2^261) as f29_mul(a, a).
+template <class M = P29>
 ZK_HD F29 f29_sqr(const F29& a) {
   uint32_t a2[9];
 #pragma unroll
@@ -287,16 +289,16 @@ ZK_HD F29 f29_sqr(const F29& a) {
       const int j = k - i;
       if (i < j) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)a2[i] * a.v[j];
       else if (i == j) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)a.v[i] * a.v[i];
-      if (i < k) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)m[i] * P29::P[k - i];
+      if (i < k) acc[F29_SPLIT ? (t++ & 1) : 0] += (uint64_t)m[i] * M::P[k - i];
     }
     f29_keep(acc[0]);
     f29_keep(acc[1]);
     uint64_t c = acc[0] + acc[1];
     if (k < 9) {
-      m[k] = ((uint32_t)c * P29::NINV) & P29::MASK;
-      c += (uint64_t)m[k] * P29::P[0];
+      m[k] = ((uint32_t)c * M::NINV) & M::MASK;
+      c += (uint64_t)m[k] * M::P[0];
     } else {
-      r.v[k - 9] = (uint32_t)c & P29::MASK;
+      r.v[k - 9] = (uint32_t)c & M::MASK;
     }
     carry = c >> 29;
   }
@@ -647,8 +649,8 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
 // Affine arithmetic for the batch-affine rounds of the G1 accumulation (msm_affine.h): canonical
 // coordinates (< p), one shared inversion per round for all additions of an MSM.
 // ---------------------------------------------------------------------------
-// normalized a < (k + 1) p -> canonical (< p): k conditional subtractions of p
-template <int K>
+// normalized a < (k + 1) p -> canonical (< p): k conditional subtractions of p (M: the modulus)
+template <int K, class M = P29>
 ZK_HD F29 f29_canon_sub(F29 a) {
 #pragma unroll
   for (int t = 0; t < K; t++) {
@@ -656,11 +658,11 @@ ZK_HD F29 f29_canon_sub(F29 a) {
     int32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      const int32_t x = (int32_t)a.v[i] - (int32_t)P29::P[i] + c;
-      s.v[i] = (uint32_t)x & P29::MASK;
+      const int32_t x = (int32_t)a.v[i] - (int32_t)M::P[i] + c;
+      s.v[i] = (uint32_t)x & M::MASK;
       c = x >> 29;
     }
-    const int32_t top = (int32_t)a.v[8] - (int32_t)P29::P[8] + c;
+    const int32_t top = (int32_t)a.v[8] - (int32_t)M::P[8] + c;
     s.v[8] = (uint32_t)top;
     const bool ge = top >= 0;
 #pragma unroll

@@ -10,9 +10,14 @@
 // "Assert Failed"; here ZKFL_E_CONSTRAINT).
 //
 // Schedule: ops are stored level by level (a level's ops only read wires of earlier levels);
-// one launch per level, one lane per (witness, op), values in Montgomery form; a final pass
-// checks the asserts and writes the standard-form witness.  Independent of the circuit: the
-// program image carries the linear combinations, the Poseidon templates and constants.
+// one launch per level, one lane per (witness, op); a final pass checks the asserts and writes
+// the standard-form witness.  Independent of the circuit: the program image carries the linear
+// combinations, the Poseidon templates and constants.
+// Arithmetic: the 29-bit engine over Fr (fr29.h).  The wire vector, the coefficients and the
+// Poseidon constants are kept as canonical x 2^261 (the image's 2^256 Montgomery coefficients
+// and constants are converted once at load, k_wit_to_m261); a level of Poseidon permutations is
+// a chain of ~4 dependent products per round on one wave per SIMD, so the product's latency is
+// the witness engine's pace (config 5).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -23,6 +28,7 @@
 
 #include "common.h"
 #include "field.h"
+#include "fr29.h"
 #include "host_parse.h"
 #include "witness.h"
 #include "wtrace.h"
@@ -50,20 +56,27 @@ struct ProgView {  // device pointers, passed by value
   uint32_t n_wires;
 };
 
-ZK_DEV Fr lc_eval(const ProgView& P, const Fr* w, uint32_t lc) {
-  Fr acc = fp_zero<FrP>();
+// term wire bit 31: coefficient one (no product)
+ZK_DEV Fr29 lc_eval(const ProgView& P, const Fr* w, uint32_t lc) {
+  Fr29 acc = f29_zero();
   const uint32_t e = P.lc_ptr[lc + 1];
   for (uint32_t t = P.lc_ptr[lc]; t < e; t++) {
     const uint32_t x = P.term_wire[t];
-    Fr v = w[x & 0x7FFFFFFFu];
-    if (!(x >> 31)) v = fp_mul(v, P.term_coef[t]);
-    acc = fp_add(acc, v);
+    Fr29 v = fr29_ld(w[x & 0x7FFFFFFFu]);
+    if (!(x >> 31)) v = fr29_mul(v, fr29_ld(P.term_coef[t]));
+    acc = fr29_add(acc, v);
   }
   return acc;
 }
 
+// the image's 2^256 Montgomery field elements (coefficients, Poseidon constants) -> x 2^261
+__global__ __launch_bounds__(256) void k_wit_to_m261(Fr* a, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = fr29_st(fr29_from_m256(a[i]));
+}
+
 // circomlib Poseidon permutation (zkfl/field.py::poseidon_perm_trace) of width T for one K_POS op
-// per group of T lanes: lane i of a group holds state element i (8 VGPRs, no scratch), applies
+// per group of T lanes: lane i of a group holds state element i (9 VGPRs, no scratch), applies
 // the ARK constant and, in full rounds or for i = 0, the S-box (writing x^2, x^4, x^5 when the
 // template marks that S-box live), then computes MDS row i from the group's state read with
 // cross-lane shuffles, 4 products per Montgomery reduction.  The latency of a round is one row,
@@ -80,7 +93,7 @@ __global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t o
   const uint4 op = P.ops[op0 + (uint32_t)(jj % cnt)];
   Fr* w = W + (jj / cnt) * P.n_wires;
   const uint32_t gb = (g < G ? g : 0) * T;  // the group's first lane
-  Fr st = (active && i > 0) ? lc_eval(P, w, op.z + i - 1) : fp_zero<FrP>();
+  Fr29 st = (active && i > 0) ? lc_eval(P, w, op.z + i - 1) : f29_zero();
   const PosWidth pw = P.width[T];
   const Fr* __restrict__ C = P.consts + pw.c_off;
   const Fr* __restrict__ Mrow = P.consts + pw.m_off + (size_t)i * T;
@@ -95,11 +108,11 @@ __global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t o
   }
   const uint32_t rp = pw.rp, rounds = 8 + rp;
   for (uint32_t r = 0; r < rounds; r++) {
-    st = fp_add(st, C[r * T + i]);
+    st = fr29_add(st, fr29_ld(C[r * T + i]));
     const bool full = r < 4 || r >= 4 + rp;
     if (full || i == 0) {
       const uint32_t sb = r < 4 ? r * T + i : (r < 4 + rp ? 4 * T + (r - 4) : 4 * T + rp + (r - 4 - rp) * T + i);
-      const Fr x2 = fp_sqr(st), x4 = fp_sqr(x2), x5 = fp_mul(x4, st);
+      const Fr29 x2 = fr29_sqr(st), x4 = fr29_sqr(x2), x5 = fr29_mul(x4, st);
       const uint32_t q = sb >> 5, bit = sb & 31;
       uint32_t word = 0, rank = 0;
 #pragma unroll
@@ -110,24 +123,24 @@ __global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t o
         }
       if ((word >> bit) & 1u) {
         const uint32_t k = op.y + 3 * (rank + __popc(word & ((1u << bit) - 1u)));
-        w[k] = x2;
-        w[k + 1] = x4;
-        w[k + 2] = x5;
+        w[k] = fr29_st(x2);
+        w[k + 1] = fr29_st(x4);
+        w[k + 2] = fr29_st(x5);
       }
       st = x5;
     }
-    Fr acc = fp_zero<FrP>();
+    Fr29 acc = f29_zero();
     for (uint32_t j0 = 0; j0 < T; j0 += 4) {
-      Fr x[4], y[4];
+      Fr29 x[4], y[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t j = j0 + k;
         const uint32_t src = gb + (j < T ? j : 0);
 #pragma unroll
-        for (int v = 0; v < 8; v++) x[k].v[v] = __shfl((int)st.v[v], (int)src);
-        y[k] = j < T ? Mrow[j] : fp_zero<FrP>();
+        for (int v = 0; v < 9; v++) x[k].v[v] = __shfl((int)st.v[v], (int)src);
+        y[k] = j < T ? fr29_ld(Mrow[j]) : f29_zero();
       }
-      acc = fp_add(acc, fp_mul_sum4(x, y));
+      acc = fr29_add(acc, fr29_mulsum<4>(x, y));
     }
     st = acc;
   }
@@ -140,13 +153,13 @@ __global__ __launch_bounds__(64) void k_wit_inputs(size_t n, uint32_t nw, uint32
   const size_t j = l / (n_in + 1), i = l % (n_in + 1);
   Fr* w = W + j * nw;
   if (i == n_in) {
-    w[0] = fp_one<FrP>();
+    w[0] = fr29_st(f29_const(R29::ONE));
     return;
   }
   Fr v;
 #pragma unroll
   for (int q = 0; q < 8; q++) v.v[q] = inputs[(j * n_in + i) * 8 + q];
-  w[in_first + i] = fp_to_mont(v);
+  w[in_first + i] = fr29_st(fr29_from_plain(v));
 }
 
 __global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t op0, uint32_t cnt, Fr* W) {
@@ -158,19 +171,19 @@ __global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t
   Fr* w = W + j * P.n_wires;
   switch (op.x) {
     case K_LC:
-      w[op.y] = lc_eval(P, w, op.z);
+      w[op.y] = fr29_st(lc_eval(P, w, op.z));
       break;
     case K_MUL:
-      w[op.y] = fp_mul(lc_eval(P, w, op.z), lc_eval(P, w, op.z + 1));
+      w[op.y] = fr29_st(fr29_mul(lc_eval(P, w, op.z), lc_eval(P, w, op.z + 1)));
       break;
-    case K_INV: {
-      Fr v = lc_eval(P, w, op.z);
-      w[op.y] = fp_is_zero(v) ? v : fp_inv(v);
+    case K_INV: {  // rare (IsZero hints): the 32-bit engine's inverse
+      const Fr29 v = lc_eval(P, w, op.z);
+      w[op.y] = fr29_is_zero(v) ? fr29_st(v) : fr29_st(fr29_from_m256(fp_inv(fr29_to_m256(v))));
       break;
     }
     case K_BITS: {
-      Fr v = fp_from_mont(lc_eval(P, w, op.z));
-      const Fr one = fp_one<FrP>(), zero = fp_zero<FrP>();
+      Fr v = fr29_to_plain(lc_eval(P, w, op.z));
+      const Fr one = fr29_st(f29_const(R29::ONE)), zero = fp_zero<FrP>();
 #pragma unroll
       for (uint32_t q = 0; q < 8; q++) {  // constant limb index: v stays in registers
 #pragma unroll 1
@@ -196,16 +209,16 @@ __global__ __launch_bounds__(64) void k_wit_asserts(ProgView P, size_t n, uint32
   const uint32_t a = (uint32_t)(l % na);
   const Fr* w = W + j * P.n_wires;
   const uint32_t lc0 = P.asserts[a];
-  Fr ab = fp_mul(lc_eval(P, w, lc0), lc_eval(P, w, lc0 + 1));
-  if (!fp_eq(ab, lc_eval(P, w, lc0 + 2))) atomicMin(fail + j, a);
+  const Fr29 ab = fr29_mul(lc_eval(P, w, lc0), lc_eval(P, w, lc0 + 1));
+  if (!fr29_eq(ab, lc_eval(P, w, lc0 + 2))) atomicMin(fail + j, a);
 }
 
-// Montgomery -> standard form into each witness's output buffer
+// x 2^261 -> standard form into each witness's output buffer
 __global__ __launch_bounds__(256) void k_wit_out(size_t n, uint32_t nw, const Fr* W, Fr* const* outs) {
   size_t l = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= n * nw) return;
   const size_t j = l / nw, i = l % nw;
-  outs[j][i] = fp_from_mont(W[l]);
+  outs[j][i] = fr29_to_plain(fr29_ld(W[l]));
 }
 
 int hip_err(hipError_t e, const char* where, std::string& err) {
@@ -307,6 +320,12 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
       if (u.bytes) e = hipMemcpyAsync(*u.dst, u.src, u.bytes, hipMemcpyHostToDevice, st);
     }
   }
+  // the coefficients and constants into the witness engine's x 2^261 form
+  const size_t n_c = consts.size() / 32;
+  if (e == hipSuccess && n_terms)
+    hipLaunchKernelGGL(k_wit_to_m261, dim3(zk_grid(n_terms, 256)), dim3(256), 0, st, (Fr*)d_tc, (size_t)n_terms);
+  if (e == hipSuccess && n_c) hipLaunchKernelGGL(k_wit_to_m261, dim3(zk_grid(n_c, 256)), dim3(256), 0, st, (Fr*)d_c, n_c);
+  if (e == hipSuccess) e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
     wprog_free(p);

@@ -1270,6 +1270,9 @@ int get_pair(zkfl_key* k, size_t idx, ProofPair** out) {
 // group g - 1 (when group g + 1 is enqueued, the slots have drained group g - 2, so its set is
 // free).  Per-slot witnesses cost ~25 small launches per proof on the slot's stream, each a
 // permutation-latency chain; batched, a group's 15 levels cost as much as one witness's.
+// Witness sets of a key's pipe: group g uses set g % WIT_SETS; groups run up to WIT_SETS - 2 ahead
+// of the group the key's slots start (full_prove_piped)
+constexpr int WIT_SETS = 4;
 struct WitPipe {
   struct Set {
     Fr* W = nullptr;          // [G][nw] Montgomery scratch
@@ -1282,7 +1285,7 @@ struct WitPipe {
   };
   size_t G = 0, nw = 0, n_in = 0;
   hipStream_t st = nullptr;
-  Set set[3];
+  Set set[WIT_SETS];
 };
 
 namespace {
@@ -2944,12 +2947,16 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
   }
   uint8_t* pin_out = nullptr;
   HIP_TRY(hipHostMalloc(&pin_out, off[n] + 16), "pinned witness outputs");
+  // groups enqueued ahead of the one the slots start (ZKFL_WIT_AHEAD, 1..WIT_SETS - 2): a group
+  // is computed while the slots run the `ahead` groups before it
+  static const size_t ahead = (size_t)std::clamp(getenv("ZKFL_WIT_AHEAD") ? atoi(getenv("ZKFL_WIT_AHEAD")) : 2, 1,
+                                                 WIT_SETS - 2);
   auto enqueue_group = [&](PerKey& pk, size_t g) -> int {
     WitPipe* P = pk.pipe;
-    WitPipe::Set& b = P->set[g % 3];
+    WitPipe::Set& b = P->set[g % WIT_SETS];
     const size_t l0 = g * pk.G, m = std::min(pk.G, pk.jobs.size() - l0), nw = pk.key->nVars;
     const size_t npub = pk.key->nPub;
-    HIP_TRY(host_wait(b.ev, true), "witness set reuse");  // its group of 3 groups ago
+    HIP_TRY(host_wait(b.ev, true), "witness set reuse");  // its group of WIT_SETS groups ago
     for (size_t j = 0; j < m; j++) {
       const uint8_t* in = nullptr;
       int r = get_input(pk.jobs[l0 + j], &in);
@@ -2969,19 +2976,20 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
   };
   int rc = ZKFL_OK;
   for (auto& pk : ks)
-    for (size_t g = 0; g < 2 && g < pk.groups && rc == ZKFL_OK; g++) rc = enqueue_group(pk, g);
+    for (size_t g = 0; g <= ahead && g < pk.groups && rc == ZKFL_OK; g++) rc = enqueue_group(pk, g);
   if (rc == ZKFL_OK)
     rc = run_jobs(ctx, n, [&](size_t i, Job& J) {
       PerKey& pk = ks[kidx[i]];
       const size_t g = local[i] / pk.G, j = local[i] % pk.G;
-      // the key's slots hold its group g - 1 now and have drained group g - 2, whose set g + 1 takes
-      if (j == 0 && g >= 1 && g + 1 < pk.groups) {
-        int r = enqueue_group(pk, g + 1);
+      // the key's slots hold its group g - 1 now and have drained group g - 2, whose set (mod
+      // WIT_SETS) group g + ahead takes (ahead <= WIT_SETS - 2)
+      if (j == 0 && g >= 1 && g + ahead < pk.groups) {
+        int r = enqueue_group(pk, g + ahead);
         if (r) return r;
       }
       J.key = pk.key;
-      J.w = pk.pipe->set[g % 3].d + j * pk.key->nVars;
-      J.w_ready = pk.pipe->set[g % 3].ev;
+      J.w = pk.pipe->set[g % WIT_SETS].d + j * pk.key->nVars;
+      J.w_ready = pk.pipe->set[g % WIT_SETS].ev;
       J.rs = rs ? rs + 64 * i : nullptr;
       J.proof_out = proofs_out + 256 * i;
       return ZKFL_OK;
