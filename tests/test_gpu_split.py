@@ -160,6 +160,35 @@ def test_assemble_rejects_malformed_points(gpu_ctx, case):
     assert bn.g1_from_bytes_std(proof[:64]) == bn.G1_GEN
 
 
+@pytest.mark.parametrize("case", ["double", "cancel"])
+def test_assemble_exceptional_sums(gpu_ctx, case):
+    """The assembly's quad operations run on lazy values (csrc/zkfl.hip Q29: below small multiples
+    of p, is_zero<K> over 0, p, .., (K-1) p): equal points in different XYZZ scalings must still
+    take the doubling branch, opposite ones the infinity branch.  double: A' = B1' = P (scalings
+    3 and 7), r = s, C' = H = Q (scalings 2 and 11); cancel: B1' = -A', H = -C'."""
+    from split_model import assemble
+    Q = bn.Q
+
+    def put(buf, word, pt, lam):
+        x, y = pt
+        for k, v in enumerate((x * lam * lam % Q, y * pow(lam, 3, Q) % Q, lam * lam % Q, pow(lam, 3, Q))):
+            buf[4 * (word + 8 * k):4 * (word + 8 * k) + 32] = _le(v)
+
+    P = bn.mul(bn.G1_GEN, 0x1234567)
+    Pc = bn.mul(bn.G1_GEN, 0x7654321)
+    neg = lambda pt: (pt[0], (Q - pt[1]) % Q)  # noqa: E731
+    part = bytearray(768)
+    put(part, 0, P, 3)
+    put(part, 32, P if case == "double" else neg(P), 7)
+    put(part, 128, Pc, 2)
+    put(part, 160, Pc if case == "double" else neg(Pc), 11)
+    rs = b"".join(_le(v) + _le(v) for v in (5, R - 2, 0x1F2E3D4C5B6A79880))
+    out = gpu_ctx.assemble(bytes(part) * 3, 1, rs)
+    assert out == assemble(bytes(part) * 3, 1, rs)
+    if case == "cancel":
+        assert all(p[128:] == bytes(128) for p in out)  # pi_c = infinity
+
+
 def test_sharded_key_refuses_whole_proofs(gpu_ctx, small):
     """a key loaded as one shard of a split proof holds only its share of every MSM (and
     shards > 0 no alpha/beta/delta terms): proving a whole proof with it is ZKFL_E_ARG, not a

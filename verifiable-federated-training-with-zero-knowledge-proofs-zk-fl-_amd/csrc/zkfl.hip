@@ -381,12 +381,18 @@ __device__ void store_affine_std<Fq2Ops>(const Affine<Fq2Ops>& a, uint32_t* out)
 // control flow stays uniform inside a quad.  A chain of point operations then costs one
 // multiply latency per level (doubling 3, addition 4) instead of one per product (9 / 14).
 // ---------------------------------------------------------------------------
-// The quad operations are written once over a field policy QF (T, mul, add, sub, dbl, is_zero,
-// zero, one, bcast<K>, pick4).  k_assemble runs them on Q29: canonical (< p) values in the 29-bit
-// engine's limbs and Montgomery domain (field29.h), so a product is one f29_mul (81 + 81
-// v_mad_u64_u32, two column chains: ~2.5x shorter single-lane latency than the 32-bit fp_mul) and
-// one conditional subtraction -- no bound bookkeeping, every value stays canonical:
-//   a, b < p -> f29_mul < p + p^2 / 2^261 < 1.006p;  a + b < 2p;  a + p - b in (0, 2p).
+// The quad operations are written once over a field policy QF (T, mul, add, sub<K>, dbl,
+// is_zero<K>, zero, one, bcast<K>, pick4).  k_assemble runs them on Q29: the 29-bit engine's
+// limbs and Montgomery domain (field29.h), a product one f29_mul (81 + 81 v_mad_u64_u32, two
+// column chains: ~2.5x shorter single-lane latency than the 32-bit fp_mul).  Values are LAZY
+// (normalized limbs, below a small multiple of p, tracked per site in the formulas' comments):
+//   mul(a, b) < p + a b / 2^261 < 2p whenever a b < 169 p^2 (2^261 ~ 169.3 p);
+//   add(a, b) < bound(a) + bound(b);  sub<K>(a, b) = a + K p - b for b < K p, < bound(a) + K p;
+//   is_zero<K>(a) for a < K p (a == 0, p, .., (K-1) p).
+// A quad operation keeps X < 8p, Y < 4p, ZZ, ZZZ < 2p (in and out), so no product or sum is
+// brought below p on the chain: the canonical (< p) form is taken once, when a point leaves
+// (g1q_to).  The round-4 canonical policy spent a conditional subtraction (~40 VALU) after every
+// product, sum and difference of the chain.
 // lane K of the caller's quad to all four lanes: DPP quad_perm [K,K,K,K] (a VALU move, no
 // LDS-path round trip as with ds_bpermute)
 template <int K, int N>
@@ -401,6 +407,26 @@ ZK_DEV void pick4_words(int q, const uint32_t (&a)[N], const uint32_t (&b)[N], c
   for (int i = 0; i < N; i++) r[i] = (q & 2) ? ((q & 1) ? d[i] : c[i]) : ((q & 1) ? b[i] : a[i]);
 }
 
+// k p (k < 64) in nine 29-bit limbs: normalized, or borrowed by one for a + k p - b (every lower
+// limb raised by 2^29, the next lowered by one, so no limb goes negative for a normalized b)
+struct Limbs9 {
+  uint32_t v[9];
+};
+__host__ __device__ constexpr Limbs9 p29_times(uint32_t k, bool borrowed) {
+  Limbs9 r{};
+  uint64_t c = 0;
+  for (int i = 0; i < 9; i++) {
+    c += (uint64_t)k * P29::P[i];
+    r.v[i] = i < 8 ? (uint32_t)(c & P29::MASK) : (uint32_t)c;
+    c >>= 29;
+  }
+  if (borrowed) {
+    for (int i = 0; i < 8; i++) r.v[i] += (1u << 29) - (i ? 1u : 0u);
+    r.v[8] -= 1u;
+  }
+  return r;
+}
+
 struct Q29 {
   using T = F29;
   // ZKFL_Q29_ACC: accumulators per product column of the assembly's quad operations (an A/B knob:
@@ -410,15 +436,37 @@ struct Q29 {
 #ifndef ZKFL_Q29_ACC
 #define ZKFL_Q29_ACC 2
 #endif
-  static ZK_DEV T mul(const T& a, const T& b) { return f29_canon_sub<1>(f29_mul_acc<ZKFL_Q29_ACC>(a, b)); }
+  static ZK_DEV T mul(const T& a, const T& b) { return f29_mul_acc<ZKFL_Q29_ACC>(a, b); }
   static ZK_DEV T add(const T& a, const T& b) {
     T r = f29_add_lazy(a, b);
     f29_norm(r);
-    return f29_canon_sub<1>(r);
+    return r;
   }
-  static ZK_DEV T sub(const T& a, const T& b) { return f29_canon_sub<1>(f29_sub_canon(a, b)); }
+  template <int K>
+  static ZK_DEV T sub(const T& a, const T& b) {
+    constexpr Limbs9 k = p29_times(K, true);
+    T r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + k.v[i] - b.v[i];
+    f29_norm(r);
+    return r;
+  }
   static ZK_DEV T dbl(const T& a) { return add(a, a); }
-  static ZK_DEV bool is_zero(const T& a) { return f29_is_zero(a); }
+  template <int K>
+  static ZK_DEV bool is_zero(const T& a) {
+    bool z = false;
+#pragma unroll
+    for (int m = 0; m < K; m++) {
+      const Limbs9 mp = p29_times(m, false);
+      uint32_t d = 0;
+#pragma unroll
+      for (int i = 0; i < 9; i++) d |= a.v[i] ^ mp.v[i];
+      z = z || d == 0;
+    }
+    return z;
+  }
+  // a < 8p -> canonical (< p)
+  static ZK_DEV T canon(const T& a) { return f29_canon_sub<7>(a); }
   static ZK_DEV T zero() { return f29_zero(); }
   static ZK_DEV T one() { return f29_const(P29::ONE); }
   template <int K>
@@ -454,18 +502,21 @@ struct QPoint {
   typename QF::T X, Y, ZZ, ZZZ;
 };
 template <class QF>
-ZK_DEV bool qp_is_inf(const QPoint<QF>& p) { return QF::is_zero(p.ZZ); }
+ZK_DEV bool qp_is_inf(const QPoint<QF>& p) { return QF::template is_zero<2>(p.ZZ); }  // ZZ < 2p
 template <class QF>
 ZK_DEV QPoint<QF> qp_inf() { return {QF::one(), QF::one(), QF::zero(), QF::zero()}; }
 using G1Q = QPoint<Q29>;
 ZK_DEV G1Q g1q_from(const G1P& p) {
   return {Q29::from_fq(p.X), Q29::from_fq(p.Y), Q29::from_fq(p.ZZ), Q29::from_fq(p.ZZZ)};
 }
-ZK_DEV G1P g1q_to(const G1Q& p) {
-  return {Q29::to_fq(p.X), Q29::to_fq(p.Y), Q29::to_fq(p.ZZ), Q29::to_fq(p.ZZZ)};
+ZK_DEV G1P g1q_to(const G1Q& p) {  // canonical coordinates out
+  return {Q29::to_fq(Q29::canon(p.X)), Q29::to_fq(Q29::canon(p.Y)), Q29::to_fq(Q29::canon(p.ZZ)),
+          Q29::to_fq(Q29::canon(p.ZZZ))};
 }
 
 // dbl-2008-s-1 by levels: {U^2, X^2} -> {U V, X V, V ZZ, M^2} -> {M (S - X3), W Y, W ZZZ}
+// Bounds (X < 8p, Y < 4p, ZZ, ZZZ < 2p in): U < 8p; V, X2 < 2p (64 p^2); M < 6p; W, S, ZZ3, M2
+// < 2p (36 p^2); X3 < 6p; S - X3 < 8p; Y3's products < 2p (48 p^2), Y3 < 4p.
 template <class QF>
 ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
   using T = typename QF::T;
@@ -479,9 +530,9 @@ ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
   const T W = QF::template bcast<0>(t), S = QF::template bcast<1>(t), ZZ3 = QF::template bcast<2>(t),
           M2 = QF::template bcast<3>(t);
   QPoint<QF> r;
-  r.X = QF::sub(M2, QF::dbl(S));
-  t = QF::mul(QF::pick4(q, M, W, W, W), QF::pick4(q, QF::sub(S, r.X), p.Y, p.ZZZ, p.ZZZ));
-  r.Y = QF::sub(QF::template bcast<0>(t), QF::template bcast<1>(t));
+  r.X = QF::template sub<4>(M2, QF::dbl(S));
+  t = QF::mul(QF::pick4(q, M, W, W, W), QF::pick4(q, QF::template sub<6>(S, r.X), p.Y, p.ZZZ, p.ZZZ));
+  r.Y = QF::template sub<2>(QF::template bcast<0>(t), QF::template bcast<1>(t));
   r.ZZ = ZZ3;
   r.ZZZ = QF::template bcast<2>(t);
   return r;
@@ -489,6 +540,9 @@ ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
 
 // add-2008-s by levels: {U1, U2, S1, S2} -> {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2} -> {P PP, U1 PP, ZZ PP}
 // -> {R (Q - X3), S1 PPP, ZZZ PPP}
+// Bounds (both points X < 8p, Y < 4p, ZZ, ZZZ < 2p): U1, U2, S1, S2 < 2p (16 p^2); P, R < 4p;
+// PP, R2, Z12, ZZZ12 < 2p; PPP, Q, ZZ3 < 2p; X3 < 8p; Q - X3 < 10p; Y3's products < 2p
+// (40 p^2), Y3 < 4p.
 template <class QF>
 ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
   using T = typename QF::T;
@@ -497,9 +551,9 @@ ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
   T t = QF::mul(QF::pick4(q, p.X, o.X, p.Y, o.Y), QF::pick4(q, o.ZZ, p.ZZ, o.ZZZ, p.ZZZ));
   const T U1 = QF::template bcast<0>(t), U2 = QF::template bcast<1>(t), S1 = QF::template bcast<2>(t),
           S2 = QF::template bcast<3>(t);
-  const T P = QF::sub(U2, U1), R = QF::sub(S2, S1);
-  if (QF::is_zero(P)) {
-    if (QF::is_zero(R)) return quad_dbl<QF>(p, q);
+  const T P = QF::template sub<2>(U2, U1), R = QF::template sub<2>(S2, S1);
+  if (QF::template is_zero<4>(P)) {
+    if (QF::template is_zero<4>(R)) return quad_dbl<QF>(p, q);
     return qp_inf<QF>();
   }
   t = QF::mul(QF::pick4(q, P, R, p.ZZ, p.ZZZ), QF::pick4(q, P, R, o.ZZ, o.ZZZ));
@@ -509,10 +563,10 @@ ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
   const T PPP = QF::template bcast<0>(t), Q = QF::template bcast<1>(t);
   QPoint<QF> r;
   r.ZZ = QF::template bcast<2>(t);
-  r.X = QF::sub(QF::sub(R2, PPP), QF::dbl(Q));
-  const T QX = QF::sub(Q, r.X);
+  r.X = QF::template sub<4>(QF::template sub<2>(R2, PPP), QF::dbl(Q));
+  const T QX = QF::template sub<8>(Q, r.X);
   t = QF::mul(QF::pick4(q, R, S1, ZZZ12, R), QF::pick4(q, QX, PPP, PPP, QX));
-  r.Y = QF::sub(QF::template bcast<0>(t), QF::template bcast<1>(t));
+  r.Y = QF::template sub<2>(QF::template bcast<0>(t), QF::template bcast<1>(t));
   r.ZZZ = QF::template bcast<2>(t);
   return r;
 }
@@ -592,7 +646,7 @@ ZK_DEV G1Q glv_quad_mul(const G1P* __restrict__ res, const GlvScalar* __restrict
     if (nib) {
       const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
       G1Q t = tab[(d < 0 ? -d : d) - 1];
-      const F29 ny = Q29::sub(Q29::zero(), t.Y);
+      const F29 ny = Q29::sub<4>(Q29::zero(), t.Y);  // Y < 4p
 #pragma unroll
       for (int i = 0; i < 9; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
       acc = quad_add<Q29>(acc, t, q);
