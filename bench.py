@@ -103,14 +103,19 @@ def draw_rs(n):
 
 def timed_run(key, warm_w, steps_w, rs, ctx, dist):
     """W untimed steps, then exactly K timed steps (K x slots proofs in one batch call) bracketed
-    by barrier + synchronize on both sides; returns (max-over-ranks elapsed seconds, proofs)."""
+    by barrier + synchronize on both sides; returns (max-over-ranks elapsed seconds, proofs, host
+    CPU seconds of this process over the timed region -- the warm-up's graph captures excluded)."""
     if warm_w:
         key.prove_batch(warm_w)
     _barrier(ctx, dist)
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t_start = time.perf_counter()
     proofs = key.prove_batch(steps_w, rs)      # K steps x `slots` proofs, `slots` in flight
     _barrier(ctx, dist)
-    return _max_over_ranks(time.perf_counter() - t_start, dist), proofs
+    dt = time.perf_counter() - t_start
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    busy = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    return _max_over_ranks(dt, dist), proofs, busy
 
 
 def verify_all(ctx, zk, proofs, pubs_of):
@@ -495,8 +500,8 @@ def extra_circuit_leg(ctx, rank, world, circuit, steps, slots, dist):
     log(f"[bench r{rank}] {circuit}: {b.n_constraints} constraints, domain {key.domain_size} "
         f"(setup {time.perf_counter() - t0:.1f} s)")
     n = steps * slots
-    elapsed, proofs = timed_run(key, [res[i % 2] for i in range(slots)], [res[i % 2] for i in range(n)],
-                                draw_rs(n), ctx, dist)
+    elapsed, proofs, _ = timed_run(key, [res[i % 2] for i in range(slots)], [res[i % 2] for i in range(n)],
+                                   draw_rs(n), ctx, dist)
     pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]
     ok = _sum_over_ranks(verify_all(ctx, zk, proofs, lambda i: pubs[i % 2]), dist)
     if ok != world * n:
@@ -921,10 +926,8 @@ def main():
     # on a fresh process on others)
     lat = latency_leg(key, res)
     log(f"[bench r{rank}] one proof alone: {lat}")
-    ru0 = resource.getrusage(resource.RUSAGE_SELF)
-    elapsed, proofs = timed_run(key, warm_w, steps_w, rs, ctx, dist)
-    ru1 = resource.getrusage(resource.RUSAGE_SELF)
-    host_cpu = {"main": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) * 1e3 / n_timed, 3)}
+    elapsed, proofs, busy = timed_run(key, warm_w, steps_w, rs, ctx, dist)
+    host_cpu = {"main": round(busy * 1e3 / n_timed, 3)}
     assert len(proofs) == n_timed and all(len(p) == 256 for p in proofs)
     pubs = [w[76 + 32:76 + 32 * (1 + key.n_public)] for w in wts]   # wtns v2: header 76 B, wire 0 = 1
     verified = verify_all(ctx, zk, proofs, lambda i: pubs[i % len(pubs)])

@@ -46,7 +46,7 @@ def _worker(rank, world, port, out_path):
     pin = bench.pin_host_cores(rank, world)   # the N>1 rule: each rank its share of the host cores
     dist.init_process_group("gloo", rank=rank, world_size=world)
     key = _StubKey(rank)
-    elapsed, proofs = bench.timed_run(key, [0], list(range(8)), None, _StubCtx(), dist)
+    elapsed, proofs, _ = bench.timed_run(key, [0], list(range(8)), None, _StubCtx(), dist)
     verified = bench._sum_over_ranks(len(proofs), dist)
     host = bench.host_report(rank, rank, dist, pin, {"main": 0.5 + rank})
     prof = {k: (0.0, 0, 0.0, 0.0) for k in bench.PROFILED}
