@@ -1245,19 +1245,24 @@ hipError_t msm_sort_p(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, co
   uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
   uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
   return msm_with_c(b.c, [&](auto cc) {
-    constexpr int C = decltype(cc)::value, NL = msm_sort_nl<C, P>();
-    static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
-    hipLaunchKernelGGL((k_msm_bin_count<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
-                       per_blk, cnt);
-    hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
-    if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
-      pl.ko_sorted = 1;
-      hipLaunchKernelGGL((k_msm_bin_scatter<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start,
-                         b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
-      hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
-                         bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+    constexpr int C = decltype(cc)::value;
+    if constexpr (P > 1 && C > 16) {  // proof pairs: 2 NB bucket keys must fit a u16
+      return hipErrorInvalidValue;
+    } else {
+      constexpr int NL = msm_sort_nl<C, P>();
+      static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
+      hipLaunchKernelGGL((k_msm_bin_count<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
+                         per_blk, cnt);
+      hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
+      if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
+        pl.ko_sorted = 1;
+        hipLaunchKernelGGL((k_msm_bin_scatter<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start,
+                           b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
+        hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
+                           bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+      }
+      return hipGetLastError();
     }
-    return hipGetLastError();
   });
 }
 
