@@ -20,6 +20,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "verifiable-federated-training-with-zero-knowledge-proofs-zk-fl-_amd"))
 
 
+def _thread_cpu():
+    """{tid: (name, utime + stime ticks)} of this process's threads."""
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        fields = st[st.rindex(")") + 2:].split()
+        out[tid] = (name, int(fields[11]) + int(fields[12]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=48)
@@ -27,6 +42,8 @@ def main():
     ap.add_argument("--slots", type=int, default=20)
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--latency", type=int, default=0)
+    ap.add_argument("--threads", action="store_true",
+                    help="also print each thread's host CPU over the timed batch (/proc/self/task)")
     args = ap.parse_args()
     from zkfl import circuits, clients, native, wprog, zkey
     b = circuits.build("sgd_verified", 128, 4, 7, 1000)
@@ -61,10 +78,17 @@ def main():
         res = wp.compute_resident(key, [wprog.input_bytes(b, o) for o in objs])
         key.prove_batch([res[i % 4] for i in range(args.warmup * args.slots)])
         ctx.synchronize()
+        c0 = _thread_cpu() if args.threads else None
         t0 = time.perf_counter()
         key.prove_batch([res[i % 4] for i in range(n)])
     ctx.synchronize()
     dt = time.perf_counter() - t0
+    if args.threads and c0 is not None:
+        c1 = _thread_cpu()
+        tick = os.sysconf("SC_CLK_TCK")
+        use = sorted(((c1[t][1] - c0.get(t, (None, 0))[1], c1[t][0], t) for t in c1), reverse=True)
+        for ticks, name, tid in use[:8]:
+            print(f"  thread {tid} {name}: {ticks / tick * 1e3 / n:.3f} ms host CPU per proof", flush=True)
     print(f"{os.environ.get('ZKFL_LIB', 'in-tree')}: {n / dt:.2f} proofs/s ({dt / n * 1e3:.3f} ms per proof)")
 
 
