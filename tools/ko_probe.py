@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--slots", type=int, default=20)
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--latency", type=int, default=0)
+    ap.add_argument("--c5-first", action="store_true", help="run bench.py's config-5 leg first (as bench.py does)")
     ap.add_argument("--threads", action="store_true",
                     help="also print each thread's host CPU over the timed batch (/proc/self/task)")
     args = ap.parse_args()
@@ -50,6 +51,10 @@ def main():
     objs = [clients.Client(c + 1, 128, 4, 7, clients.JsLcg(12345 + c)).training_input(128, 1000, 100000000)[0]
             for c in range(4)]
     ctx = native.Context(0)
+    if args.c5_first:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        bench.c5_leg(ctx, 0, 1, 4, 8, None, 0)
     zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
     key = native.ProvingKey(ctx, zk)
     key.set_slots(args.slots)
