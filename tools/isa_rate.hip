@@ -29,6 +29,9 @@ __global__ void __launch_bounds__(256) krate(uint64_t* out, double* dout, int it
     } else if (KIND == 3) {
 #define FMA64(i) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(f[i]) : "v"(fx), "v"(fy));
       REP8(FMA64)
+    } else if (KIND == 6) {
+#define ADDF64(i) asm volatile("v_add_f64 %0, %1, %0" : "+v"(f[i]) : "v"(fx));
+      REP8(ADDF64)
     } else if (KIND == 4) {
 #define ADD64(i) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
       REP8(ADD64)
@@ -54,8 +57,8 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  const char* names[6] = {"v_mad_u64_u32", "v_addc_co_u32", "v_mul_lo_u32", "v_fma_f64", "v_lshl_add_u64", "v_add_u32"};
-  for (int k = 0; k < 6; k++) {
+  const char* names[7] = {"v_mad_u64_u32", "v_addc_co_u32", "v_mul_lo_u32", "v_fma_f64", "v_lshl_add_u64", "v_add_u32", "v_add_f64"};
+  for (int k = 0; k < 7; k++) {
     for (int rep = 0; rep < 2; rep++) {
       hipEventRecord(a);
       switch (k) {
@@ -64,6 +67,7 @@ int main() {
         case 2: hipLaunchKernelGGL(krate<2>, dim3(blocks), dim3(threads), 0, 0, d, dd, iters); break;
         case 3: hipLaunchKernelGGL(krate<3>, dim3(blocks), dim3(threads), 0, 0, d, dd, iters); break;
         case 4: hipLaunchKernelGGL(krate<4>, dim3(blocks), dim3(threads), 0, 0, d, dd, iters); break;
+        case 6: hipLaunchKernelGGL(krate<6>, dim3(blocks), dim3(threads), 0, 0, d, dd, iters); break;
         default: hipLaunchKernelGGL(krate<5>, dim3(blocks), dim3(threads), 0, 0, d, dd, iters); break;
       }
       hipEventRecord(b);
