@@ -691,11 +691,11 @@ def _cpulist(text):
     return out
 
 
-def _gpu_local_cpus():
-    """Host CPUs local to each visible GPU, in HIP's device order, from sysfs alone (no HIP call:
-    this runs before the rank initializes the runtime).  KFD topology nodes with SIMDs are the GPUs
-    (node order = device order); a node's PCI location gives /sys/bus/pci/devices/<bdf>/local_cpulist.
-    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES (numeric lists) select and reorder them.  [] if unknown."""
+def _gpu_topology():
+    """Host CPUs local to every GPU of the node, in KFD order (= HIP's device order when nothing is
+    hidden), from sysfs alone (no HIP call: this runs before the rank initializes the runtime).  KFD
+    topology nodes with SIMDs are the GPUs; a node's PCI location gives
+    /sys/bus/pci/devices/<bdf>/local_cpulist.  [] if unknown."""
     base = "/sys/class/kfd/kfd/topology/nodes"
     gpus = []
     try:
@@ -715,34 +715,57 @@ def _gpu_local_cpus():
             gpus.append(cpus)
     except (OSError, ValueError):
         return []
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
-        sel = os.environ.get(var)
-        if sel:
-            try:
-                gpus = [gpus[int(x)] for x in sel.split(",") if x.strip()]
-            except (ValueError, IndexError):
-                return []
     return gpus
 
 
-def pin_host_cores(local_rank, local_world):
+def _visible_gpus(n_all):
+    """Indices (into the node's GPUs) this process sees, from ROCR_VISIBLE_DEVICES then
+    HIP_VISIBLE_DEVICES (numeric lists; HIP's list indexes what ROCr left visible); None if neither
+    is set, [] if a list does not parse."""
+    idx = None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        sel = os.environ.get(var)
+        if sel:
+            base = idx if idx is not None else list(range(n_all))
+            try:
+                idx = [base[int(x)] for x in sel.split(",") if x.strip()]
+            except (ValueError, IndexError):
+                return []
+    return idx
+
+
+def pin_host_cores(local_rank, local_world, topo=None, allowed=None, apply=True):
     """With several ranks on one node, pins this rank (before its first HIP call) to the host cores
     local to its GPU, shared evenly with the other ranks whose GPUs hang off the same cores; when
     the topology is unknown or leaves too few allowed cores, to an even 1/local_world share of the
     allowed cores.  The config-5 legs parse input.json and launch ~50 kernels per proof on host
     threads (0.6-0.9 ms of host CPU per proof, ~1.2-1.8 cores per rank), so 8 unpinned ranks
     compete for the same cores and cross NUMA nodes.  One rank alone is left unpinned.
-    ZKFL_PIN=0 disables it.  Returns what was done (reported per rank in the bench line)."""
-    allowed = sorted(os.sched_getaffinity(0))
+    ZKFL_PIN=0 disables it.  Which GPU is this rank's: local rank r drives device r of what it sees
+    (bench.py: `local_rank % n_dev`); when a launcher gives each rank ONE visible GPU
+    (ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES = its index), that GPU, and the peers are counted
+    on the node's whole topology with rank r on node GPU r.  topo / allowed / apply: the node's GPU
+    topology, the allowed cores and whether to set the affinity (tests fake an 8-GPU node).
+    Returns what was done (reported per rank in the bench line)."""
+    allowed = sorted(allowed if allowed is not None else os.sched_getaffinity(0))
     info = {"allowed_cpus": len(allowed), "pinned": False, "cpus": len(allowed), "source": "none"}
     if local_world <= 1 or os.environ.get("ZKFL_PIN", "1") == "0":
         return info
-    gpus = _gpu_local_cpus()
+    node = topo if topo is not None else _gpu_topology()
+    sel = _visible_gpus(len(node)) if node else None
+    if node and sel is not None and len(sel) == 1:
+        gpu_of = [node[r % len(node)] for r in range(local_world)]   # rank r on node GPU r
+        mine = node[sel[0]]
+    else:
+        seen = [node[i] for i in sel] if (node and sel) else ([] if sel == [] else node)
+        gpu_of = [seen[r % len(seen)] for r in range(local_world)] if seen else []
+        mine = gpu_of[local_rank] if seen else None
     share, source = None, "even split of the allowed cores"
-    if gpus:
-        mine = gpus[local_rank % len(gpus)]
+    if mine is not None:
         pool = [c for c in allowed if c in set(mine)]
-        peers = [r for r in range(local_world) if gpus[r % len(gpus)] == mine]
+        peers = [r for r in range(local_world) if gpu_of[r] == mine]
+        if local_rank not in peers:
+            peers = sorted(peers + [local_rank])
         n, k = len(peers), peers.index(local_rank)
         if len(pool) >= max(2, len(allowed) // (2 * local_world)) * n:
             share = pool[k * len(pool) // n:(k + 1) * len(pool) // n]
@@ -750,9 +773,13 @@ def pin_host_cores(local_rank, local_world):
     if not share:
         n = len(allowed)
         share = allowed[local_rank * n // local_world:(local_rank + 1) * n // local_world] or allowed
-    os.sched_setaffinity(0, share)
-    info.update(pinned=True, cpus=len(share), source=source, cpulist=f"{share[0]}-{share[-1]}"
-                if share == list(range(share[0], share[-1] + 1)) else ",".join(map(str, share)))
+    if apply:
+        os.sched_setaffinity(0, share)
+    info.update(pinned=True, cpus=len(share), source=source, share=share if not apply else None,
+                cpulist=f"{share[0]}-{share[-1]}" if share == list(range(share[0], share[-1] + 1))
+                else ",".join(map(str, share)))
+    if apply:
+        del info["share"]
     return info
 
 

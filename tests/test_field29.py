@@ -107,16 +107,13 @@ def test_sqr_normalized_extremes(f29):
         assert r == m, "square and product differ"
 
 
-def test_inverse_canon_and_affine_add(f29):
-    """The batch-affine pieces (msm_affine.h): Montgomery inversion, canonicalization and the
-    affine addition with canonical inputs and outputs, on real BN254 points."""
+def test_inverse_and_canon(f29):
+    """The assembly's inversion (binary extended Euclid, k_assemble's affine conversions) and the
+    canonicalization, against Python big integers."""
     rng = random.Random(31)
     vals = [1, 2, P - 1, R % P] + [rng.randrange(1, P) for _ in range(40)]
     lifted = [v + rng.randrange(2) * P for v in vals]          # inputs < 2p
-    got = f29(["inv " + limbs(v) for v in lifted])
-    for v, (r,) in zip(vals, got):
-        assert r < 2 * P and r % P == pow(v * RINV, -1, P) * R % P
-    got = f29(["invb " + limbs(v) for v in lifted])          # binary extended Euclid, canonical out
+    got = f29(["invb " + limbs(v) for v in lifted])          # canonical out
     for v, (r,) in zip(vals, got):
         assert r == pow(v * RINV, -1, P) * R % P
     # 0 and p (both 0 mod p) have no inverse: 0 comes back at once (it used to halve u = 0 forever,
@@ -126,20 +123,6 @@ def test_inverse_canon_and_affine_add(f29):
     got = f29(["canon " + limbs(v) for v in cv])
     for v, (r,) in zip(cv, got):
         assert r == v % P
-    G = (1, 2)
-    pts = [g1_mul(rng.randrange(1, P), G) for _ in range(30)]
-    cases, want = [], []
-    for i in range(120):
-        a, b = rng.sample(pts, 2)
-        if i % 5 == 0:
-            b = (b[0], (P - b[1]) % P)                       # a signed (negated) base
-        m = lambda v: v * R % P  # noqa: E731
-        cases.append(f"aadd {limbs(m(a[0]))} {limbs(m(a[1]))} {limbs(m(b[0]))} {limbs(m(b[1]))}")
-        want.append(g1_add(a, b))
-    got = f29(cases)
-    for w, (x, y) in zip(want, got):
-        assert x < P and y < P, "affine sum not canonical"
-        assert (x * RINV % P, y * RINV % P) == w
 
 
 def test_below256(f29):

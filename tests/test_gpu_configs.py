@@ -133,10 +133,7 @@ def test_config4_secagg_three_clients_mask_cancel(gpu_ctx):
 # ---------------------------------------------------------------------------
 # Config 5: one federated round, 8 clients x {training, secagg}, keys interleaved
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("pairs", ["0", "1"])
-def test_config5_round_interleaved_multi_key(gpu_ctx, monkeypatch, pairs):
-    """ZKFL_PAIRS=1: two proofs of a key per chain (ProofPair), the witness groups twice as long."""
-    monkeypatch.setenv("ZKFL_PAIRS", pairs)
+def test_config5_round_interleaved_multi_key(gpu_ctx):
     from oracle import cbaseline
     from zkfl import circuits, clients, native, wprog, zkey
     bt = circuits.build("sgd_verified", 8, 4, 3, 1000)

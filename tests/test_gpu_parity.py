@@ -375,16 +375,13 @@ def test_resident_batch_and_errors(gpu_ctx):
     key.close()
 
 
-@pytest.mark.parametrize("pairs,width", [("0", "14"), ("1", "14"), ("0", "16"), ("1", "16")])
-def test_batch_equals_single_proofs(gpu_ctx, monkeypatch, pairs, width):
+@pytest.mark.parametrize("width", ["14", "16"])
+def test_batch_equals_single_proofs(gpu_ctx, monkeypatch, width):
     """A 12-proof batch of a small key over 3 slots (the one-stream chain, every slot's later proofs
-    graph-replayed; with ZKFL_FOLD=1 the folded s pi_A + r pi_B1 MSM, zkfl_key::bRS; with
-    ZKFL_PAIRS=1 two proofs per chain, ProofPair: pair sorts over 2 NB bucket keys, per-half
-    reductions) must equal the same proofs taken alone (the latency schedule, the GLV scalar
+    graph-replayed) must equal the same proofs taken alone (the latency schedule, the GLV scalar
     multiplications) byte for byte, and one of them the oracle's -- at the small keys' 14-bit
     windows (the default for this key) and at the large keys' 16."""
     from zkfl import clients, native, zkey
-    monkeypatch.setenv("ZKFL_PAIRS", pairs)
     monkeypatch.setenv("ZKFL_MSM_C", width)
     b, zk = _setup(gpu_ctx, "balance_unified", 8, 3, 4)
     key = native.ProvingKey(gpu_ctx, zk)

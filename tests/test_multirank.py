@@ -1,5 +1,6 @@
 """bench.py's N>1 control plane (barrier, max-over-ranks timing, summed verification counts, weak-scaling
-value, rank-0 report) on 2 gloo ranks with a stub prover (CPU).  The same path driving the real
+value, rank-0 report) on 2 and 8 gloo ranks with a stub prover (CPU), and the host-core pinning of 8
+ranks on a faked 8-GPU node.  The same path driving the real
 prover on the GPU is tests/test_gpu_multirank.py; there is no data-path collective (independent
 proofs per rank)."""
 import json
@@ -41,6 +42,8 @@ class _StubCtx:
 def _worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     sys.path.insert(0, ROOT)
+    import torch
+    torch.set_num_threads(1)
     import torch.distributed as dist
     import bench
     pin = bench.pin_host_cores(rank, world)   # the N>1 rule: each rank its share of the host cores
@@ -88,6 +91,72 @@ def test_two_rank_gloo_report(tmp_path):
         assert r["pin"]["allowed_cpus"] == allowed
         if allowed >= 2:   # two ranks: disjoint halves of the allowed cores
             assert r["pin"]["pinned"] and r["pin"]["cpus"] == allowed // 2 + (allowed % 2) * r["rank"]
+
+
+def test_eight_rank_gloo_report(tmp_path):
+    """The driver's 8-GPU run, rehearsed on the CPU: 8 ranks, each its stub proofs, rank 0's line
+    counts all 64 proofs at the slowest rank's time, and every rank's host facts reach it."""
+    pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rep8.json")
+    mp.start_processes(_worker, args=(8, _free_port(), out), nprocs=8, join=True, start_method="spawn")
+    rep = json.load(open(out))
+    assert rep["n_gpus"] == 8 and rep["verified"] == 64 and rep["scaling"] == "weak"
+    assert rep["ms_per_step"] >= 8 * 80 / 8 * 0.9           # rank 7: 8 proofs x 80 ms
+    assert abs(rep["value"] - 8 * 8 / (rep["ms_per_step"] * 8 / 1e3)) < 1e-3 * rep["value"] + 1e-6
+    ranks = rep["host"]["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(8))
+    assert [r["host_cpu_ms_per_proof"]["main"] for r in ranks] == [0.5 + r for r in range(8)]
+    allowed = len(os.sched_getaffinity(0))
+    if allowed >= 8:   # this container: 8 cores, one each
+        assert all(r["pin"]["pinned"] and r["pin"]["cpus"] == allowed // 8 for r in ranks)
+
+
+# A node of the driver's kind: 8 GPUs, 2 per NUMA node, 64 host cores per NUMA node
+_NODE = [list(range(64 * (g // 2), 64 * (g // 2) + 64)) for g in range(8)]
+
+
+def _shares(monkeypatch, env=None):
+    sys.path.insert(0, ROOT)
+    import bench
+    out = []
+    for r in range(8):
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+            monkeypatch.delenv(var, raising=False)
+        for k, v in (env(r) if env else {}).items():
+            monkeypatch.setenv(k, v)
+        info = bench.pin_host_cores(r, 8, topo=_NODE, allowed=range(256), apply=False)
+        assert info["pinned"] and info["source"].startswith("GPU-local"), info
+        out.append(info["share"])
+    return out
+
+
+def _check_node_shares(shares):
+    for r, sh in enumerate(shares):
+        assert len(sh) == 32 and set(sh) <= set(_NODE[r]), (r, sh[:4])   # half of its GPU's NUMA node
+    flat = [c for sh in shares for c in sh]
+    assert len(flat) == len(set(flat)) == 256                                 # disjoint, all cores used
+
+
+def test_pin_eight_ranks_gpu_local(monkeypatch):
+    """8 ranks on a faked 8-GPU node (2 GPUs per NUMA node), every GPU visible to every rank
+    (rank r drives device r): disjoint shares of 32 cores, each on its own GPU's NUMA node."""
+    _check_node_shares(_shares(monkeypatch))
+
+
+def test_pin_eight_ranks_one_visible_gpu_each(monkeypatch):
+    """The same node with a launcher that shows each rank only its own GPU (ROCR_VISIBLE_DEVICES=r):
+    the peers are counted on the node's topology, so each rank still gets half of its NUMA node
+    (it used to count all 8 ranks as peers on one GPU's cores)."""
+    _check_node_shares(_shares(monkeypatch, lambda r: {"ROCR_VISIBLE_DEVICES": str(r)}))
+    _check_node_shares(_shares(monkeypatch, lambda r: {"HIP_VISIBLE_DEVICES": str(r)}))
+
+
+def test_pin_unknown_topology_even_split(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    shares = [bench.pin_host_cores(r, 8, topo=[], allowed=range(256), apply=False)["share"] for r in range(8)]
+    assert [len(s) for s in shares] == [32] * 8 and sorted(c for s in shares for c in s) == list(range(256))
 
 
 def test_pin_single_rank_untouched():

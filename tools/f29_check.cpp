@@ -1,7 +1,7 @@
 // Host-side driver for the 29-bit-limb field and point formulas (csrc/field29.h), used by
 // tests/test_field29.py: the formulas are __host__ __device__, so their bound analysis is
 // checked on the CPU against Python big integers.  One operation per stdin line:
-//   mul a b | sqr a | inv a | canon a | aadd x0 y0 x1 y1 | mulsum2 a b c d | below256 a | dbl P | madd P x y | madds P x y neg | add P Q
+//   mul a b | sqr a | invb a | canon a | mulsum2 a b c d | below256 a | dbl P | madd P x y | madds P x y neg | add P Q
 //   g2dbl P | g2madd P x y | g2add P Q   (Fq2 values as two elements: c0 c1)
 //   rmul a b | rsqr a | radd a b | rmulsum4 x0 x1 x2 x3 y0 y1 y2 y3 | rfromplain a | rtoplain a |
 //   rfrom256 a | rto256 a   (Fr in the witness engine's 29-bit form, csrc/fr29.h)
@@ -175,21 +175,10 @@ int main() {
       wr(f29_pack(fr29_to_m256(rd(in)).v));
     } else if (op == "sqr") {
       wr(f29_sqr(rd(in)));
-    } else if (op == "inv") {
-      wr(f29_inv(rd(in)));
     } else if (op == "invb") {
       wr(f29_inv_bgcd(rd(in)));
     } else if (op == "canon") {  // normalized a < 4p -> canonical
       wr(f29_canon_sub<3>(rd(in)));
-    } else if (op == "aadd") {  // canonical affine points (x0, y0) + (x1, y1), x0 != x1
-      Affine<FqOps29> a0, a1;
-      a0.x = rd(in);
-      a0.y = rd(in);
-      a1.x = rd(in);
-      a1.y = rd(in);
-      const Affine<FqOps29> r = f29_affine_add(a0, a1, f29_inv(f29_sub_canon(a1.x, a0.x)));
-      wr(r.x);
-      wr(r.y);
     } else if (op == "mulsum2") {
       F29 a = rd(in), b = rd(in), c = rd(in), d = rd(in);
       wr(f29_mulsum2(a, b, c, d));

@@ -646,8 +646,7 @@ ZK_HD XYZZ<FqOps29> f29_madd_signed(const XYZZ<FqOps29>& p, const Affine<FqOps29
 }
 
 // ---------------------------------------------------------------------------
-// Affine arithmetic for the batch-affine rounds of the G1 accumulation (msm_affine.h): canonical
-// coordinates (< p), one shared inversion per round for all additions of an MSM.
+// Canonicalization and inversion (the assembly's affine conversions, k_assemble)
 // ---------------------------------------------------------------------------
 // normalized a < (k + 1) p -> canonical (< p): k conditional subtractions of p (M: the modulus)
 template <int K, class M = P29>
@@ -671,43 +670,10 @@ ZK_HD F29 f29_canon_sub(F29 a) {
   return a;
 }
 
-// x1 - x0 (canonical inputs) -> normalized, < 2p
-ZK_HD F29 f29_sub_canon(const F29& x1, const F29& x0) {
-  F29 d = f29_ksub(P29::K1_1, x1, x0);
-  f29_norm(d);
-  return d;
-}
-
-// a^-1 (Montgomery: (a R)^-1 R = a^(p-2) R) for normalized a < 2p, a != 0 mod p; fixed
-// square-and-multiply over the bits of p - 2 (254 squarings, 4-bit windows: 63 products).
-ZK_HD F29 f29_inv(const F29& a) {
-  // p - 2 in 4-bit digits, most significant first (p = 0x30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd47)
-  const char* hex = "30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd45";
-  F29 tab[16];
-  tab[0] = f29_const(P29::ONE);
-  tab[1] = a;
-#pragma unroll 1
-  for (int i = 2; i < 16; i++) tab[i] = f29_mul(tab[i - 1], a);
-  F29 r = f29_const(P29::ONE);
-#pragma unroll 1
-  for (int k = 0; k < 64; k++) {
-    const char h = hex[k];
-    const int dgt = h <= '9' ? h - '0' : h - 'a' + 10;
-    if (k) {
-      r = f29_sqr(r);
-      r = f29_sqr(r);
-      r = f29_sqr(r);
-      r = f29_sqr(r);
-    }
-    if (dgt) r = f29_mul(r, tab[dgt]);
-  }
-  return r;
-}
-
-// The same inverse by the binary extended Euclidean algorithm (one lane, no products in the loop:
-// shifts, compares and subtractions of 9-limb values; ~1.4 x 254 steps): the batch-affine root
-// inversion sits on a proof's critical path, where a chain of 316 dependent Montgomery products
-// is ~5x longer.  In: normalized a < 2p, a != 0 mod p (Montgomery form a R); out: a^-1 R, < p.
+// a^-1 by the binary extended Euclidean algorithm (one lane, no products in the loop: shifts,
+// compares and subtractions of 9-limb values; ~1.4 x 254 steps): the assembly's inversions sit on
+// a proof's critical path, where Fermat's chain of ~316 dependent Montgomery products is ~5x
+// longer.  In: normalized a < 2p, a != 0 mod p (Montgomery form a R); out: a^-1 R, < p.
 struct P29Inv {
   // R^3 mod p (R = 2^261): a plain inverse x = (aR)^-1 times R^3 through a Montgomery product is
   // a^-1 R (the Montgomery form of the inverse)
@@ -794,24 +760,6 @@ ZK_HD F29 f29_inv_bgcd(const F29& a_in) {
   }
   const F29 x = f29_is_one_plain(u) ? x1 : x2;  // (a R)^-1, canonical
   return f29_canon_sub<1>(f29_mul(x, f29_const(P29Inv::R3)));
-}
-
-// (x0, y0) + (x1, y1) given inv = (x1 - x0)^-1 (normalized, < 2p), canonical in and out:
-//   dy = y1 + p - y0 < 2p; lambda = dy inv < p + 4p / 169 = 1.03p; lambda^2 < 1.01p;
-//   x2 = lambda^2 + 2p - x0 - x1 < 3.01p -> canonical (3 subtractions);
-//   y2 = lambda (x0 + p - x2) + p - y0 < 1.02p + 2p -> canonical (3 subtractions).
-ZK_HD Affine<FqOps29> f29_affine_add(const Affine<FqOps29>& a, const Affine<FqOps29>& b, const F29& inv) {
-  const F29 dy = f29_sub_canon(b.y, a.y);
-  const F29 lam = f29_mul(dy, inv);
-  const F29 l2 = f29_sqr(lam);
-  F29 x2 = f29_ksub(P29::K1_1, l2, a.x);
-  x2 = f29_ksub(P29::K1_1, x2, b.x);
-  f29_norm(x2);
-  x2 = f29_canon_sub<3>(x2);
-  F29 y2 = f29_ksub(P29::K1_1, f29_mul(lam, f29_sub_canon(a.x, x2)), a.y);
-  f29_norm(y2);
-  y2 = f29_canon_sub<3>(y2);
-  return {x2, y2};
 }
 
 // add-2008-s.  In: X, Y < 6p, ZZ, ZZZ < 2p (both).  U1, U2, S1, S2 < 1.08p; P = U2 + 2p - U1,

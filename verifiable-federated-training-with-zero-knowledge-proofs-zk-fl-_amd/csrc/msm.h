@@ -28,7 +28,6 @@
 #pragma once
 #include <algorithm>
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 
 #include "field29.h"
 #include "msm_api.h"
@@ -51,10 +50,6 @@ namespace zkfl {
 // throughput (399.5 vs 400.9 proofs/s, profiles/r02_s5_ab_limb29_g2.log); 2 keeps scratch out.
 #ifndef MSM_G2_WAVES
 #define MSM_G2_WAVES 2
-#endif
-// minimum waves per SIMD of the batch-affine apply/accumulate kernel (msm_affine.h)
-#ifndef MSM_G1_AFF_WAVES
-#define MSM_G1_AFF_WAVES 3
 #endif
 // 1: the next entry's base is loaded while the current one is added (one affine point of
 // registers); 0: loaded after it, latency hidden by the other waves only.  Without it G1 at 4
@@ -85,13 +80,12 @@ namespace zkfl {
 // Compute type -> storage: how the point kernels read and write the stored points.  G1 and plain
 // Fq2 hold a point per lane; Fq2PairOps holds it across a lane pair (component h of every
 // coordinate in lane 2k+h), reading and writing Affine/XYZZ<Fq2Ops> memory.
-// PIECES: 16-B LDS-DMA pieces of one lane's share of a base record; REC: Affine<S> slots per stored
-// base record (the record stride of the window table).
+// PIECES: 16-B LDS-DMA pieces of one lane's share of a base record.
 template <class F>
 struct MsmIO {
   using S = F;
   static constexpr int LANES = 1;
-  static constexpr int PIECES = 4, REC = 1;
+  static constexpr int PIECES = 4;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return p[i]; }
   // the 16-B piece q < 4 of this lane's share of base i, and a share rebuilt from its pieces
   // (G1: the whole 64-B point; the LDS-DMA prefetch of k_msm_accumulate)
@@ -110,7 +104,7 @@ template <>
 struct MsmIO<Fq2PairOps> {
   using S = Fq2Ops;
   static constexpr int LANES = 2;
-  static constexpr int PIECES = 4, REC = 1;
+  static constexpr int PIECES = 4;
   static ZK_DEV Affine<Fq2PairOps> ld_aff(const Affine<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
     const uint32_t h = pair_half();
@@ -148,7 +142,7 @@ template <class F>
 struct MsmIOSameLayout {
   using S = FqOps;
   static constexpr int LANES = 1;
-  static constexpr int PIECES = 4, REC = 1;
+  static constexpr int PIECES = 4;
   static ZK_DEV Affine<F> ld_aff(const Affine<S>* p, size_t i) { return reinterpret_cast<const Affine<F>*>(p)[i]; }
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
     return reinterpret_cast<const uint4*>(p + i) + q;
@@ -167,41 +161,24 @@ template <>
 struct MsmIO<FqOpsLazy> : MsmIOSameLayout<FqOpsLazy> {};
 // G1 in 29-bit limbs (field29.h): the same 8 x 32-bit storage, converted on every load / store
 // (stored values < 2^256, in the 2^261 Montgomery domain)
-// (MSM_G1_PACKED: the bases as 128-B records of x, y in nine 29-bit limbs each, k_msm_pack29)
+// (pre-packed 128-B records of nine 29-bit limbs per coordinate were measured neutral in round 5,
+// 430.4 vs 430.1 proofs/s for twice the window table, and removed: DESIGN.md §13)
 template <>
 struct MsmIO<FqOps29> {
   using S = FqOps;
   static constexpr int LANES = 1;
-  static constexpr int PIECES = MSM_G1_PACKED ? 5 : 4, REC = MSM_G1_PACKED ? 2 : 1;
+  static constexpr int PIECES = 4;
   static ZK_DEV Affine<FqOps29> ld_aff(const Affine<S>* p, size_t i) {
-#if MSM_G1_PACKED
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(p + REC * i);
-    Affine<FqOps29> a;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      a.x.v[k] = w[k];
-      a.y.v[k] = w[9 + k];
-    }
-    return a;
-#else
     const Affine<S> a = p[i];
     return {f29_pack(a.x.v), f29_pack(a.y.v)};
-#endif
   }
   static ZK_DEV const uint4* piece(const Affine<S>* p, size_t i, int q) {
-    return reinterpret_cast<const uint4*>(p + REC * i) + q;
+    return reinterpret_cast<const uint4*>(p + i) + q;
   }
   // the record's words as read from LDS (word by word: a memcpy through HIP's uint4 was lowered to
   // byte permutes, ~45 VALU instructions per entry)
   static ZK_DEV Affine<FqOps29> from_pieces(const uint32_t (&w)[4 * PIECES]) {
     Affine<FqOps29> a;
-#if MSM_G1_PACKED
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      a.x.v[k] = w[k];
-      a.y.v[k] = w[9 + k];
-    }
-#else
     uint32_t x[8], y[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -210,7 +187,6 @@ struct MsmIO<FqOps29> {
     }
     a.x = f29_pack(x);
     a.y = f29_pack(y);
-#endif
     return a;
   }
   static ZK_DEV XYZZ<FqOps29> ld(const XYZZ<S>* p, size_t i) {
@@ -236,7 +212,7 @@ template <>
 struct MsmIO<Fq2Pair29> {
   using S = Fq2Ops;
   static constexpr int LANES = 2;
-  static constexpr int PIECES = 4, REC = 1;
+  static constexpr int PIECES = 4;
   static ZK_DEV Affine<Fq2Pair29> ld_aff(const Affine<S>* p, size_t i) {
     const Fq* q = reinterpret_cast<const Fq*>(p + i);
     const uint32_t h = pair_half();
@@ -292,29 +268,6 @@ static __global__ void __launch_bounds__(256) k_msm_to_m29(Fq* __restrict__ a, s
 #pragma unroll
   for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
   a[i] = fp_mul(a[i], c);
-}
-// MSM_G1_PACKED: n expanded G1 bases (64-B records, 2^256 domain) -> 128-B records of x, y in nine
-// 29-bit limbs each, 2^261 domain (the layout MsmIO<FqOps29> reads), words 18..31 zero
-static __global__ void __launch_bounds__(256) k_msm_pack29(const Affine<FqOps>* __restrict__ in, size_t n,
-                                                          uint32_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  Fq c;
-#pragma unroll
-  for (int k = 0; k < 8; k++) c.v[k] = P29::C261[k];
-  const Affine<FqOps> a = in[i];
-  const F29 x = f29_pack(fp_mul(a.x, c).v), y = f29_pack(fp_mul(a.y, c).v);
-  uint32_t w[32];
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    w[k] = x.v[k];
-    w[9 + k] = y.v[k];
-  }
-#pragma unroll
-  for (int k = 18; k < 32; k++) w[k] = 0;
-  uint4* o = reinterpret_cast<uint4*>(out + 32 * i);
-#pragma unroll
-  for (int q = 0; q < 8; q++) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 // MSM_G2_F29 (default): lane pairs in 29-bit limbs (Fq2Pair29); 0: 32-bit limbs (Fq2PairOps).
 #ifndef MSM_G2_F29
@@ -379,55 +332,8 @@ ZK_DEV uint32_t msm_window(const uint32_t (&s)[8], int j) {
   return x & ((1u << C) - 1u);
 }
 
-// Signed-digit decomposition; entry (i, j) -> key = bucket, val = (i*W+j) | sign<<31, written
-// window-major (position j*n + i: consecutive lanes store consecutive words; the sort that
-// follows does not care about the input order).  Also counts the non-zero digits into *nnz
-// (the sorted prefix the accumulation covers).
-template <int C>
-__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
-                                                           const uint32_t* __restrict__ extra,
-                                                           const uint32_t* __restrict__ sidx, uint32_t extra_start,
-                                                           size_t n, uint16_t* __restrict__ keys,
-                                                           uint32_t* __restrict__ vals, uint32_t* __restrict__ nnz) {
-  constexpr int W = msm_w_of(C), NB = msm_nb_of(C);
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t cnt = 0;
-  if (i < n) {
-    const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
-    const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
-    const uint4* sp = reinterpret_cast<const uint4*>(src);
-    uint4 a = sp[0], b = sp[1];
-    uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < W; j++) {
-      uint32_t raw = msm_window<C>(s, j);
-      int32_t d = (int32_t)(raw + carry);
-      if (d > NB) {
-        d -= (1 << C);
-        carry = 1;
-      } else {
-        carry = 0;
-      }
-      uint32_t key = MSM_KEY_NONE, val = 0;
-      if (d != 0) {
-        const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-        key = mag - 1;
-        val = (uint32_t)(i * W + j) | (d < 0 ? 0x80000000u : 0u);
-        cnt++;
-      }
-      keys[(size_t)j * n + i] = (uint16_t)key;
-      vals[(size_t)j * n + i] = val;
-    }
-  }
-  // one atomic per wave
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(nnz, cnt);
-}
-
 // ---------------------------------------------------------------------------
-// Bucket sort of the digits (the default; MSM_SORT_ROCPRIM=1 keeps the rocPRIM radix sort).
+// Bucket sort of the digits (rocPRIM's onesweep radix sort until round 2: DESIGN.md §5).
 // Keys are (c-1)-bit bucket numbers, so two counting passes put every non-zero digit in bucket
 // order with no look-back and no memsets:
 //   count   per block of bases: digits -> LDS histogram of the high key bits -> cnt[bin][block]
@@ -439,21 +345,16 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
 // Zero digits are dropped (the accumulation reads only the first nnz pairs).  The order inside
 // a bucket is arbitrary: a bucket's sum does not depend on it, and the proof is affine.
 // ---------------------------------------------------------------------------
-// Proof pairs (P = 2, small keys: msm_sort_pair): the digits of two proofs' scalars over the same
-// bases sort as ONE problem with 2 NB bucket keys, proof p's buckets at p NB ("virtual bases"
-// i + p n); the accumulation and stitching run unchanged over the doubled key range and the bucket
-// reduction takes each half apart (msm_tails_pair).  The high bins stay MSM_SORT_HB: a pair sorts
-// one more low bit inside each (MSM_SORT_LB + 1).
 constexpr int MSM_SORT_T = 256;           // threads per block in count / scatter
 constexpr int MSM_SORT_HB = 1 << MSM_SORT_HIGH_BITS; // high bins (every window width)
-// key bits sorted inside a high bin of a P-proof sort at window width C, and its low counters
-template <int C, int P>
+// key bits sorted inside a high bin at window width C, and its low counters
+template <int C>
 constexpr int msm_sort_lb() {
-  return C - 1 - MSM_SORT_HIGH_BITS + P - 1;
+  return C - 1 - MSM_SORT_HIGH_BITS;
 }
-template <int C, int P>
+template <int C>
 constexpr int msm_sort_nl() {
-  return 1 << msm_sort_lb<C, P>();
+  return 1 << msm_sort_lb<C>();
 }
 constexpr int MSM_SORT_MAXBLK = 32768 / MSM_SORT_HB; // count/scatter blocks (the scan holds cnt in LDS)
 static_assert(MSM_SORT_HB <= MSM_SORT_T, "bucket sort split");
@@ -461,24 +362,12 @@ constexpr int MSM_SORT_BT = 1024;         // threads of the scan workgroup
 constexpr int MSM_SORT_BINT = MSM_SORT_BIN_THREADS;  // threads per high-bin workgroup
 static_assert(MSM_SORT_HB * MSM_SORT_MAXBLK == 32 * MSM_SORT_BT, "scan: 32 counters per thread");
 
-// The scalars of one sort: proof p's scalar vector and extra slots (p < P)
-struct MsmScalars {
-  const uint32_t* sc[2];
-  const uint32_t* ex[2];
-};
-
-// Signed digits of virtual base v (base i = v mod n of proof p = v / n): fn(key, val) for every
-// non-zero digit, key = bucket + p NB (as k_msm_digits for P = 1).
-template <int C, int P, class Fn>
-ZK_DEV void msm_for_digits(const MsmScalars& S, const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t n,
-                           size_t v, Fn&& fn) {
-  static_assert(P == 1 || C <= 16, "proof pairs: 2 NB bucket keys in a u16");
+// Signed digits of base i: fn(key, val) for every non-zero digit d of its scalar (window j),
+// key = |d| - 1 (the bucket), val = (i W + j) | sign << 31
+template <int C, class Fn>
+ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ extra,
+                           const uint32_t* __restrict__ sidx, uint32_t extra_start, size_t i, Fn&& fn) {
   constexpr int W = msm_w_of(C), NB = msm_nb_of(C);
-  const uint32_t p = P > 1 && v >= n ? 1u : 0u;
-  const size_t i = v - p * n;
-  const uint32_t* __restrict__ scalars = P > 1 && p ? S.sc[1] : S.sc[0];
-  const uint32_t* __restrict__ extra = P > 1 && p ? S.ex[1] : S.ex[0];
-  const uint32_t koff = p * NB;
   const uint32_t si = sidx ? sidx[i] : (uint32_t)i;
   const uint32_t* src = si < extra_start ? scalars + (size_t)si * 8 : extra + (size_t)(si - extra_start) * 8;
   const uint4* sp = reinterpret_cast<const uint4*>(src);
@@ -493,34 +382,33 @@ ZK_DEV void msm_for_digits(const MsmScalars& S, const uint32_t* __restrict__ sid
     if (carry) d -= (1 << C);
     if (d != 0) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      fn(koff + mag - 1, (uint32_t)(i * W + j) | (d < 0 ? 0x80000000u : 0u));
+      fn(mag - 1, (uint32_t)(i * W + j) | (d < 0 ? 0x80000000u : 0u));
     }
   }
 }
 
-// n: bases per proof; the blocks cover the P n virtual bases
-template <int C, int P>
-__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const MsmScalars S, const uint32_t* __restrict__ sidx,
-                                                            uint32_t extra_start, size_t n, size_t per_blk,
-                                                            uint32_t* __restrict__ cnt) {
+template <int C>
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint32_t* __restrict__ scalars,
+                                                            const uint32_t* __restrict__ extra,
+                                                            const uint32_t* __restrict__ sidx, uint32_t extra_start,
+                                                            size_t n, size_t per_blk, uint32_t* __restrict__ cnt) {
   ZK_WT(WT_SORT_COUNT);
   ZK_LIGHT();
-  constexpr int LB = msm_sort_lb<C, P>();
+  constexpr int LB = msm_sort_lb<C>();
   __shared__ uint32_t h[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
   __syncthreads();
-  const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
+  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<C, P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
+    msm_for_digits<C>(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
   __syncthreads();
   if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
 // cnt[HB * nblk] (bin-major) -> exclusive offsets in place; bin_start[HB + 1]; *nnz.
-// The scan keeps all 32 K counters in LDS (~139 KB): gfx950's 160 KB per workgroup.  Any other
-// device target must use the rocPRIM sort (MSM_SORT_ROCPRIM=1).
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !MSM_SORT_ROCPRIM
-#error "the bucket sort's scan needs gfx950's 160 KB of LDS: build with MSM_SORT_ROCPRIM=1 for this target"
+// The scan keeps all 32 K counters in LDS (~139 KB): gfx950's 160 KB per workgroup.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "the bucket sort's scan needs gfx950's 160 KB of LDS"
 #endif
 static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* __restrict__ cnt, uint32_t nblk,
                                                                    uint32_t* __restrict__ bin_start,
@@ -566,20 +454,22 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* _
   }
 }
 
-template <int C, int P>
-__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const MsmScalars S, const uint32_t* __restrict__ sidx,
-                                                              uint32_t extra_start, size_t n, size_t per_blk,
+template <int C>
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const uint32_t* __restrict__ scalars,
+                                                              const uint32_t* __restrict__ extra,
+                                                              const uint32_t* __restrict__ sidx, uint32_t extra_start,
+                                                              size_t n, size_t per_blk,
                                                               const uint32_t* __restrict__ cnt,
                                                               uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   ZK_WT(WT_SORT_SCATTER);
   ZK_LIGHT();
-  constexpr int LB = msm_sort_lb<C, P>();
+  constexpr int LB = msm_sort_lb<C>();
   __shared__ uint32_t cur[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
-  const size_t nv = P * n, i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < nv ? i0 + per_blk : nv;
+  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<C, P>(S, sidx, extra_start, n, i, [&](uint32_t key, uint32_t val) {
+    msm_for_digits<C>(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t val) {
       const uint32_t p = atomicAdd(&cur[key >> LB], 1u);
       keys[p] = (uint16_t)key;
       vals[p] = val;
@@ -785,7 +675,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
 }
 
 }  // namespace zkfl
-#include "msm_affine.h"
 namespace zkfl {
 
 // Item count of stitching level `level` (>= 1), derived on the device from nnz.
@@ -1035,7 +924,7 @@ hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n, int c) {
   b.n = n;
   b.c = c;
   using IO = MsmIO<typename MsmCompute<F>::type>;
-  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * msm_w_of(c) * IO::REC * sizeof(Affine<F>)));
+  ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * msm_w_of(c) * sizeof(Affine<F>)));
   return hipSuccess;
 }
 
@@ -1059,24 +948,12 @@ hipError_t msm_bases_set(MsmBases<F>& b, const Affine<F>* d_bases, const uint32_
   }
   using FC = typename MsmCompute<F>::type;
   const size_t m = b.n * msm_w_of(b.c);
-  auto expand = [&](Affine<F>* out) {
-    return msm_with_c(b.c, [&](auto cc) {
+  if (b.n)
+    ZK_CHECK(msm_with_c(b.c, [&](auto cc) {
       hipLaunchKernelGGL((k_msm_expand<F, decltype(cc)::value>), dim3(zk_grid(b.n, 64)), dim3(64), 0, st, d_bases,
-                         b.n, out);
+                         b.n, b.bases_w);
       return hipSuccess;
-    });
-  };
-  if constexpr (MsmIO<FC>::REC == 2) {  // MSM_G1_PACKED: expand into a temporary table, then pack
-    if (!m) return hipGetLastError();
-    Affine<F>* tmp = nullptr;
-    ZK_CHECK(hipMallocAsync(reinterpret_cast<void**>(&tmp), m * sizeof(Affine<F>), st));
-    ZK_CHECK(expand(tmp));
-    hipLaunchKernelGGL(k_msm_pack29, dim3(zk_grid(m, 256)), dim3(256), 0, st, tmp, m,
-                       reinterpret_cast<uint32_t*>(b.bases_w));
-    ZK_CHECK(hipFreeAsync(tmp, st));
-    return hipGetLastError();
-  }
-  if (b.n) ZK_CHECK(expand(b.bases_w));
+    }));
   if constexpr (std::is_same<FC, FqOps29>::value || std::is_same<FC, Fq2Pair29>::value) {
     const size_t nfq = m * (sizeof(Affine<F>) / sizeof(Fq));
     if (nfq)
@@ -1094,15 +971,9 @@ hipError_t msm_scratch_alloc(MsmScratch<F>& s, size_t cap, int c, hipStream_t st
   ZK_CHECK(hipMalloc(&s.keys_out, m * sizeof(uint16_t)));
   ZK_CHECK(hipMalloc(&s.vals_in, m * sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&s.vals_out, m * sizeof(uint32_t)));
-#if MSM_SORT_ROCPRIM
-  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, s.sort_tmp_bytes, s.keys_in, s.keys_out, s.vals_in, s.vals_out, m, 0,
-                                     16, st));
-#else
   s.sort_tmp_bytes = (MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_HB + 1) * sizeof(uint32_t);
-#endif
   ZK_CHECK(hipMalloc(&s.sort_tmp, s.sort_tmp_bytes));
-  if constexpr (std::is_same<F, FqOps>::value)
-    if (MSM_G1_AFFINE) ZK_CHECK(msm_aff_alloc(s.aff, m));
+  (void)st;
   return hipSuccess;
 }
 
@@ -1111,7 +982,6 @@ void msm_scratch_free(MsmScratch<F>& s) {
   void* ptrs[] = {s.keys_in, s.keys_out, s.vals_in, s.vals_out, s.sort_tmp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  msm_aff_free(s.aff);
   s = MsmScratch<F>();
 }
 
@@ -1122,8 +992,6 @@ uint32_t msm_resident_chunks() {
 #if !MSM_ADAPTIVE_L
   return 0;
 #else
-  if constexpr (std::is_same<F, FqOps>::value)
-    if (MSM_G1_AFFINE) return 0;  // the batch-affine rounds use the fixed L
   // tests: ZKFL_MSM_TARGET=<chunks> forces a small target, so small MSMs run long chunks too
   if (const char* e = getenv("ZKFL_MSM_TARGET")) return (uint32_t)strtoul(e, nullptr, 10);
   using FC = typename MsmCompute<F>::type;
@@ -1152,19 +1020,13 @@ uint32_t msm_tail_l0(size_t cap) {
   return l < 1 ? 1u : l > 255 ? 255u : l;
 }
 
-// pairs = 2: the tail of a proof pair (msm_sort_pair): cap = both proofs' bases, 2 NB buckets and
-// reduction scratch per half
 template <class F>
-hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int c, int pairs = 1) {
+hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int c) {
   if (c != MSM_C && c != MSM_C_SMALL) return hipErrorInvalidValue;
   t.c = c;
   const size_t m = cap * msm_w_of(c);
   t.target = std::min<uint32_t>(msm_resident_chunks<F>(), 0xFFFFFFu);
   t.l0 = msm_tail_l0<F>(cap);
-  // the batch-affine rounds write their items with the fixed AFF_L: the stitching levels must count
-  // level-0 items with the same chunk length (msm_items_at)
-  if constexpr (std::is_same<F, FqOps>::value)
-    if (MSM_G1_AFFINE) t.l0 = AFF_L;
   t.max_chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) t.max_chunks = std::min<size_t>(t.max_chunks, t.target);  // msm_chunk_len bounds the lanes
   t.item_cap[0] = 2 * t.max_chunks;
@@ -1173,10 +1035,10 @@ hipError_t msm_tail_alloc(MsmTail<F>& t, size_t cap, int c, int pairs = 1) {
     ZK_CHECK(hipMalloc(&t.item_key[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(uint32_t)));
     ZK_CHECK(hipMalloc(&t.item_val[k], (t.item_cap[k] ? t.item_cap[k] : 2) * sizeof(XYZZ<F>)));
   }
-  ZK_CHECK(hipMalloc(&t.buckets, pairs * msm_nb_of(c) * sizeof(XYZZ<F>)));
-  // <= 2 level-1 blocks (fast: 128 lanes) per half
-  ZK_CHECK(hipMalloc(&t.red_a, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
-  ZK_CHECK(hipMalloc(&t.red_s, pairs * MSM_TAIL_RED * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.buckets, msm_nb_of(c) * sizeof(XYZZ<F>)));
+  // <= 2 level-1 blocks (fast: 128 lanes)
+  ZK_CHECK(hipMalloc(&t.red_a, MSM_TAIL_RED * sizeof(XYZZ<F>)));
+  ZK_CHECK(hipMalloc(&t.red_s, MSM_TAIL_RED * sizeof(XYZZ<F>)));
   ZK_CHECK(hipMalloc(&t.nnz, sizeof(uint32_t)));
   ZK_CHECK(hipMalloc(&t.live, MSM_LIVE_LEVELS * sizeof(uint32_t)));
   return hipSuccess;
@@ -1227,80 +1089,50 @@ hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
   return hipGetLastError();
 }
 
-// digits (+ nnz) -> sort by bucket into pl.keys_out / pl.vals_out (the first *nnz pairs).  With the
-// rocPRIM sort *nnz must be zero on entry; the bucket sort writes it.
-// The bucket sort of P proofs' digits over the same bases (P = 2: a proof pair, keys + p NB).
-template <int P, class F>
-hipError_t msm_sort_p(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const MsmScalars& S, hipStream_t st) {
-  const size_t nv = P * b.n;  // virtual bases
-  if (nv > pl.cap) return hipErrorInvalidValue;
-  if (b.n == 0) return hipSuccess;
+// digits (+ nnz) -> sort by bucket into pl.keys_out / pl.vals_out (the first *nnz pairs; the sort
+// writes *nnz)
+template <class F>
+hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
+                    const uint32_t* d_extra, hipStream_t st) {
+  const size_t n = b.n;
+  if (n > pl.cap) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
   // count / scan / scatter / bins (see k_msm_bin_count); keys_in/vals_in hold the high-bin order
-  const size_t per_blk = (nv + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
+  const size_t per_blk = (n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
                              ? (size_t)MSM_SORT_T
-                             : ((nv + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
-  const uint32_t nblk = (uint32_t)((nv + per_blk - 1) / per_blk);
+                             : ((n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
+  const uint32_t nblk = (uint32_t)((n + per_blk - 1) / per_blk);
   if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
   if (b.c != pl.c) return hipErrorInvalidValue;
   uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
   uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
   return msm_with_c(b.c, [&](auto cc) {
     constexpr int C = decltype(cc)::value;
-    if constexpr (P > 1 && C > 16) {  // proof pairs: 2 NB bucket keys must fit a u16
-      return hipErrorInvalidValue;
-    } else {
-      constexpr int NL = msm_sort_nl<C, P>();
-      static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
-      hipLaunchKernelGGL((k_msm_bin_count<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start, b.n,
-                         per_blk, cnt);
-      hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
-      if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
-        pl.ko_sorted = 1;
-        hipLaunchKernelGGL((k_msm_bin_scatter<C, P>), dim3(nblk), dim3(MSM_SORT_T), 0, st, S, b.sidx, b.extra_start,
-                           b.n, per_blk, cnt, pl.keys_in, pl.vals_in);
-        hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
-                           bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
-      }
-      return hipGetLastError();
+    constexpr int NL = msm_sort_nl<C>();
+    static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
+    hipLaunchKernelGGL((k_msm_bin_count<C>), dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
+                       b.extra_start, n, per_blk, cnt);
+    hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
+    if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
+      pl.ko_sorted = 1;
+      hipLaunchKernelGGL((k_msm_bin_scatter<C>), dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
+                         b.extra_start, n, per_blk, cnt, pl.keys_in, pl.vals_in);
+      hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
+                         bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
     }
+    return hipGetLastError();
   });
-}
-
-template <class F>
-hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
-                    const uint32_t* d_extra, hipStream_t st) {
-#if !MSM_SORT_ROCPRIM
-  const MsmScalars S = {{d_scalars, nullptr}, {d_extra, nullptr}};
-  return msm_sort_p<1>(b, pl, nnz, S, st);
-#else
-  if (b.n > pl.cap || b.c != pl.c) return hipErrorInvalidValue;
-  if (b.n == 0) return hipSuccess;
-  const size_t m = b.n * msm_w_of(b.c);
-  size_t need = 0;
-  ZK_CHECK(rocprim::radix_sort_pairs(nullptr, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16, st));
-  if (need > pl.sort_tmp_bytes) return hipErrorInvalidValue;
-  ZK_CHECK(msm_with_c(b.c, [&](auto cc) {
-    hipLaunchKernelGGL(k_msm_digits<decltype(cc)::value>, dim3(zk_grid(b.n, 256)), dim3(256), 0, st, d_scalars,
-                       d_extra, b.sidx, b.extra_start, b.n, pl.keys_in, pl.vals_in, nnz);
-    return hipSuccess;
-  }));
-  if (!(ZK_KNOCKOUT & 2))
-    ZK_CHECK(rocprim::radix_sort_pairs(pl.sort_tmp, need, pl.keys_in, pl.keys_out, pl.vals_in, pl.vals_out, m, 0, 16,
-                                       st));
-  return hipGetLastError();
-#endif
 }
 
 // Accumulation (level 0: fixed chunks, closed runs straight into the buckets, open runs as items)
 // over sorted (bucket, entry) pairs and t.nnz.  The pairs may come from another MSM with the same
 // scalars and base index map (B1's sort serves B2: msm_sort once, accumulate on both curves).
-// pairs = 2: the pairs of a proof pair's sort (msm_sort_p<2>: up to 2 n W entries)
 template <class F>
 hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, MsmTail<F>& t,
-                                 hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr, int pairs = 1) {
+                                 hipStream_t st, Profiler* prof = nullptr, const char* tag = nullptr) {
   if (b.n == 0) return hipSuccess;
   if (b.c != t.c) return hipErrorInvalidValue;
-  const size_t m = pairs * b.n * msm_w_of(b.c);
+  const size_t m = b.n * msm_w_of(b.c);
   size_t chunks = (m + t.l0 - 1) / t.l0;
   if (t.target) chunks = std::min<size_t>(chunks, t.target);  // lanes of msm_chunk_len(nnz, target)
   if (chunks > t.max_chunks) return hipErrorInvalidValue;
@@ -1308,19 +1140,10 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
   using FC = typename MsmCompute<F>::type;
   constexpr int LN = MsmIO<FC>::LANES;
   constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
-  bool done = false;
-  if constexpr (std::is_same<F, FqOps>::value) {
-    if (MSM_G1_AFFINE && t.aff && t.aff->lanes && !(ZK_KNOCKOUT & 64)) {  // batch-affine rounds
-      ZK_CHECK(msm_aff_accumulate<MSM_G1_AFF_WAVES>(b, keys, vals, t, *t.aff, st));
-      // it does not track open runs: stitch every level (the whole flag word, not its low byte)
-      ZK_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(t.live), 1u, 1, st));
-      done = true;
-    }
-  }
   // measurement knob: ZKFL_ACC_PAD_LDS=<bytes> reserves unused LDS per accumulation block, which
   // lowers the number of resident waves without changing the chunking (PMC traffic attribution)
   static const size_t pad_lds = getenv("ZKFL_ACC_PAD_LDS") ? strtoul(getenv("ZKFL_ACC_PAD_LDS"), nullptr, 10) : 0;
-  if (!done && !((ZK_KNOCKOUT & 64) && LN == 1))
+  if (!((ZK_KNOCKOUT & 64) && LN == 1))
     hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), pad_lds, st, keys, vals,
                        b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, msm_target_arg(t), t.live);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
@@ -1335,7 +1158,6 @@ hipError_t msm_accumulate(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t
                           const uint32_t* d_extra, hipStream_t st, Profiler* prof = nullptr,
                           const char* tag = nullptr) {
   ZK_CHECK(msm_sort(b, pl, t.nnz, d_scalars, d_extra, st));
-  if (pl.aff.lanes) t.aff = &pl.aff;  // G1: accumulate through the batch-affine rounds
   return msm_accumulate_sorted(b, pl.keys_out, pl.vals_out, t, st, prof, tag);
 }
 
@@ -1400,26 +1222,6 @@ hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStrea
   return msm_wsum(msm_tail_args<F>(t, outs, n), n, st, fast);
 }
 
-// Tails of n proof-pair MSMs (msm_sort_pair, msm_tail_alloc(.., 2)): the stitching levels over each
-// pair's 2 NB buckets as one MSM, then the reduction of each half apart: outs[2 i + h] = the sum of
-// pair i's proof h.
-template <class F>
-hipError_t msm_tails_pair(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) {
-  if (2 * n > MSM_TAIL_MAX) return hipErrorInvalidValue;
-  ZK_CHECK(msm_stitch(t, n, st));
-  MsmTailArgs<F> ta = {};
-  ta.c = t[0]->c;
-  for (int i = 0; i < n; i++)
-    for (int h = 0; h < 2; h++) {
-      const int y = 2 * i + h;
-      ta.buckets[y] = t[i]->buckets + (size_t)h * msm_nb_of(ta.c);
-      ta.red_a[y] = t[i]->red_a + (size_t)h * MSM_TAIL_RED;
-      ta.red_s[y] = t[i]->red_s + (size_t)h * MSM_TAIL_RED;
-      ta.out[y] = outs[y];
-    }
-  return msm_wsum(ta, 2 * n, st, fast);
-}
-
 template <class F>
 hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const uint32_t* d_scalars,
                    const uint32_t* d_extra, XYZZ<F>* d_out, hipStream_t st, Profiler* prof = nullptr,
@@ -1444,21 +1246,6 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
   }                                                                                                      \
   void msm_scratch_free_##SUF(MsmScratch<F>& s) { msm_scratch_free(s); }                                 \
   hipError_t msm_tail_alloc_##SUF(MsmTail<F>& t, size_t cap, int c) { return msm_tail_alloc(t, cap, c); } \
-  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap, int c) {                               \
-    return msm_tail_alloc(t, cap, c, 2);                                                                 \
-  }                                                                                                      \
-  hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0,  \
-                                 const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st) { \
-    const MsmScalars S = {{sc0, sc1}, {ex0, ex1}};                                                       \
-    return msm_sort_p<2>(b, s, nnz, S, st);                                                              \
-  }                                                                                                      \
-  hipError_t msm_tails_pair_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) { \
-    return msm_tails_pair(t, outs, n, st, fast);                                                         \
-  }                                                                                                      \
-  hipError_t msm_accumulate_sorted_pair_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, \
-                                              MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag) { \
-    return msm_accumulate_sorted(b, keys, vals, t, st, prof, tag, 2);                                    \
-  }                                                                                                      \
   void msm_tail_free_##SUF(MsmTail<F>& t) { msm_tail_free(t); }                                          \
   hipError_t msm_accumulate_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* sc, \
                                   const uint32_t* ex, hipStream_t st, Profiler* prof, const char* tag) { \

@@ -20,7 +20,9 @@ namespace zkfl {
 // The width is chosen per MSM base set (per proving key: msm_pick_c): MSM_C for large keys, where
 // the accumulation dominates, MSM_C_SMALL for keys of at most MSM_SMALL_C_BASES bases, whose
 // proofs are chains of latency-bound reduction launches (config 5: 2,335 vs 2,152 proofs/s at 14
-// vs 16 bits, the metric key 388 vs 427 -- profiles/r05_ab_window_bits.log).
+// vs 16 bits, the metric key 388 vs 427 -- profiles/r05_ab_window_bits.log).  17 bits (15 windows,
+// 2^16 buckets) was measured and rejected in round 5 (config 5 -11%, M within noise:
+// profiles/r05_ab_c17_c5_latency.log, r05_ab_c17_large_keys.log) and is no longer accepted.
 #ifndef MSM_WINDOW_BITS
 #define MSM_WINDOW_BITS 16
 #endif
@@ -37,8 +39,8 @@ __host__ __device__ constexpr int msm_nb_of(int c) { return 1 << (c - 1); }     
 constexpr int MSM_W = msm_w_of(MSM_C);
 constexpr int MSM_NB = msm_nb_of(MSM_C);
 constexpr int MSM_W_MAX = msm_w_of(MSM_C < MSM_C_SMALL ? MSM_C : MSM_C_SMALL);
-static_assert(MSM_C >= 14 && MSM_C <= 17 && MSM_C_SMALL >= 14 && MSM_C_SMALL <= 16,
-              "window width: u16 bucket keys, >= 64 low counters per high bin of the bucket sort");
+static_assert(MSM_C >= 14 && MSM_C <= 16 && MSM_C_SMALL >= 14 && MSM_C_SMALL <= 16,
+              "window width: the widths the GPU parity suite runs (>= 64 low counters per high bin of the bucket sort)");
 // Knock-out builds for marginal-cost measurements (tools/ko_probe.py; proofs are WRONG, timing
 // only): 1 assembly, 2 digit sort, 4 NTT, 8 stitching, 16 bucket reduction, 32 the G2 MSM,
 // 64 the G1 accumulation kernel.  0 in every real build; a non-zero value only compiles together
@@ -50,12 +52,6 @@ static_assert(MSM_C >= 14 && MSM_C <= 17 && MSM_C_SMALL >= 14 && MSM_C_SMALL <= 
 #if ZK_KNOCKOUT != 0 && !defined(ZK_KNOCKOUT_AB_ONLY)
 #error "ZK_KNOCKOUT builds compute wrong proofs: timing A/B only (define ZK_KNOCKOUT_AB_ONLY to acknowledge)"
 #endif
-// 1: digits sorted by rocPRIM's radix sort (A/B builds); 0: the two-pass bucket sort in msm.h
-#ifndef MSM_SORT_ROCPRIM
-#define MSM_SORT_ROCPRIM 0
-#endif
-// the rocPRIM path keys zero digits MSM_KEY_NONE = 0xFFFF, a real bucket at c = 17
-static_assert(!MSM_SORT_ROCPRIM || MSM_C <= 16, "rocPRIM digit sort: c <= 16");
 // high key bits of the bucket sort (its high bins, every window width): the low c - 1 - HIGH_BITS
 // bits are sorted inside one high bin (6 at c = 14, 8 at c = 16, 9 at c = 17)
 #ifndef MSM_SORT_HIGH_BITS
@@ -69,28 +65,8 @@ static_assert(!MSM_SORT_ROCPRIM || MSM_C <= 16, "rocPRIM digit sort: c <= 16");
 #ifndef MSM_SORT_BIN_THREADS
 #define MSM_SORT_BIN_THREADS 1024
 #endif
-// 1: batch-affine rounds in front of the G1 accumulation (msm_affine.h, A/B builds); 0 (default):
-// XYZZ only.  Measured on MI355X: correct (50 GPU parity tests, metric-size proofs equal the C
-// oracle) but 347 vs 421 proofs/s -- 2,818 VALU instructions per entry against 2,509 for the XYZZ
-// kernel (profiles/r03_affine_v2_kernels_counters.txt)
-// 1: G1 expanded bases stored pre-packed for the 29-bit engine -- x and y as nine 29-bit limbs in
-// the 2^261 Montgomery domain (72 B) padded to a 128-B record, one L2 line per base, fetched as
-// five 16-B LDS-DMA pieces -- so the accumulation does no 8 x 32 -> 9 x 29 repacking per entry.
-// A 64-B record already costs a whole 128-B line per gather: twice the HBM
-// footprint of the window table, the same HBM traffic.  0: 64-B records in 8 x 32-bit limbs.
-#ifndef MSM_G1_PACKED
-#define MSM_G1_PACKED 0
-#endif
-#ifndef MSM_G1_AFFINE
-#define MSM_G1_AFFINE 0
-#endif
-static_assert(!(MSM_G1_PACKED && MSM_G1_AFFINE), "the batch-affine rounds read 64-B base records");
 #ifndef MSM_G1_L
-#if MSM_G1_AFFINE
-#define MSM_G1_L 32
-#else
 #define MSM_G1_L 16
-#endif
 #endif
 #ifndef MSM_STITCH_SG
 #define MSM_STITCH_SG 8
@@ -99,7 +75,6 @@ constexpr int MSM_L = MSM_G1_L;            // sorted entries per accumulation la
 constexpr int MSM_SG = MSM_STITCH_SG;      // partial sums per lane in each stitching level
 constexpr int MSM_RB = 64;                 // items per block (one wave) in the weighted bucket reduction
 constexpr uint32_t MSM_ITEM_DUMMY = 0x80000000u;  // stitch item flag: padding (its value is infinity)
-constexpr uint16_t MSM_KEY_NONE = 0xFFFFu; // zero digit (rocPRIM path only): sorted past every bucket
 #ifndef MSM_G2_L
 #define MSM_G2_L 16
 #endif
@@ -152,21 +127,6 @@ struct MsmBases {
   uint32_t extra_start = 0xFFFFFFFFu;
 };
 
-// Device scratch of the batch-affine rounds (msm_affine.h), shared by the G1 MSMs a slot runs one
-// after another.
-struct MsmAffScratch {
-  size_t lanes = 0, wgs = 0;
-  uint32_t* pref = nullptr;      // [2][MSM_L / 2][9][lanes] exclusive prefix products, rounds 1 and 2
-  uint32_t* tree = nullptr;      // [wgs][512][9] workgroup product heaps (node 1 = root, leaves 256..511)
-  uint32_t* wgprod = nullptr;    // [wgs][9]
-  uint32_t* wginv = nullptr;     // [wgs][9]
-  Affine<FqOps>* pts[1] = {nullptr};  // [MSM_L / 2][lanes] round-1 sums
-  uint16_t* key1 = nullptr;      // [MSM_L][lanes] item list after round 1 (descending positions)
-  uint32_t* ref1 = nullptr;      // [MSM_L][lanes]
-  uint8_t* cnt1 = nullptr;       // [lanes]
-  uint32_t* mask2 = nullptr;     // [lanes] round-2 pairing bits (pair i = items 2i, 2i + 1)
-};
-
 // Mutable, per in-flight proof (one stream at a time): digit/sort scratch shared by the MSMs a
 // slot runs one after another.
 template <class F>
@@ -180,7 +140,6 @@ struct MsmScratch {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int ko_sorted = 0;             // sort knock-out builds only: this scratch holds a sort already
-  MsmAffScratch aff;             // G1 with MSM_G1_AFFINE: the batch-affine rounds' scratch
 };
 
 // Per MSM of a proof: what the accumulation leaves for the tail (stitching + reduction), so the
@@ -202,7 +161,6 @@ struct MsmTail {
   uint32_t* live = nullptr;
   uint32_t target = 0;          // accumulation lanes resident at once (msm_chunk_len; 0: fixed L)
   uint32_t l0 = 0;              // minimum entries per accumulation lane (msm_tail_l0)
-  const MsmAffScratch* aff = nullptr;  // G1: batch-affine scratch to accumulate with (not owned)
 };
 
 // msm_chunk_len's argument: resident lanes (bits 0-23) | minimum chunk length (bits 24-31)
@@ -220,7 +178,7 @@ inline int msm_pick_c(size_t n) {
   return n <= (size_t)MSM_SMALL_C_BASES ? MSM_C_SMALL : MSM_C;
 }
 
-constexpr int MSM_TAIL_MAX = 6;  // MSM tails per batched launch (the 4 G1 MSMs of a proof; 3 pairs' halves)
+constexpr int MSM_TAIL_MAX = 4;  // MSM tails per batched launch (the 4 G1 MSMs of a proof)
 constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket set (<= 2 level-1 blocks of 128 lanes)
 
 #define ZKFL_MSM_DECLARE(SUF, F)                                                                    \
@@ -246,15 +204,7 @@ constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket 
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st,     \
                              bool fast = false);                                                      \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \
-                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag); \
-  /* proof pairs (small keys): two proofs' digits over the same bases as one sort with 2 NB bucket  \
-     keys into a pair tail (cap = both proofs' bases); its tails reduce each half: outs[2 i + h] */ \
-  hipError_t msm_tail_alloc_pair_##SUF(MsmTail<F>& t, size_t cap, int c);                           \
-  hipError_t msm_sort_pair_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, uint32_t* nnz, const uint32_t* sc0, \
-                                 const uint32_t* ex0, const uint32_t* sc1, const uint32_t* ex1, hipStream_t st); \
-  hipError_t msm_tails_pair_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast); \
-  hipError_t msm_accumulate_sorted_pair_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals, \
-                                              MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag);
+                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
 
 ZKFL_MSM_DECLARE(g1, FqOps)
 ZKFL_MSM_DECLARE(g2, Fq2Ops)

@@ -290,67 +290,6 @@ __global__ void __launch_bounds__(256) k_proof_start(const uint32_t* __restrict_
   if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ps.live[y][threadIdx.x] = 0;
 }
 
-// A proof pair's first kernel (ProofPair): both witnesses staged from the addresses the host left
-// in the pair's pinned buffer, both proofs' augmentation scalars and r, s, GLV halves (d_rs: r0 s0 |
-// r1 s1 | ks0[4] | ks1[4], the layout k_assemble reads with blockIdx.x = proof), res[3] and res[8]
-// = infinity (the merged C + H), and the pair tails emptied (blockIdx.y = tail).
-struct PairStart {
-  const uint32_t* rs_host[2];   // r, s, GLV halves of proof p (RS_WORDS words, pinned)
-  const uint64_t* w_src_host[2];
-  uint4* w_dst[2];
-  uint32_t w_nvec;
-  Fr* extra[2];
-  uint32_t* d_rs;
-  uint32_t* res;
-  uint4* buckets[4];
-  uint32_t nvec[4];
-  uint32_t* nnz[4];
-  uint32_t* live[4];
-  int n;
-};
-__global__ void __launch_bounds__(256) k_pair_start(const PairStart ps) {
-  ZK_WT(WT_SET_EXTRA);
-  ZK_LIGHT();
-  const int y = blockIdx.y;
-  {
-    __shared__ const uint4* src[2];
-    if (threadIdx.x < 2) src[threadIdx.x] = reinterpret_cast<const uint4*>(*ps.w_src_host[threadIdx.x]);
-    __syncthreads();
-    const size_t nb = (size_t)gridDim.x * gridDim.y * blockDim.x, tot = 2 * (size_t)ps.w_nvec;
-    for (size_t i = ((size_t)y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < tot; i += nb) {
-      const int q = i >= ps.w_nvec;
-      const size_t j = i - (size_t)q * ps.w_nvec;
-      ps.w_dst[q][j] = src[q][j];
-    }
-  }
-  if (y == 0 && blockIdx.x == 2 && threadIdx.x < 2 * RS_WORDS) {
-    const int q = threadIdx.x >= RS_WORDS, w = threadIdx.x - q * RS_WORDS;
-    ps.d_rs[w < 16 ? 16 * q + w : 32 + 32 * q + (w - 16)] = ps.rs_host[q][w];
-  }
-  if (y == 0 && blockIdx.x == 0 && threadIdx.x < 2) {
-    const int q = threadIdx.x;
-    const Fr* rs = reinterpret_cast<const Fr*>(ps.rs_host[q]);
-    Fr one = fp_zero<FrP>();
-    one.v[0] = 1u;
-    const Fr r = rs[0], s = rs[1];
-    ps.extra[q][0] = one;
-    ps.extra[q][1] = r;
-    ps.extra[q][2] = s;
-    ps.extra[q][3] = fp_from_mont(fp_neg(fp_mul(fp_to_mont(r), fp_to_mont(s))));
-  }
-  if (y == 0 && blockIdx.x == 1 && threadIdx.x < 2 * sizeof(G1P) / 4) {
-    const int q = threadIdx.x >= sizeof(G1P) / 4;
-    ps.res[(3 + 5 * q) * sizeof(G1P) / 4 + threadIdx.x - q * sizeof(G1P) / 4] = 0u;  // res[3], res[8]: ZZ = 0
-  }
-  if (y >= ps.n) return;
-  uint4* b = ps.buckets[y];
-  const size_t nv = ps.nvec[y];
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
-    b[i] = make_uint4(0, 0, 0, 0);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ps.nnz[y] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < MSM_LIVE_LEVELS) ps.live[y][threadIdx.x] = 0;
-}
-
 template <class F>
 __device__ void store_affine_std(const Affine<F>& a, uint32_t* out);
 
@@ -749,37 +688,6 @@ __global__ void __launch_bounds__(128) k_assemble_c(const G1P* __restrict__ res,
   }
 }
 
-// Folded keys (key_folds_rs): the scalars of the s pi_A + r pi_B1 MSM over bRS -- element i of the
-// witness-and-extras vector x = (w_0 .. w_{nVars-1}, 1, r, s, -rs) times s, then times r:
-// sw[i] = s x_i, sw[nVars + 4 + i] = r x_i (standard form, as the witness)
-__global__ void __launch_bounds__(256) k_rs_scale(const Fr* __restrict__ w, const Fr* __restrict__ extra, uint32_t nV,
-                                                  Fr* __restrict__ sw) {
-  ZK_WT(WT_SET_EXTRA);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, total = nV + 4;
-  if (i >= total) return;
-  const Fr x = fp_to_mont(i < nV ? w[i] : extra[i - nV]);  // x R
-  sw[i] = fp_mul(x, extra[2]);                              // x R s / R = x s
-  sw[total + i] = fp_mul(x, extra[1]);
-}
-
-// The assembly of a folded key: res[3] = s pi_A + r pi_B1 (the bRS MSM), so pi_c = C' + H + res[3]
-// needs one addition and its affine conversion; pi_a and pi_b are converted beside it.
-__global__ void __launch_bounds__(192) k_assemble_f(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
-                                                    uint32_t* __restrict__ proof) {
-  ZK_WT(WT_ASSEMBLE);
-  ZK_LIGHT();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int g = lane >> 2, q = lane & 3;
-  if (wave == 0 && g == 0) {
-    const G1Q C = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
-    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
-  } else if (wave == 1 && lane == 0) {
-    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
-  } else if (wave == 2 && lane == 0) {
-    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
-  }
-}
-
 // Parts of a split proof (zkfl_groth16_prove_part_batch / zkfl_groth16_assemble): a shard's MSM
 // results as XYZZ points, every coordinate in standard form (so the parts cross process boundaries
 // in a defined encoding without an inversion per point): A' (32 words) | B1' (32) | B2' (64: each
@@ -964,7 +872,6 @@ struct ProofSlot {
   MsmScratch<Fq2Ops> g2s;
   MsmTail<Fq2Ops> g2t;
   Fr* extra = nullptr;  // [4] blinding scalars 1, r, s, -rs (= h + n: the extra slots follow h)
-  Fr* sw = nullptr;     // folded keys: [2 (nVars + 4)] scalars s w | s extra | r w | r extra (k_rs_scale)
   Fr* abc = nullptr;  // [3n]
   Fr* abc_head = nullptr;  // [ceil(K / ABC_L)] ABC segmented-sum partials
   Fr* abc_tail = nullptr;
@@ -1009,35 +916,6 @@ struct ProofSlot {
   uint8_t* out_part = nullptr;    // split proofs: where the 768 part bytes go (nullable)
 };
 
-// Two proofs of one small key through ONE chain of launches (batches with ZKFL_PAIRS=1,
-// zkfl_key::pairs; an A/B knob, see key_pairs).  The idea: config 5's 16 proofs in flight are
-// chains of ~37 small kernels whose summed kernel time (3.1 ms per proof,
-// profiles/r05_c5_kernels_8slots.csv) is well under the ~7.5 ms a chain takes under load, and more
-// chains (slots) than 8 per key oversubscribe the hardware queues (10 slots: 1,167 vs 2,139
-// proofs/s), so half the launches per proof should have paid.  A pair sorts both proofs' digits as
-// one problem with 2 NB bucket keys (msm_sort_pair: proof p's buckets at p NB), so the accumulations
-// and stitching levels run once for both; only the bucket reductions take the halves apart
-// (msm_tails_pair), and ABC / NTT stay per proof.  Pair k runs on slot k's stream (no more streams,
-// no more hardware queues), its per-proof vectors in two stream-less half slots.
-struct ProofPair {
-  ProofSlot* slot = nullptr;      // the key's slot whose stream this pair uses (not owned)
-  ProofSlot* half[2] = {nullptr, nullptr};  // per-proof vectors: abc, h | extra, witness stage (owned)
-  hipEvent_t ev_done = nullptr;
-  MsmScratch<FqOps> g1s;          // the pair sorts (A, B1 = B2, C + H), 2 x the bases each
-  MsmTail<FqOps> g1t[3];          // A, B1, C + H pair tails (2 NB buckets)
-  MsmTail<Fq2Ops> g2t;            // B2's pair tail; counts with B1's nnz
-  G1P* res = nullptr;             // [2][5]: proof p's A', B1', C' + H, (infinity), unused
-  G2P* resB2 = nullptr;           // [2]
-  uint32_t* d_rs = nullptr;       // r0 s0 | r1 s1 (16 words each), then GLV halves [2][4] (k_assemble's ks)
-  uint8_t* pinned = nullptr;      // proofs (2 x 256) | r, s, GLV halves (2 x 256 at 512) | witness addresses (at 1024)
-  hipGraph_t g = nullptr;         // the pair chain, captured on the pair's second use
-  hipGraphExec_t ex = nullptr;
-  uint32_t direct = 0;
-  bool busy = false;
-  uint8_t* out_proof[2] = {nullptr, nullptr};
-};
-constexpr size_t PAIR_RS_OFF = 512, PAIR_RS_STRIDE = 256, PAIR_W_OFF = 1024;
-
 #ifndef ZK_NO_SHARE_B
 #define ZK_NO_SHARE_B 0  // 1: B2 sorts its own digits (A/B builds)
 #endif
@@ -1061,11 +939,6 @@ struct zkfl_key {
   // the extra pointer = the slot's h vector, whose extra slots 1, r, s, -rs follow it).  bC / bH
   // stay for the parity hook (zkfl_debug_prove_parts returns C and H apart).
   MsmBases<FqOps> bCH;
-  // Small keys (key_folds_rs): s pi_A + r pi_B1 as ONE more MSM instead of the assembly's GLV scalar
-  // multiplications -- A's bases (with alpha1, delta1) then B1's (beta1, delta1), scalars s w | r w
-  // (k_rs_scale): sum = s (alpha + sum w A + r delta) + r (beta + sum w B1 + s delta).
-  MsmBases<FqOps> bRS;
-  bool fold = false;
   // the parity hook's zeros (zkfl_debug_prove_parts, first call): with C and H merged it runs the
   // C + H MSM twice, once with a zero h (C alone) and once with a zero witness (H alone), so the key
   // holds no separate C and H bases (they were ~0.5 GB of expanded bases per key at 2^18)
@@ -1074,7 +947,6 @@ struct zkfl_key {
   int msm_c = MSM_C;     // window bits of every base set of the key (msm_pick_c of its largest)
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
-  std::vector<ProofPair*> pairs;  // proof pairs of batches (small keys), pair k on slot k's stream
   int max_slots = 3;
   // Split proofs (zkfl_zkey_load_shard): this key holds base i of every query only when
   // i % nshards == shard, and the alpha/beta/delta augmentation bases only on shard 0, so its
@@ -1117,7 +989,7 @@ void slot_release(ProofSlot* s) {
   msm_scratch_free_g2(s->g2s);
   msm_tail_free_g2(s->g2t);
   void* ptrs[] = {s->abc, s->abc_head, s->abc_tail, s->h, s->res, s->resB2, s->d_rs, s->d_parts,
-                  s->w_stage, s->sw};  // extra lives in h
+                  s->w_stage};  // extra lives in h
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->pinned) (void)hipHostFree(s->pinned);
@@ -1146,24 +1018,6 @@ void slot_release(ProofSlot* s) {
 
 int graph_mode();
 
-void pair_release(ProofPair* pr) {
-  if (!pr) return;
-  if (pr->slot && pr->slot->st_main) (void)hipStreamSynchronize(pr->slot->st_main);
-  if (pr->ex) (void)hipGraphExecDestroy(pr->ex);
-  if (pr->g) (void)hipGraphDestroy(pr->g);
-  for (ProofSlot* h : pr->half) slot_release(h);
-  msm_scratch_free_g1(pr->g1s);
-  for (auto& t : pr->g1t) msm_tail_free_g1(t);
-  pr->g2t.nnz = nullptr;  // g1t[1]'s
-  msm_tail_free_g2(pr->g2t);
-  void* ptrs[] = {pr->res, pr->resB2, pr->d_rs};
-  for (void* q : ptrs)
-    if (q) (void)hipFree(q);
-  if (pr->pinned) (void)hipHostFree(pr->pinned);
-  if (pr->ev_done) (void)hipEventDestroy(pr->ev_done);
-  delete pr;
-}
-
 // Release a slot's latency-schedule streams and events (made again on its next batch of one).
 void slot_drop_lowlat(ProofSlot* s) {
   for (hipStream_t& st : s->st_lat)
@@ -1183,7 +1037,7 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
   ProofSlot* s = new ProofSlot();
   *out = s;
   const size_t nV = k->nVars, n = k->n;
-  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n, k->bCH.n, k->bRS.n});
+  const size_t cap1 = std::max<size_t>({k->bA.n, k->bB1.n, k->bC.n, k->bH.n, k->bCH.n});
   hipStream_t st = k->ctx->st;
   ZK_CHECK(hipStreamCreateWithFlags(&s->st_main, hipStreamNonBlocking));
   // One stream per slot by default: a slot's proof is a serial chain and throughput comes from
@@ -1202,10 +1056,8 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     ZK_CHECK(hipMemsetAsync(x.vals_out, 0, cap1 * msm_w_of(c) * sizeof(uint32_t), st));
   }
 #endif
-  // tail 3 is H's; with C and H merged the parity hook uses it for the C + H MSM, a folded key
-  // for s pi_A + r pi_B1
-  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n),
-                          std::max({k->bH.n, k->bCH.n, k->bRS.n})};
+  // tail 3 is H's; with C and H merged the parity hook uses it for the C + H MSM
+  const size_t caps[4] = {k->bA.n, k->bB1.n, std::max(k->bC.n, k->bCH.n), std::max(k->bH.n, k->bCH.n)};
   for (int i = 0; i < 4; i++) ZK_CHECK(msm_tail_alloc_g1(s->g1t[i], caps[i], c));
   ZK_CHECK(msm_scratch_alloc_g2(s->g2s, k->bB2.n, c, st));
   ZK_CHECK(msm_tail_alloc_g2(s->g2t, k->bB2.n, c));
@@ -1215,7 +1067,6 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     s->nnz_alias = true;
   }
   if (graph_mode()) ZK_CHECK(hipMalloc(&s->w_stage, nV * 32));
-  if (k->fold) ZK_CHECK(hipMalloc(&s->sw, 2 * (nV + 4) * 32));
   ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
   s->extra = s->h + n;
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
@@ -1245,74 +1096,6 @@ int get_slot(zkfl_key* k, size_t idx, ProofSlot** out) {
     k->slots.push_back(s);
   }
   *out = k->slots[want];
-  return ZKFL_OK;
-}
-
-// A pair's per-proof vectors: a slot without streams or MSM structures
-hipError_t half_create(zkfl_key* k, ProofSlot** out) {
-  ProofSlot* s = new ProofSlot();
-  *out = s;
-  const size_t n = k->n;
-  ZK_CHECK(hipMalloc(&s->w_stage, (size_t)k->nVars * 32));
-  ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));
-  s->extra = s->h + n;
-  ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
-  const size_t abc_chunks = (k->K + ABC_L - 1) / ABC_L + 1;
-  ZK_CHECK(hipMalloc(&s->abc_head, abc_chunks * 32));
-  ZK_CHECK(hipMalloc(&s->abc_tail, abc_chunks * 32));
-  return hipSuccess;
-}
-
-hipError_t pair_create(zkfl_key* k, ProofSlot* slot, ProofPair** out) {
-  ProofPair* pr = new ProofPair();
-  *out = pr;
-  pr->slot = slot;
-  for (ProofSlot*& h : pr->half) ZK_CHECK(half_create(k, &h));
-  ZK_CHECK(hipEventCreateWithFlags(&pr->ev_done, hipEventDisableTiming));
-  const size_t cap = std::max<size_t>({k->bA.n, k->bB1.n, k->bCH.n});
-  const int c = k->msm_c;
-  ZK_CHECK(msm_scratch_alloc_g1(pr->g1s, 2 * cap, c, k->ctx->st));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[0], 2 * k->bA.n, c));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[1], 2 * k->bB1.n, c));
-  ZK_CHECK(msm_tail_alloc_pair_g1(pr->g1t[2], 2 * k->bCH.n, c));
-  ZK_CHECK(msm_tail_alloc_pair_g2(pr->g2t, 2 * k->bB2.n, c));
-  ZK_CHECK(hipFree(pr->g2t.nnz));  // B2 counts with B1's nnz (the same sort)
-  pr->g2t.nnz = pr->g1t[1].nnz;
-  ZK_CHECK(hipMalloc(&pr->res, 10 * sizeof(G1P)));
-  ZK_CHECK(hipMalloc(&pr->resB2, 2 * sizeof(G2P)));
-  ZK_CHECK(hipMalloc(&pr->d_rs, 2 * 64 + 8 * sizeof(GlvScalar)));
-  ZK_CHECK(hipHostMalloc(&pr->pinned, 2048, hipHostMallocCoherent));
-  return hipStreamSynchronize(k->ctx->st);
-}
-
-// ZKFL_PAIRS=1 (an A/B knob, off; read per batch): batches of a small key run their proofs two at a
-// time through one chain (ProofPair).  Bit-exact (the GPU suite passes with it on), but config 5
-// measured 1,714 vs 2,154 proofs/s at 8 slots per key, and 2,098 / 2,158 at 4 pair slots against
-// 2,133 at 8 single slots (profiles/r05_ab_c5_pairs.log): the launches a pair saves do not set the
-// pace -- about 16 proofs in flight do, however they are grouped.
-bool key_pairs(const zkfl_key* k) {
-  const char* e = getenv("ZKFL_PAIRS");
-  const int on = e ? atoi(e) : 0;
-  static const int lim = getenv("ZKFL_PAIRS_LOGN") ? atoi(getenv("ZKFL_PAIRS_LOGN")) : 16;
-  return on && MSM_MERGE_CH && !ZK_KNOCKOUT && k->share_b && k->nshards == 1 && k->logn <= lim &&
-         !k->ctx->prof.on && !k->ctx->prof.serialize;
-}
-
-int get_pair(zkfl_key* k, size_t idx, ProofPair** out) {
-  const size_t want = idx % (size_t)k->max_slots;
-  while (k->pairs.size() <= want) {
-    ProofSlot* slot = nullptr;
-    int rc = get_slot(k, k->pairs.size(), &slot);
-    if (rc) return rc;
-    ProofPair* pr = nullptr;
-    hipError_t e = pair_create(k, slot, &pr);
-    if (e != hipSuccess) {
-      pair_release(pr);
-      return hip_fail(e, "proof pair allocation");
-    }
-    k->pairs.push_back(pr);
-  }
-  *out = k->pairs[want];
   return ZKFL_OK;
 }
 
@@ -1390,8 +1173,6 @@ void key_release(zkfl_key* k) {
   if (!k) return;
   wpipe_release(k->wpipe);
   k->wpipe = nullptr;
-  for (ProofPair* pr : k->pairs) pair_release(pr);
-  k->pairs.clear();
   for (ProofSlot* s : k->slots) slot_release(s);
   k->slots.clear();
   msm_bases_free_g1(k->bA);
@@ -1399,7 +1180,6 @@ void key_release(zkfl_key* k) {
   msm_bases_free_g1(k->bC);
   msm_bases_free_g1(k->bH);
   msm_bases_free_g1(k->bCH);
-  msm_bases_free_g1(k->bRS);
   msm_bases_free_g2(k->bB2);
   if (k->dbg_zero) (void)hipFree(k->dbg_zero);
   ntt_plan_free(k->ntt);
@@ -1476,19 +1256,6 @@ bool lowlat_fast_wsum() {
 // shorter-chain reduction in batches too: their proofs are chains of small latency-bound kernels
 // that leave most of the GPU idle (config-5 wave trace: SIMD share 0.135 with a wave resident 99%
 // of the time), so the reduction's extra waves are free and its shorter chain is not.
-// ZKFL_FOLD=1 (an A/B knob, off): small keys (domain <= 2^ZKFL_FOLD_LOGN, default 2^16) fold the
-// assembly's scalar multiplications s pi_A + r pi_B1 into one more MSM (zkfl_key::bRS): k_assemble's
-// four 128-bit GLV multiplications in one wave are ~0.8 ms of a small proof's ~3.4 ms of kernels,
-// the extra MSM (A's and B1's bases, 2 x nVars scalars) a sort, an accumulation and a fourth tail.
-// Bit-exact, but config 5 measured 2,095 vs 2,165 proofs/s without it (3 same-box alternations,
-// profiles/r05_ab_c5_fold_wait.log): under 16 proofs in flight the assembly overlaps other chains,
-// the extra launches and tail work do not.
-bool key_folds_rs(int logn, uint32_t nshards) {
-  static const int on = getenv("ZKFL_FOLD") ? atoi(getenv("ZKFL_FOLD")) : 0;
-  static const int lim = getenv("ZKFL_FOLD_LOGN") ? atoi(getenv("ZKFL_FOLD_LOGN")) : 16;
-  return on && MSM_MERGE_CH && nshards == 1 && logn <= lim;
-}
-
 bool small_key_fast_wsum(const zkfl_key* k) {
   static const int logn = getenv("ZKFL_FAST_WSUM_LOGN") ? atoi(getenv("ZKFL_FAST_WSUM_LOGN")) : 16;
   return lowlat_fast_wsum() && k->logn <= logn;
@@ -1709,13 +1476,11 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   int pp = prof->begin("prove", st);
   const bool lowlat_path =
       lowlat && plain == 0 && MSM_MERGE_CH && k->share_b && !prof->serialize && !s->st_g2 && !ZK_KNOCKOUT;
-  // a folded key's s pi_A + r pi_B1 MSM (tail 3, res[3]) instead of the assembly's scalar multiplications
-  const bool fold = k->fold && !lowlat_path && MSM_MERGE_CH && plain == 0 && s->sw;
   {
     // the tails this chain accumulates into: G1 A, B1, C (+ H), [H]; G2 B2 when it shares B1's sort
     // on this stream (a separate G2 stream's msm_run empties its own).  The condition is the body's
     // `share` below: a slot with a second stream under serialized profiling shares too.
-    const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1 && !fold) ? 3 : 4;
+    const int ng1 = lowlat_path || (MSM_MERGE_CH && plain != 1) ? 3 : 4;
     const bool g2 = lowlat_path || (k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32));
     ProofStart ps = {};
     auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
@@ -1728,7 +1493,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     const size_t nb = msm_nb_of(k->msm_c);
     for (int i = 0; i < ng1; i++) add(s->g1t[i].buckets, nb * sizeof(G1P), s->g1t[i].nnz, s->g1t[i].live);
     if (g2) add(s->g2t.buckets, nb * sizeof(G2P), s->g2t.nnz, s->g2t.live);
-    uint32_t* res3 = MSM_MERGE_CH && plain != 1 && !fold ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
+    uint32_t* res3 = MSM_MERGE_CH && plain != 1 ? reinterpret_cast<uint32_t*>(s->res + 3) : nullptr;
     if (s->w_stage && d_w == s->w_stage) {  // graph replay (enqueue_proof): stage the witness here
       ps.w_src_host = reinterpret_cast<const uint64_t*>(s->pinned + W_PTR_OFF);
       ps.w_dst = reinterpret_cast<uint4*>(s->w_stage);
@@ -1754,7 +1519,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   const bool split_ch = MSM_MERGE_CH && plain == 1;
   if (split_ch && !k->dbg_zero) return fail(ZKFL_E_ARG, "parity hook: zeros not allocated");
   const uint32_t* Z = (const uint32_t*)k->dbg_zero;
-  const int ntails = merge && !fold ? 3 : 4;
+  const int ntails = merge ? 3 : 4;
   // Stage order.  Every slot runs the same chain, so under load the slots move as a convoy: the
   // accumulations fill the GPU one at a time, and the slots that leave them together reach ABC +
   // NTT together -- the wave timeline (tools/wtrace.py) showed stretches of ~4 ms with no
@@ -1782,12 +1547,6 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   if (light_first) {
     const int rc = abc_ntt();
     if (rc) return rc;
-  }
-  if (fold) {
-    const uint32_t nV4 = k->nVars + 4;
-    hipLaunchKernelGGL(k_rs_scale, dim3((nV4 + 255) / 256), dim3(256), 0, st, d_w, s->extra, k->nVars, s->sw);
-    HIP_TRY(msm_accumulate_g1(k->bRS, sA, s->g1t[3], (const uint32_t*)s->sw, nullptr, st, prof, "msm_accumulate_g1"),
-            "msm rs");
   }
   HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
   if (share) {
@@ -1834,12 +1593,9 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
-    if (fold)
-      hipLaunchKernelGGL(k_assemble_f, dim3(1), dim3(192), 0, st, s->res, s->resB2, proof_out(s));
-    else
-      hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
-                         reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64),
-                         proof_out(s));
+    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
+                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64),
+                       proof_out(s));
     prof->end(pa, st, 1.0);
   }
   prof->end(pp, st, 1.0);
@@ -1918,7 +1674,8 @@ int enqueue_proof(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, const
 // host core for the whole wait: it was most of config 5's host CPU per proof (0.55-0.57 ms, 1.2
 // cores busy at ~2,100 proofs/s).  A batch (poll = true) polls instead, sleeping ZKFL_WAIT_US
 // (default 50) microseconds between queries: 0.13-0.16 ms per proof, 0.3 cores, throughput within
-// the spread (2,091 vs 2,095 proofs/s, 3 same-box alternations, profiles/r05_ab_c5_fold_wait.log);
+// the spread (2,091 vs 2,095 proofs/s, 3 same-box alternations, profiles/r05_ab_c5_fold_wait.log,
+// which A/Bs the waits beside a since-removed fold knob);
 // the scheduler refills a freed slot up to that much later, ~0.1% of an M step.  A proof alone (the
 // latency path) keeps the spin.  ZKFL_WAIT_US=0 spins everywhere.
 static hipError_t host_wait(hipEvent_t ev, bool poll) {
@@ -1936,122 +1693,6 @@ int wait_slot(ProofSlot* s, bool poll = false) {
   if (s->out_proof) memcpy(s->out_proof, s->pinned, 256);
   if (s->out_part) memcpy(s->out_part, s->pinned + 512, PART_WORDS * 4);
   s->busy = false;
-  return ZKFL_OK;
-}
-
-// The chain of a proof pair (ProofPair) on its slot's stream: the witnesses staged by k_pair_start,
-// ABC + NTT per proof, then A, B1 (+ B2 on B1's pairs) and C + H each as one pair MSM, the G2 and G1
-// tails with per-half reductions (small keys: the short-chain reduction), and k_assemble over both
-// proofs (blockIdx.x = proof) into the pair's pinned buffer.
-int enqueue_pair_body(zkfl_ctx* ctx, zkfl_key* k, ProofPair* pr) {
-  Profiler* prof = &ctx->prof;
-  hipStream_t st = pr->slot->st_main;
-  {
-    PairStart ps = {};
-    for (int q = 0; q < 2; q++) {
-      ps.rs_host[q] = reinterpret_cast<const uint32_t*>(pr->pinned + PAIR_RS_OFF + q * PAIR_RS_STRIDE);
-      ps.w_src_host[q] = reinterpret_cast<const uint64_t*>(pr->pinned + PAIR_W_OFF + 8 * q);
-      ps.w_dst[q] = reinterpret_cast<uint4*>(pr->half[q]->w_stage);
-      ps.extra[q] = pr->half[q]->extra;
-    }
-    ps.w_nvec = (uint32_t)((size_t)k->nVars * 32 / sizeof(uint4));
-    ps.d_rs = pr->d_rs;
-    ps.res = reinterpret_cast<uint32_t*>(pr->res);
-    auto add = [&](void* buckets, size_t bytes, uint32_t* nnz, uint32_t* live) {
-      ps.buckets[ps.n] = static_cast<uint4*>(buckets);
-      ps.nvec[ps.n] = (uint32_t)(bytes / sizeof(uint4));
-      ps.nnz[ps.n] = nnz;
-      ps.live[ps.n] = live;
-      ps.n++;
-    };
-    const size_t nb = msm_nb_of(k->msm_c);
-    for (auto& t : pr->g1t) add(t.buckets, 2 * nb * sizeof(G1P), t.nnz, t.live);
-    add(pr->g2t.buckets, 2 * nb * sizeof(G2P), pr->g2t.nnz, pr->g2t.live);
-    hipLaunchKernelGGL(k_pair_start, dim3(64, ps.n), dim3(256), 0, st, ps);
-  }
-  for (ProofSlot* h : pr->half) {
-    const int rc = enqueue_abc_ntt(k, h, h->w_stage, st, prof);
-    if (rc) return rc;
-  }
-  const uint32_t *W0 = (const uint32_t*)pr->half[0]->w_stage, *W1 = (const uint32_t*)pr->half[1]->w_stage;
-  const uint32_t *E0 = (const uint32_t*)pr->half[0]->extra, *E1 = (const uint32_t*)pr->half[1]->extra;
-  const uint32_t *H0 = (const uint32_t*)pr->half[0]->h, *H1 = (const uint32_t*)pr->half[1]->h;
-  const bool fast = small_key_fast_wsum(k);
-  HIP_TRY(msm_sort_pair_g1(k->bA, pr->g1s, pr->g1t[0].nnz, W0, E0, W1, E1, st), "pair A sort");
-  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bA, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[0], st, prof,
-                                   "msm_accumulate_g1"), "pair A");
-  HIP_TRY(msm_sort_pair_g1(k->bB1, pr->g1s, pr->g1t[1].nnz, W0, E0, W1, E1, st), "pair B sort");
-  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bB1, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[1], st, prof,
-                                   "msm_accumulate_g1"), "pair B1");
-  HIP_TRY(msm_accumulate_sorted_pair_g2(k->bB2, pr->g1s.keys_out, pr->g1s.vals_out, pr->g2t, st, prof,
-                                   "msm_accumulate_g2"), "pair B2");
-  {
-    MsmTail<Fq2Ops>* t2 = &pr->g2t;
-    G2P* o2[2] = {pr->resB2, pr->resB2 + 1};
-    HIP_TRY(msm_tails_pair_g2(&t2, o2, 1, st, fast), "pair B2 tail");
-  }
-  HIP_TRY(msm_sort_pair_g1(k->bCH, pr->g1s, pr->g1t[2].nnz, W0, H0, W1, H1, st), "pair C+H sort");
-  HIP_TRY(msm_accumulate_sorted_pair_g1(k->bCH, pr->g1s.keys_out, pr->g1s.vals_out, pr->g1t[2], st, prof,
-                                   "msm_accumulate_g1"), "pair C+H");
-  {
-    MsmTail<FqOps>* tl[3] = {&pr->g1t[0], &pr->g1t[1], &pr->g1t[2]};
-    G1P* outs[6] = {pr->res + 0, pr->res + 5, pr->res + 1, pr->res + 6, pr->res + 2, pr->res + 7};
-    HIP_TRY(msm_tails_pair_g1(tl, outs, 3, st, fast), "pair tails");
-  }
-  if (!(ZK_KNOCKOUT & 1))
-    hipLaunchKernelGGL(k_assemble, dim3(2), dim3(192), 0, st, pr->res, pr->resB2,
-                       reinterpret_cast<const GlvScalar*>(pr->d_rs + 32), reinterpret_cast<uint32_t*>(pr->pinned));
-  return ZKFL_OK;
-}
-
-// Two jobs of one key through one pair chain: r, s (+ GLV halves) and the witness addresses into the
-// pinned buffer, then the chain -- kernel by kernel on the pair's first use, from its graph after.
-int enqueue_pair(zkfl_ctx* ctx, zkfl_key* k, ProofPair* pr, const Fr* const w[2], const uint32_t* const rs[2]) {
-  for (int q = 0; q < 2; q++) {
-    uint8_t* r = pr->pinned + PAIR_RS_OFF + q * PAIR_RS_STRIDE;
-    memcpy(r, rs[q], 64);
-    GlvScalar* ks = reinterpret_cast<GlvScalar*>(r + 64);
-    glv_split(rs[q] + 8, ks[0], ks[1]);  // s -> s1, s2 (pi_A)
-    glv_split(rs[q], ks[2], ks[3]);      // r -> r1, r2 (B1)
-    const uint64_t src = reinterpret_cast<uint64_t>(w[q]);
-    memcpy(pr->pinned + PAIR_W_OFF + 8 * q, &src, sizeof(src));
-  }
-  hipStream_t st = pr->slot->st_main;
-  if (graph_mode() && pr->direct > 0 && !pr->ex) {
-    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "begin capture");
-    const int rc = enqueue_pair_body(ctx, k, pr);
-    const hipError_t ec = hipStreamEndCapture(st, &pr->g);
-    if (rc) {
-      if (pr->g) (void)hipGraphDestroy(pr->g);
-      pr->g = nullptr;
-      return rc;
-    }
-    HIP_TRY(ec, "end capture");
-    const hipError_t ei = hipGraphInstantiate(&pr->ex, pr->g, nullptr, nullptr, 0);
-    if (ei != hipSuccess) {
-      (void)hipGraphDestroy(pr->g);
-      pr->g = nullptr;
-      pr->ex = nullptr;
-      return hip_fail(ei, "graph instantiate");
-    }
-  }
-  if (pr->ex) {
-    HIP_TRY(hipGraphLaunch(pr->ex, st), "graph launch");
-  } else {
-    pr->direct++;
-    const int rc = enqueue_pair_body(ctx, k, pr);
-    if (rc) return rc;
-  }
-  HIP_TRY(hipEventRecord(pr->ev_done, st), "event");
-  HIP_TRY(hipGetLastError(), "launch");
-  return ZKFL_OK;
-}
-
-int wait_pair(ProofPair* pr, bool poll) {
-  HIP_TRY(host_wait(pr->ev_done, poll), "sync");
-  for (int q = 0; q < 2; q++)
-    if (pr->out_proof[q]) memcpy(pr->out_proof[q], pr->pinned + 256 * q, 256);
-  pr->busy = false;
   return ZKFL_OK;
 }
 
@@ -2075,11 +1716,7 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
   HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
   struct PerKey {
     zkfl_key* key;
-    size_t issued = 0, pairs = 0;  // proofs issued on single slots / pairs issued in this batch
-    bool pend = false;             // a job waiting for its partner (proof pairs)
-    Job pj;
-    size_t pi = 0;
-    uint32_t prs[16];
+    size_t issued = 0;  // proofs issued in this batch
   };
   std::vector<PerKey> cursor;
   // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
@@ -2087,7 +1724,7 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
   static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
   // A/B knob: ZKFL_LOWLAT_BATCH=1 runs every proof of a batch on the low-latency schedule
   static const bool lowlat_batch = getenv("ZKFL_LOWLAT_BATCH") && atoi(getenv("ZKFL_LOWLAT_BATCH")) != 0;
-  auto single = [&](PerKey& pk, size_t i, const Job& J, const uint32_t* rsl) -> int {
+  auto issue = [&](PerKey& pk, size_t i, const Job& J, const uint32_t* rsl) -> int {
     ProofSlot* s = nullptr;
     int rc = get_slot(J.key, pk.issued++, &s);
     if (rc) return rc;
@@ -2127,54 +1764,12 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
       cursor.emplace_back();
       cursor.back().key = J.key;
     }
-    PerKey& pk = cursor[c];
-    if (n > 1 && !J.part_out && key_pairs(J.key)) {  // two proofs of one key per chain
-      if (!pk.pend) {
-        pk.pend = true;
-        pk.pj = J;
-        pk.pi = i;
-        memcpy(pk.prs, rsl, sizeof(rsl));
-        continue;
-      }
-      ProofPair* pr = nullptr;
-      rc = get_pair(J.key, pk.pairs++, &pr);
-      if (rc) break;
-      if (pr->busy) {
-        rc = wait_pair(pr, true);
-        if (rc) break;
-      }
-      for (const Job* x : {&pk.pj, &J})
-        if (x->w_ready) {
-          hipError_t e = hipStreamWaitEvent(pr->slot->st_main, x->w_ready, 0);
-          if (e != hipSuccess) rc = hip_fail(e, "wait for the witness group");
-        }
-      if (rc) break;
-      pr->out_proof[0] = pk.pj.proof_out;
-      pr->out_proof[1] = J.proof_out;
-      const Fr* w[2] = {pk.pj.w, J.w};
-      const uint32_t* rsp[2] = {pk.prs, rsl};
-      rc = enqueue_pair(ctx, J.key, pr, w, rsp);
-      if (rc) break;
-      pr->busy = true;
-      pk.pend = false;
-      continue;
-    }
-    rc = single(pk, i, J, rsl);
+    rc = issue(cursor[c], i, J, rsl);
   }
-  for (auto& pk : cursor)  // a key's odd last job runs alone
-    if (rc == ZKFL_OK && pk.pend) {
-      rc = single(pk, pk.pi, pk.pj, pk.prs);
-      pk.pend = false;
-    }
   for (auto& pk : cursor) {
     for (ProofSlot* s : pk.key->slots)
       if (s->busy) {
         int r2 = wait_slot(s, n > 1);
-        if (rc == ZKFL_OK) rc = r2;
-      }
-    for (ProofPair* pr : pk.key->pairs)
-      if (pr->busy) {
-        int r2 = wait_pair(pr, n > 1);
         if (rc == ZKFL_OK) rc = r2;
       }
   }
@@ -2498,7 +2093,6 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
   k->nPub = nPub;
   k->n = dom;
   k->logn = logn;
-  k->fold = key_folds_rs(logn, nshards);
   k->nC = nC;
   k->K = ncoef;
   k->shard = shard;
@@ -2594,7 +2188,7 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
       o.sidx.swap(c.sidx);
       o.sidx.insert(o.sidx.end(), h.sidx.begin(), h.sidx.end());
     };
-    enum { QA, QB1, QB2, QC, QH, QCH, QRS, NQ };
+    enum { QA, QB1, QB2, QC, QH, QCH, NQ };
     std::vector<Img> im(NQ);
     {
       std::vector<std::thread> th;
@@ -2609,13 +2203,6 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
         th.emplace_back([&] { image(im[QH], 64, z.secH, dom, 0, {}, h_identity); });
       }
       for (auto& t : th) t.join();
-    }
-    if (k->fold) {  // s pi_A + r pi_B1: A's image then B1's, B1's scalars behind the first nVars + 4
-      Img& o = im[QRS];
-      o.img = im[QA].img;
-      o.img.insert(o.img.end(), im[QB1].img.begin(), im[QB1].img.end());
-      o.sidx = im[QA].sidx;
-      for (uint32_t x : im[QB1].sidx) o.sidx.push_back(x + X + 4);
     }
     mark("bases_host");
     size_t most = 0;
@@ -2640,8 +2227,6 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && im[QB1].sidx == im[QB2].sidx && !im[QB1].sidx.empty();
     if (e == hipSuccess && MSM_MERGE_CH) e = upload(k->bCH, im[QCH], false, X);
-    // every index of the folded map addresses the scalar vector sw itself (no extra slots)
-    if (e == hipSuccess && k->fold) e = upload(k->bRS, im[QRS], false, 2 * (X + 4));
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bC, im[QC], false, X);
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bH, im[QH], h_identity, 0xFFFFFFFFu);
     const hipError_t es = hipStreamSynchronize(st);
@@ -2810,11 +2395,6 @@ int zkfl_key_set_slots(zkfl_key* key, int slots) {
   for (ProofSlot* s : key->slots) {
     if (s->busy) return fail(ZKFL_E_ARG, "slots busy");
   }
-  for (ProofPair* pr : key->pairs) {
-    if (pr->busy) return fail(ZKFL_E_ARG, "slots busy");
-  }
-  for (ProofPair* pr : key->pairs) pair_release(pr);  // pair k lives on slot k's stream
-  key->pairs.clear();
   while ((int)key->slots.size() > slots) {
     slot_release(key->slots.back());
     key->slots.pop_back();
@@ -2983,11 +2563,11 @@ int full_prove_piped(zkfl_ctx* ctx, size_t n, KeyOf key_of, ProgOf prog_of, GetI
       uint32_t nw = 0, nin = 0, np = 0;
       wprog_info(pk.prog, &nw, &nin, &np);
       pk.n_in = nin;
-      // one group >= the proofs a key holds in flight (pairs hold two per slot): the witness sets'
+      // one group >= the proofs a key holds in flight: the witness sets'
       // reuse (enqueue_group) relies on it.  ZKFL_WIT_GROUP=m: m times that (a witness launch
       // serves m x as many witnesses; its kernels are latency-bound, so they take about as long)
       static const int wg = getenv("ZKFL_WIT_GROUP") ? std::max(1, atoi(getenv("ZKFL_WIT_GROUP"))) : 1;
-      pk.G = (size_t)k->max_slots * (n > 1 && key_pairs(k) ? 2 : 1) * wg;
+      pk.G = (size_t)k->max_slots * wg;
       ks.push_back(pk);
     }
     kidx[i] = c;
