@@ -52,3 +52,32 @@ def test_c_gen_mul_matches_python(cb):
     ks = b"".join(k.to_bytes(32, "little") for k in (0, 1, 5, bn.R - 1, 1 << 250, 123456789))
     assert COraclePoints().g1_gen_mul(ks) == OraclePoints().g1_gen_mul(ks)
     assert COraclePoints().g2_gen_mul(ks) == OraclePoints().g2_gen_mul(ks)
+
+
+def test_cpu_baseline_threads_and_report(cb, monkeypatch, tmp_path):
+    """bench.py's cpu_baseline leg: every core the job may use (the allowed CPUs, capped by the
+    cgroup quota -- the GPU boxes allow 256 CPUs at a 16-core quota), no fixed cap; the report
+    carries the host's core counts and the half-threads scaling point."""
+    import builtins
+    real_open = builtins.open
+
+    def fake_open(path, *a, **k):
+        if path == "/sys/fs/cgroup/cpu.max":
+            return real_open(tmp_path / "cpu.max", *a, **k)
+        return real_open(path, *a, **k)
+    monkeypatch.setattr(builtins, "open", fake_open)
+    allowed = len(os.sched_getaffinity(0))
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert cb._cgroup_quota_cores() is None and cb.default_threads() == allowed
+    (tmp_path / "cpu.max").write_text("200000 100000\n")
+    assert cb._cgroup_quota_cores() == 2 and cb.default_threads() == min(2, allowed)
+    from zkfl import circuits, zkey
+    from oracle_backend import OraclePoints
+    b = circuits.build("poseidon_hash2")
+    w = ow.evaluate(b, {"left": 3, "right": 4})
+    zk = zkey.groth16_setup(b, OraclePoints(), zkey.Toxic(tau=99, alpha=2, beta=3, gamma=4, delta=5))
+    rep, proof = cb.time_prove(zk, zkey.wtns_bytes(w), seconds_budget=0.5)
+    assert rep["cores"] == min(2, allowed) and rep["host"]["cgroup_quota_cores"] == 2
+    assert rep["host"]["allowed_cpus"] == allowed and len(proof) == 256
+    if rep["cores"] >= 2:
+        assert rep["scaling"]["threads"] == [1, 2]
