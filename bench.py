@@ -68,6 +68,10 @@ PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 # accumulation under load (GRBM_GUI_ACTIVE / 8 / duration) prices the VALU ceiling at the clock the
 # chip actually holds (DVFS), beside the 2.4 GHz figure
 SQ_COUNTERS = os.path.join(ROOT, "profiles", "sq_counters.json")
+# the same two summaries for the 2^19-domain leg's key (tools/profile_round.sh: pmc_attrib.sh .. M19,
+# SQ_CIRCUIT=M19 sq_r03.sh), so that leg's roofline carries its own traffic and clock
+PMC_TRAFFIC_M19 = os.path.join(ROOT, "profiles", "pmc_traffic_m19.json")
+SQ_COUNTERS_M19 = os.path.join(ROOT, "profiles", "sq_counters_m19.json")
 PROFILED = ("msm_accumulate_g1", "msm_accumulate_g2", "ntt", "abc", "assemble", "prove")
 
 CIRCUITS = {
@@ -295,36 +299,38 @@ def roofline_pass(key, ctx, ws, slots, n=6, reps=3):
     return best, n
 
 
-def _pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/rocpd_summary.py pmc),
-    used only when that summary was collected on a library built from the same sources as the one
-    loaded now (its build_id == zkfl_build_id()).  -> (bytes or None, provenance note)"""
+def _pmc_traffic(kernel, path=PMC_TRAFFIC):
+    """HBM bytes per launch of `kernel` from a committed PMC summary (tools/pmc_attrib.py), used
+    only when that summary was collected on a library built from the same sources as the one loaded
+    now (its build_id == zkfl_build_id()).  -> (bytes or None, provenance note)"""
     from zkfl import native
+    rel = os.path.relpath(path, ROOT)
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, "no PMC summary (profiles/pmc_traffic.json)"
+        return None, f"no PMC summary ({rel})"
     if d.get("build_id") != native.build_id():
         return None, f"PMC summary is of build {d.get('build_id')}, not the loaded {native.build_id()}"
     for name, v in d.get("kernels", {}).items():
         if KERNEL_SYMBOL[kernel] in name:
-            return v["traffic"], f"profiles/pmc_traffic.json, build {d['build_id']}"
+            return v["traffic"], f"{rel}, build {d['build_id']}"
     return None, "kernel absent from the PMC summary"
 
 
-def _measured_clock(kernel):
-    """(GHz, provenance) of `kernel`'s effective clock from the committed SQ/GRBM counter summary."""
+def _measured_clock(kernel, path=SQ_COUNTERS):
+    """(GHz, provenance) of `kernel`'s effective clock from a committed SQ/GRBM counter summary."""
     from zkfl import native
+    rel = os.path.relpath(path, ROOT)
     try:
-        with open(SQ_COUNTERS) as f:
+        with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, "no counter summary (profiles/sq_counters.json)"
+        return None, f"no counter summary ({rel})"
     for name, v in d.get("kernels", {}).items():
         if KERNEL_SYMBOL[kernel].replace("zkfl::", "") in name.replace("zkfl::", "") and v.get("clock_GHz"):
             same = d.get("build_id") == native.build_id()
-            return v["clock_GHz"], (f"profiles/sq_counters.json ({'this build' if same else 'build ' + str(d.get('build_id'))}"
+            return v["clock_GHz"], (f"{rel} ({'this build' if same else 'build ' + str(d.get('build_id'))}"
                                     f", single-slot PMC run: GRBM_GUI_ACTIVE / 8 / kernel duration)")
     return None, "kernel absent from the counter summary"
 
@@ -343,8 +349,9 @@ def stage_times(prof, nprof):
     return out
 
 
-def roofline(prof, key, traffic=True, nprof=1):
-    """The dominant kernel's roofline."""
+def roofline(prof, key, traffic=True, nprof=1, pmc_path=PMC_TRAFFIC, sq_path=SQ_COUNTERS):
+    """The dominant kernel's roofline; pmc_path / sq_path: the counter summaries of
+    this key's one-slot runs (the metric key's by default)."""
     cand = {k: v for k, v in prof.items() if k in IMPL_BYTES_PER_ENTRY and v[1] > 0}
     if not cand:
         return None
@@ -365,10 +372,10 @@ def roofline(prof, key, traffic=True, nprof=1):
     entries = units / launches
     impl = entries * IMPL_BYTES_PER_ENTRY[dom]
     collect = traffic
-    traffic, traffic_src = _pmc_traffic(dom) if collect else (None, "not collected for this leg")
+    traffic, traffic_src = _pmc_traffic(dom, pmc_path) if collect else (None, "not collected for this leg")
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     fq = entries * FQMUL_PER_ENTRY[dom] / avg_s / 1e9 if avg_s > 0 else 0.0
-    clk, clk_src = _measured_clock(dom) if collect else (None, "not collected for this leg")
+    clk, clk_src = _measured_clock(dom, sq_path) if collect else (None, "not collected for this leg")
     peak_clk = FQMUL_PEAK_GPS * clk / 2.4 if clk else None
     # "bound" stays the roofline of record (north_star: HBM bandwidth fraction); "binding" names the
     # one that limits this kernel: the integer VALU issue rate (the "valu" object below)
@@ -514,8 +521,9 @@ def extra_circuit_leg(ctx, rank, world, circuit, steps, slots, dist):
            "workload": f"groth16 prove, {name}{params} (BATCH,DIM,DEPTH,PRECISION)",
            "constraints": b.n_constraints, "domain": key.domain_size, "ms_per_step": round(elapsed / steps * 1e3, 3),
            "stage_ms_isolated_per_proof": stage_times(prof, nprof),
-           "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key, traffic=False,
-                                   nprof=nprof)}
+           "roofline_g1": roofline({k: v for k, v in prof.items() if k == "msm_accumulate_g1"}, key,
+                                   traffic=circuit == "M19", nprof=nprof, pmc_path=PMC_TRAFFIC_M19,
+                                   sq_path=SQ_COUNTERS_M19)}
     key.close()
     return rep
 

@@ -45,15 +45,17 @@ def main():
     ap.add_argument("--c5-first", action="store_true", help="run bench.py's config-5 leg first (as bench.py does)")
     ap.add_argument("--threads", action="store_true",
                     help="also print each thread's host CPU over the timed batch (/proc/self/task)")
+    ap.add_argument("--circuit", default="M", help="bench.py circuit name (M: the metric, M19: the 2^19 leg)")
     args = ap.parse_args()
     from zkfl import circuits, clients, native, wprog, zkey
-    b = circuits.build("sgd_verified", 128, 4, 7, 1000)
-    objs = [clients.Client(c + 1, 128, 4, 7, clients.JsLcg(12345 + c)).training_input(128, 1000, 100000000)[0]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    name, (bt, dim, depth, prec) = bench.CIRCUITS[args.circuit]
+    b = circuits.build(name, bt, dim, depth, prec)
+    objs = [clients.Client(c + 1, bt, dim, depth, clients.JsLcg(12345 + c)).training_input(bt, prec, 100000000)[0]
             for c in range(4)]
     ctx = native.Context(0)
     if args.c5_first:
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        import bench
         bench.c5_leg(ctx, 0, 1, 4, 8, None, 0)
     zk = zkey.groth16_setup(b, ctx, zkey.Toxic(tau=0x5EED, alpha=0xA1, beta=0xB2, gamma=0xC3, delta=0xD4))
     key = native.ProvingKey(ctx, zk)

@@ -70,7 +70,8 @@ def main():
                    "method": "rocprofv3 --pmc, three separate passes (tools/pmc_attrib.sh): L2 -> memory read "
                              "requests by size, 32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B (exact; "
                              "FETCH_SIZE counts a 128-B request as 64 B on gfx950), writes 32 x (WRREQ - "
-                             "WRREQ_64B) + 64 x WRREQ_64B; one-slot run of the metric circuit",
+                             "WRREQ_64B) + 64 x WRREQ_64B; one-slot run of circuit "
+                             + (sys.argv[2] if len(sys.argv) > 2 else "M"),
                    "kernels": kernels}, f, indent=1)
 
 

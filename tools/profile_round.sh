@@ -18,4 +18,10 @@ cp "$OUT/pmc/pmc_traffic.json" "$OUT/pmc_traffic.json"
 bash "$R/tools/sq_r03.sh" > "$OUT/sq.log" 2>&1
 cp "$R/gpurun_out/sq3/sq_r03.json" "$OUT/sq_counters.json"
 cp "$R/gpurun_out/sq3/sq_r03.txt" "$OUT/sq_counters.txt"
+# the 2^19-domain leg's key (bench.py extra_circuit): its own traffic and clock summaries
+bash "$R/tools/pmc_attrib.sh" "$OUT/pmc_m19" M19 > "$OUT/pmc_m19.log" 2>&1
+cp "$OUT/pmc_m19/pmc_traffic.json" "$OUT/pmc_traffic_m19.json"
+SQ_CIRCUIT=M19 bash "$R/tools/sq_r03.sh" > "$OUT/sq_m19.log" 2>&1
+cp "$R/gpurun_out/sq3_M19/sq_r03.json" "$OUT/sq_counters_m19.json"
+cp "$R/gpurun_out/sq3_M19/sq_r03.txt" "$OUT/sq_counters_m19.txt"
 echo "profiles written to $OUT"

@@ -7,11 +7,13 @@
 # Output: gpurun_out/sq3/sq_r03.txt (+ the raw per-kernel averages as JSON).  Run on the GPU box.
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$R/gpurun_out/sq3
+# SQ_CIRCUIT=M19: the 2^19 leg's key instead of the metric key (output gpurun_out/sq3_M19)
+CIRC=${SQ_CIRCUIT:-M}
+OUT=$R/gpurun_out/sq3$([ "$CIRC" = M ] || echo "_$CIRC")
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
-BENCH="$R/bench.py --steps 3 --warmup 1 --slots 1 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --c5-weak-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 --cli-runs 0"
+BENCH="$R/bench.py --circuit $CIRC --steps 3 --warmup 1 --slots 1 --no-cpu-baseline --e2e-steps 0 --c5-rounds 0 --c5-weak-rounds 0 --merkle-log2n 0 --extra-circuit none --split-proofs 0 --cli-runs 0"
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/sq" -o run -- python3 $BENCH > "$OUT/sq.log" 2>&1
 MIX=""
 n=0

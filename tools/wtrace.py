@@ -45,7 +45,7 @@ SYMBOL = {"acc": "k_msm_accumulate", "stitch": "k_msm_stitch", "wsum0": "k_msm_w
 
 def kind_name(k):
     base = KINDS.get(k & 31, f"k{k & 31}")
-    return base + ("_g2" if k & 32 else "")
+    return base + ("_g2" if k & 32 else "") + ("_joint" if k & 64 else "")
 
 
 def vgpr_share(lib_path):

@@ -780,12 +780,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
 // between levels (the items pass through global memory inside one CU) until one lane holds every
 // item -- one launch instead of ~4 dependent ones per tail batch.
 constexpr int MSM_STITCH_LAST = 128;
-template <class F, int MINW, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__(MSM_STITCH_LAST * MsmIO<F>::LANES) k_msm_stitch_last(const MsmTailArgs<S> ta,
-                                                                                       int level, int src) {
-  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
-  ZK_LIGHT();
-  const int y = blockIdx.y;
+// MSM y's last stitching levels on this workgroup (k_msm_stitch_last, k_msm_stitch_last_joint)
+template <class F, class S>
+ZK_DEV void msm_stitch_last_block(const MsmTailArgs<S>& ta, int y, int level, int src) {
   const uint32_t g = threadIdx.x / MsmIO<F>::LANES;
   const uint32_t nnz = *ta.nnz[y];
   for (; level < MSM_LIVE_LEVELS; level++, src ^= 1) {
@@ -795,6 +792,13 @@ __global__ void __launch_bounds__(MSM_STITCH_LAST * MsmIO<F>::LANES) k_msm_stitc
     __syncthreads();
     if (N <= (uint32_t)MSM_SG) break;
   }
+}
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(MSM_STITCH_LAST * MsmIO<F>::LANES) k_msm_stitch_last(const MsmTailArgs<S> ta,
+                                                                                       int level, int src) {
+  ZK_WT(WT_STITCH | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
+  msm_stitch_last_block<F>(ta, blockIdx.y, level, src);
 }
 
 // Weighted bucket reduction sum_b (b+1) S_b.  An item i stands for a group of g = 2^log2g
@@ -833,16 +837,15 @@ template <int Q0, int C>
 constexpr bool msm_wsum_fits() {
   return Q0 >= 1 && msm_nb_of(C) % (MSM_RB * Q0) == 0 && msm_wsum_rb<false, Q0, C>() <= 2 * MSM_RB;
 }
-template <class F, int MINW, bool L0, int Q0, int C, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__((msm_wsum_rb<L0, Q0, C>() * MsmIO<F>::LANES)) __attribute__((amdgpu_waves_per_eu(MINW)))
-k_msm_wsum(const MsmTailArgs<S> ta) {
+// One reduction block: MSM yb's reduction block bx at this level, this thread's logical lane t
+// (< RB), the block's LDS arrays sh / shy (RB points each); store = false runs the block (its
+// barriers) without writing a result (the idle half of a joint G1 block, k_msm_wsum_joint).
+template <class F, bool L0, int Q0, int C, class S = typename MsmIO<F>::S>
+ZK_DEV void msm_wsum_block(const MsmTailArgs<S>& ta, int yb, int bx, int t, XYZZ<S>* sh, XYZZ<S>* shy, bool store) {
   static_assert(msm_wsum_fits<Q0, C>(), "two reduction levels cover the buckets; red_a / red_s hold 2 x the level-1 block");
   constexpr int NB = msm_nb_of(C);
-  ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
-  ZK_LIGHT();
   // One kernel per level (template L0): level 0 keeps only the running sums R, W live through its
   // fold, level 1 has no fold at all, so neither carries the other's registers.
-  const int yb = blockIdx.y;
   const XYZZ<S>* __restrict__ in_a = L0 ? ta.buckets[yb] : ta.red_a[yb];
   const XYZZ<S>* __restrict__ in_s = L0 ? ta.buckets[yb] : ta.red_s[yb];
   constexpr int B0 = NB / (MSM_RB * Q0);  // level-0 blocks = level-1 items
@@ -852,9 +855,7 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
   XYZZ<S>* __restrict__ out_a = L0 ? ta.red_a[yb] : ta.out[yb];
   XYZZ<S>* __restrict__ out_s = L0 ? ta.red_s[yb] : ta.red_s[yb] + RB;
   using IO = MsmIO<F>;
-  __shared__ XYZZ<S> sh[RB], shy[RB];
-  const int t = threadIdx.x / IO::LANES;
-  const int i0 = (blockIdx.x * RB + t) * Q;  // this lane's items [i0, i0 + Q)
+  const int i0 = (bx * RB + t) * Q;  // this lane's items [i0, i0 + Q)
   XYZZ<F> R = xyzz_inf<F>(), y = xyzz_inf<F>();
   if constexpr (L0) {  // serial fold over Q buckets (a = s: the buckets themselves, g = 1)
     XYZZ<F> W = xyzz_inf<F>();
@@ -893,15 +894,98 @@ k_msm_wsum(const MsmTailArgs<S> ta) {
     __syncthreads();
   }
   XYZZ<F> x;
-  if (t == 0) {
+  if (t == 0 && store) {
     x = IO::ld(sh, 0);
     y = IO::ld(shy, 0);
     constexpr int lq = __builtin_ctz((unsigned)Q);
     for (int k = 0; k < log2g + lq; k++) x = xyzz_dbl<F>(x);
     const XYZZ<F> a = xyzz_add<F>(y, x);
     // canonical (and, for FqOps29, back in the 2^256 domain) only when it leaves the MSM
-    IO::st(out_a, blockIdx.x, L0 ? a : xyzz_canon<F>(a));
-    IO::st(out_s, blockIdx.x, R);
+    IO::st(out_a, bx, L0 ? a : xyzz_canon<F>(a));
+    IO::st(out_s, bx, R);
+  }
+}
+
+template <class F, int MINW, bool L0, int Q0, int C, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__((msm_wsum_rb<L0, Q0, C>() * MsmIO<F>::LANES)) __attribute__((amdgpu_waves_per_eu(MINW)))
+k_msm_wsum(const MsmTailArgs<S> ta) {
+  ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  ZK_LIGHT();
+  constexpr int RB = msm_wsum_rb<L0, Q0, C>();
+  __shared__ XYZZ<S> sh[RB], shy[RB];
+  msm_wsum_block<F, L0, Q0, C>(ta, blockIdx.y, blockIdx.x, threadIdx.x / MsmIO<F>::LANES, sh, shy, true);
+}
+
+// ---------------------------------------------------------------------------
+// Joint tails: the G1 tails of a proof and its G2 tail as ONE launch sequence (blockIdx.y: the n1
+// G1 MSMs, then the G2 ones), so the latency-bound stitching levels and reduction blocks of both
+// curves run side by side instead of one chain after the other.  A joint block is 128 threads:
+// 128 G1 lanes, or 64 G2 lane pairs (the stitching); two G1 reduction blocks or one G2 block (the
+// reduction).  The kernels hold both curves' code, so they take the larger register budget of the
+// two (2 waves/SIMD, as both tails' kernels already run).
+// ---------------------------------------------------------------------------
+template <class S1, class S2>
+struct MsmJointArgs {
+  MsmTailArgs<S1> a;  // G1 tails (blockIdx.y < n1)
+  MsmTailArgs<S2> b;  // G2 tails (blockIdx.y - n1)
+  int n1;
+};
+constexpr int MSM_JOINT_T = 128;
+
+template <class F1, class F2, int MINW, class S1 = typename MsmIO<F1>::S, class S2 = typename MsmIO<F2>::S>
+__global__ void __launch_bounds__(MSM_JOINT_T) __attribute__((amdgpu_waves_per_eu(MINW)))
+k_msm_stitch_joint(const MsmJointArgs<S1, S2> ja, int level, int src) {
+  ZK_WT(WT_STITCH | WT_JOINT);
+  ZK_LIGHT();
+  const int y = blockIdx.y;
+  if (y < ja.n1) {
+    if (ja.a.live[y][level - 1] == 0u) return;
+    const uint32_t g = (blockIdx.x * MSM_JOINT_T + threadIdx.x) / MsmIO<F1>::LANES;
+    const uint32_t N = msm_items_at<S1>(*ja.a.nnz[y], level, ja.a.target[y]);
+    if (g * MSM_SG < N) msm_stitch_lane<F1>(ja.a, y, level, src, g, N);
+  } else {
+    const int z = y - ja.n1;
+    if (ja.b.live[z][level - 1] == 0u) return;
+    const uint32_t g = (blockIdx.x * MSM_JOINT_T + threadIdx.x) / MsmIO<F2>::LANES;
+    const uint32_t N = msm_items_at<S2>(*ja.b.nnz[z], level, ja.b.target[z]);
+    if (g * MSM_SG < N) msm_stitch_lane<F2>(ja.b, z, level, src, g, N);
+  }
+}
+
+template <class F1, class F2, int MINW, class S1 = typename MsmIO<F1>::S, class S2 = typename MsmIO<F2>::S>
+__global__ void __launch_bounds__(2 * MSM_STITCH_LAST) k_msm_stitch_last_joint(const MsmJointArgs<S1, S2> ja, int level,
+                                                                                int src) {
+  static_assert(MsmIO<F1>::LANES == 1 && MsmIO<F2>::LANES == 2, "joint tails: G1 lanes, G2 lane pairs");
+  ZK_WT(WT_STITCH | WT_JOINT);
+  ZK_LIGHT();
+  const int y = blockIdx.y;
+  if (y < ja.n1)
+    msm_stitch_last_block<F1>(ja.a, y, level, src);  // threads >= MSM_STITCH_LAST have no lane
+  else
+    msm_stitch_last_block<F2>(ja.b, y - ja.n1, level, src);
+}
+
+// One reduction level of every tail: a G1 joint block runs two G1 reduction blocks (its two 64-
+// or 128-lane halves), a G2 joint block one G2 block on lane pairs
+template <class F1, class F2, int MINW, bool L0, int Q0, int C, class S1 = typename MsmIO<F1>::S,
+          class S2 = typename MsmIO<F2>::S>
+__global__ void __launch_bounds__((2 * msm_wsum_rb<L0, Q0, C>())) __attribute__((amdgpu_waves_per_eu(MINW)))
+k_msm_wsum_joint(const MsmJointArgs<S1, S2> ja) {
+  ZK_WT((L0 ? WT_WSUM0 : WT_WSUM1) | WT_JOINT);
+  ZK_LIGHT();
+  constexpr int RB = msm_wsum_rb<L0, Q0, C>();
+  constexpr int NBLK = L0 ? msm_nb_of(C) / (MSM_RB * Q0) : 1;  // reduction blocks per MSM at this level
+  constexpr size_t B1 = 2 * 2 * RB * sizeof(XYZZ<S1>), B2 = 2 * RB * sizeof(XYZZ<S2>);
+  __shared__ __attribute__((aligned(16))) unsigned char lds[B1 > B2 ? B1 : B2];
+  const int y = blockIdx.y;
+  if (y < ja.n1) {
+    if (2 * (int)blockIdx.x >= NBLK) return;  // the G1 blocks fit the first half of the grid
+    const int half = threadIdx.x / RB, bx = 2 * blockIdx.x + half;
+    XYZZ<S1>* sh = reinterpret_cast<XYZZ<S1>*>(lds) + half * 2 * RB;
+    msm_wsum_block<F1, L0, Q0, C>(ja.a, y, bx, threadIdx.x % RB, sh, sh + RB, bx < NBLK);
+  } else {
+    XYZZ<S2>* sh = reinterpret_cast<XYZZ<S2>*>(lds);
+    msm_wsum_block<F2, L0, Q0, C>(ja.b, y - ja.n1, blockIdx.x, threadIdx.x / MsmIO<F2>::LANES, sh, sh + RB, true);
   }
 }
 
@@ -923,7 +1007,6 @@ hipError_t msm_bases_alloc(MsmBases<F>& b, size_t n, int c) {
   if (c != MSM_C && c != MSM_C_SMALL) return hipErrorInvalidValue;
   b.n = n;
   b.c = c;
-  using IO = MsmIO<typename MsmCompute<F>::type>;
   ZK_CHECK(hipMalloc(&b.bases_w, (n ? n : 1) * msm_w_of(c) * sizeof(Affine<F>)));
   return hipSuccess;
 }
@@ -1220,6 +1303,64 @@ template <class F>
 hipError_t msm_tails(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast = false) {
   ZK_CHECK(msm_stitch(t, n, st));
   return msm_wsum(msm_tail_args<F>(t, outs, n), n, st, fast);
+}
+
+// The G1 tails t1[0..n1) and G2 tails t2[0..n2) of one proof as one launch sequence (the joint
+// kernels above): stitching levels until every tail is down to one workgroup, the last levels of
+// all of them in one launch, then the two reduction levels -> o1[i], o2[i].  Same results as
+// msm_tails on each curve; one window width for all.
+template <class S1, class S2>
+hipError_t msm_tails_joint(MsmTail<S1>* const* t1, XYZZ<S1>* const* o1, int n1, MsmTail<S2>* const* t2,
+                           XYZZ<S2>* const* o2, int n2, hipStream_t st, bool fast) {
+  if (n1 < 1 || n1 > MSM_TAIL_MAX || n2 < 1 || n2 > MSM_TAIL_MAX || !msm_tails_one_c(t1, n1) ||
+      !msm_tails_one_c(t2, n2) || t1[0]->c != t2[0]->c)
+    return hipErrorInvalidValue;
+  using F1 = typename MsmCompute<S1>::type;
+  using F2 = typename MsmCompute<S2>::type;
+  static_assert(msm_wsum_q0<S1>() == msm_wsum_q0<S2>(), "joint reduction: one fold per curve");
+  constexpr int W = MSM_G1_TAIL_WAVES < MSM_G2_TAIL_WAVES ? MSM_G1_TAIL_WAVES : MSM_G2_TAIL_WAVES;
+  constexpr int L1 = MsmIO<F1>::LANES, L2 = MsmIO<F2>::LANES;
+  static_assert(L1 == 1 && L2 == 2, "joint tails: G1 lanes, G2 lane pairs");
+  MsmJointArgs<S1, S2> ja;
+  ja.a = msm_tail_args<S1>(t1, o1, n1);
+  ja.b = msm_tail_args<S2>(t2, o2, n2);
+  ja.n1 = n1;
+  const int ny = n1 + n2;
+  size_t N1 = 2, N2 = 2;  // host-side upper bounds of the items per level (the kernels use each nnz)
+  for (int i = 0; i < n1; i++) N1 = std::max(N1, t1[i]->item_cap[0]);
+  for (int i = 0; i < n2; i++) N2 = std::max(N2, t2[i]->item_cap[0]);
+  int cur = 0;
+  for (int level = 1; !(ZK_KNOCKOUT & 8); level++) {
+    if (level >= MSM_LIVE_LEVELS) return hipErrorInvalidValue;
+    const size_t lanes1 = (N1 + MSM_SG - 1) / MSM_SG, lanes2 = (N2 + MSM_SG - 1) / MSM_SG;
+    if (lanes1 <= (size_t)MSM_STITCH_LAST && lanes2 <= (size_t)MSM_STITCH_LAST) {
+      hipLaunchKernelGGL((k_msm_stitch_last_joint<F1, F2, W>), dim3(1, ny), dim3(2 * MSM_STITCH_LAST), 0, st, ja,
+                         level, cur);
+      break;
+    }
+    const size_t bx = std::max(zk_grid(lanes1 * L1, MSM_JOINT_T), zk_grid(lanes2 * L2, MSM_JOINT_T));
+    hipLaunchKernelGGL((k_msm_stitch_joint<F1, F2, W>), dim3((uint32_t)bx, ny), dim3(MSM_JOINT_T), 0, st, ja, level, cur);
+    if (N1 > (size_t)MSM_SG) N1 = 2 * lanes1;
+    if (N2 > (size_t)MSM_SG) N2 = 2 * lanes2;
+    cur ^= 1;
+  }
+  if (ZK_KNOCKOUT & 16) return hipGetLastError();
+  return msm_with_c(t1[0]->c, [&](auto cc) {
+    constexpr int C = decltype(cc)::value, NB = msm_nb_of(C);
+    constexpr int Q0 = msm_wsum_q0<S1>(), QF = msm_wsum_q_fast<C>();
+    if (fast) {
+      hipLaunchKernelGGL((k_msm_wsum_joint<F1, F2, W, true, QF, C>), dim3(NB / (MSM_RB * QF), ny),
+                         dim3(2 * msm_wsum_rb<true, QF, C>()), 0, st, ja);
+      hipLaunchKernelGGL((k_msm_wsum_joint<F1, F2, W, false, QF, C>), dim3(1, ny), dim3(2 * msm_wsum_rb<false, QF, C>()),
+                         0, st, ja);
+    } else {
+      hipLaunchKernelGGL((k_msm_wsum_joint<F1, F2, W, true, Q0, C>), dim3(NB / (MSM_RB * Q0), ny),
+                         dim3(2 * msm_wsum_rb<true, Q0, C>()), 0, st, ja);
+      hipLaunchKernelGGL((k_msm_wsum_joint<F1, F2, W, false, Q0, C>), dim3(1, ny), dim3(2 * msm_wsum_rb<false, Q0, C>()),
+                         0, st, ja);
+    }
+    return hipGetLastError();
+  });
 }
 
 template <class F>

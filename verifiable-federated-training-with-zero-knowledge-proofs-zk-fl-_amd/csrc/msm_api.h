@@ -209,4 +209,9 @@ constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket 
 ZKFL_MSM_DECLARE(g1, FqOps)
 ZKFL_MSM_DECLARE(g2, Fq2Ops)
 
+// The G1 tails and the G2 tail of one proof as ONE launch sequence (msm_joint.hip): stitching and
+// reduction of both curves side by side, blockIdx.y over all n1 + n2 MSMs
+hipError_t msm_tails_joint(MsmTail<FqOps>* const* t1, XYZZ<FqOps>* const* o1, int n1, MsmTail<Fq2Ops>* const* t2,
+                           XYZZ<Fq2Ops>* const* o2, int n2, hipStream_t st, bool fast);
+
 }  // namespace zkfl

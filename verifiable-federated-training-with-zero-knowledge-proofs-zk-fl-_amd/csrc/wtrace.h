@@ -28,11 +28,11 @@ struct WtBuf {
   uint32_t cap = 0;
 };
 
-// kinds (tools/wtrace.py names them); G2 variants of the MSM kernels add WT_G2
+// kinds (tools/wtrace.py names them); G2 variants of the MSM kernels add WT_G2, the joint tails WT_JOINT
 enum : uint32_t {
   WT_ACC = 1, WT_STITCH, WT_WSUM0, WT_WSUM1, WT_SORT_COUNT, WT_SORT_SCAN, WT_SORT_SCATTER, WT_SORT_BINS,
   WT_TAIL_RESET, WT_NTT_COLS_INV, WT_NTT_LDS, WT_NTT_COLS_FWD, WT_ABC, WT_ABC_ROWS, WT_JOIN, WT_ASSEMBLE,
-  WT_SET_EXTRA, WT_WITNESS, WT_G2 = 32
+  WT_SET_EXTRA, WT_WITNESS, WT_G2 = 32, WT_JOINT = 64  // joint G1 + G2 tail kernels
 };
 
 #if ZK_WTRACE
@@ -82,5 +82,6 @@ hipError_t zk_wtrace_bind_g1(const WtBuf& b);
 hipError_t zk_wtrace_bind_g2(const WtBuf& b);
 hipError_t zk_wtrace_bind_ntt(const WtBuf& b);
 hipError_t zk_wtrace_bind_wit(const WtBuf& b);
+hipError_t zk_wtrace_bind_joint(const WtBuf& b);
 
 }  // namespace zkfl

@@ -1531,6 +1531,9 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
   const bool share = k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32);
+  // the G2 tail joins the G1 tails' launches (msm_tails_joint) instead of running right after B2
+  static const bool joint_on = !getenv("ZKFL_JOINT_TAILS") || atoi(getenv("ZKFL_JOINT_TAILS")) != 0;
+  const bool joint = share && joint_on;
   if (!share) {  // G2 stream
     HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
     if (!(ZK_KNOCKOUT & 32))
@@ -1559,8 +1562,10 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
       HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
     HIP_TRY(msm_accumulate_sorted_g2(k->bB2, sB.keys_out, sB.vals_out, s->g2t, st, prof,
                                      "msm_accumulate_g2"), "msm B2");
-    HIP_TRY(msm_tails_g2(&t2, &o2, 1, st, small_key_fast_wsum(k)), "msm B2 tail");
-    if (!graph) HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
+    if (!joint) {
+      HIP_TRY(msm_tails_g2(&t2, &o2, 1, st, small_key_fast_wsum(k)), "msm B2 tail");
+      if (!graph) HIP_TRY(hipEventRecord(s->ev_b2, st), "event");
+    }
   } else {
     HIP_TRY(msm_accumulate_g1(k->bB1, sB, s->g1t[1], W, E, st, prof, "msm_accumulate_g1"), "msm B1");
   }
@@ -1584,9 +1589,15 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   {
     G1P* outs[4] = {s->res + 0, s->res + 1, s->res + 2, s->res + 3};
-    HIP_TRY(msm_tails_g1(tails, outs, ntails, st, small_key_fast_wsum(k)), "msm tails");
+    if (joint) {
+      MsmTail<Fq2Ops>* t2 = &s->g2t;
+      G2P* o2 = s->resB2;
+      HIP_TRY(msm_tails_joint(tails, outs, ntails, &t2, &o2, 1, st, small_key_fast_wsum(k)), "msm tails (G1 + G2)");
+    } else {
+      HIP_TRY(msm_tails_g1(tails, outs, ntails, st, small_key_fast_wsum(k)), "msm tails");
+    }
   }
-  if (!graph) HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
+  if (!graph && !joint) HIP_TRY(hipStreamWaitEvent(st, s->ev_b2, 0), "wait");
   if (plain == 2) {
     hipLaunchKernelGGL(k_part_out, dim3(1), dim3(64), 0, st, s->res, s->resB2, s->d_parts);
     HIP_TRY(hipMemcpyAsync(s->pinned + 512, s->d_parts, PART_WORDS * 4, hipMemcpyDeviceToHost, st), "download part");
@@ -2830,6 +2841,7 @@ int zkfl_debug_wtrace(zkfl_ctx* ctx, int op, uint32_t cap, void* out, uint32_t* 
     if (e == hipSuccess) e = zk_wtrace_bind_g2(b);
     if (e == hipSuccess) e = zk_wtrace_bind_ntt(b);
     if (e == hipSuccess) e = zk_wtrace_bind_wit(b);
+    if (e == hipSuccess) e = zk_wtrace_bind_joint(b);
     return e;
   };
   HIP_TRY(hipDeviceSynchronize(), "wave trace: sync");
