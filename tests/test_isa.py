@@ -52,8 +52,10 @@ def test_checker_finds_a_dropped_wait(acc):
 
 
 def test_accumulation_kernels_do_not_spill(acc):
+    """G1 and G2, each as the one-MSM kernel and the multi-MSM one (small keys' A, B1, C + H in one
+    launch, k_msm_accumulate_multi: the same body, msm_acc_chunk)."""
     res = isa_check.resources(SO, r"k_msm_accumulate")
-    assert len(res) == 2
+    assert len(res) == 4 and sum("_multi" in n for n in res) == 2, list(res)
     for name, r in res.items():
         assert r.get("vgpr_spill_count", 0) == 0 and r.get("private_segment_fixed_size", 0) == 0, (name, r)
         assert r["group_segment_fixed_size"] == 8192, (name, r)  # two 4 KB LDS-DMA buffers per wave

@@ -387,22 +387,43 @@ ZK_DEV void msm_for_digits(const uint32_t* __restrict__ scalars, const uint32_t*
   }
 }
 
+// One sort of a launch (blockIdx.y): its scalars and base map, its blocking (per_blk bases per
+// count / scatter block, nblk blocks) and its scratch.  Every sort launch takes a table of up to
+// MSM_TAIL_MAX of them, so independent MSMs of a proof sort in the same four launches.
+struct MsmSortJob {
+  const uint32_t* scalars;
+  const uint32_t* extra;
+  const uint32_t* sidx;
+  uint32_t extra_start;
+  uint32_t n, per_blk, nblk;
+  uint32_t* cnt;        // [HB][nblk] counts, then exclusive offsets
+  uint32_t* bin_start;  // [HB + 1]
+  uint32_t* nnz;
+  uint16_t* keys_in;
+  uint32_t* vals_in;
+  uint16_t* keys_out;
+  uint32_t* vals_out;
+};
+struct MsmSortArgs {
+  MsmSortJob j[MSM_TAIL_MAX];
+};
+
 template <int C>
-__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint32_t* __restrict__ scalars,
-                                                            const uint32_t* __restrict__ extra,
-                                                            const uint32_t* __restrict__ sidx, uint32_t extra_start,
-                                                            size_t n, size_t per_blk, uint32_t* __restrict__ cnt) {
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const MsmSortArgs A) {
   ZK_WT(WT_SORT_COUNT);
   ZK_LIGHT();
   constexpr int LB = msm_sort_lb<C>();
+  const MsmSortJob& J = A.j[blockIdx.y];
+  if (blockIdx.x >= J.nblk) return;
   __shared__ uint32_t h[MSM_SORT_HB];
   if (threadIdx.x < MSM_SORT_HB) h[threadIdx.x] = 0;
   __syncthreads();
-  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  const size_t i0 = (size_t)blockIdx.x * J.per_blk, i1 = i0 + J.per_blk < J.n ? i0 + J.per_blk : J.n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<C>(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
+    msm_for_digits<C>(J.scalars, J.extra, J.sidx, J.extra_start, i,
+                      [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> LB], 1u); });
   __syncthreads();
-  if (threadIdx.x < MSM_SORT_HB) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < MSM_SORT_HB) J.cnt[(size_t)threadIdx.x * J.nblk + blockIdx.x] = h[threadIdx.x];
 }
 
 // cnt[HB * nblk] (bin-major) -> exclusive offsets in place; bin_start[HB + 1]; *nnz.
@@ -410,11 +431,13 @@ __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_count(const uint32_t* __
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "the bucket sort's scan needs gfx950's 160 KB of LDS"
 #endif
-static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* __restrict__ cnt, uint32_t nblk,
-                                                                   uint32_t* __restrict__ bin_start,
-                                                                   uint32_t* __restrict__ nnz) {
+static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(const MsmSortArgs A) {
   ZK_WT(WT_SORT_SCAN);
   ZK_LIGHT();
+  const MsmSortJob& J = A.j[blockIdx.y];
+  uint32_t* __restrict__ cnt = J.cnt;
+  uint32_t* __restrict__ bin_start = J.bin_start;
+  const uint32_t nblk = J.nblk;
   __shared__ uint32_t c[MSM_SORT_HB * MSM_SORT_MAXBLK + MSM_SORT_BT];  // +1 word per 32: no bank conflicts
   __shared__ uint32_t part[MSM_SORT_BT];
   const uint32_t total = MSM_SORT_HB * nblk, t = threadIdx.x;
@@ -450,26 +473,25 @@ static __global__ void __launch_bounds__(MSM_SORT_BT) k_msm_bin_scan(uint32_t* _
   }
   if (t == MSM_SORT_BT - 1) {
     bin_start[MSM_SORT_HB] = part[t];
-    *nnz = part[t];
+    *J.nnz = part[t];
   }
 }
 
 template <int C>
-__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const uint32_t* __restrict__ scalars,
-                                                              const uint32_t* __restrict__ extra,
-                                                              const uint32_t* __restrict__ sidx, uint32_t extra_start,
-                                                              size_t n, size_t per_blk,
-                                                              const uint32_t* __restrict__ cnt,
-                                                              uint16_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+__global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const MsmSortArgs A) {
   ZK_WT(WT_SORT_SCATTER);
   ZK_LIGHT();
   constexpr int LB = msm_sort_lb<C>();
+  const MsmSortJob& J = A.j[blockIdx.y];
+  if (blockIdx.x >= J.nblk) return;
   __shared__ uint32_t cur[MSM_SORT_HB];
-  if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x];
+  if (threadIdx.x < MSM_SORT_HB) cur[threadIdx.x] = J.cnt[(size_t)threadIdx.x * J.nblk + blockIdx.x];
   __syncthreads();
-  const size_t i0 = (size_t)blockIdx.x * per_blk, i1 = i0 + per_blk < n ? i0 + per_blk : n;
+  uint16_t* __restrict__ keys = J.keys_in;
+  uint32_t* __restrict__ vals = J.vals_in;
+  const size_t i0 = (size_t)blockIdx.x * J.per_blk, i1 = i0 + J.per_blk < J.n ? i0 + J.per_blk : J.n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += MSM_SORT_T)
-    msm_for_digits<C>(scalars, extra, sidx, extra_start, i, [&](uint32_t key, uint32_t val) {
+    msm_for_digits<C>(J.scalars, J.extra, J.sidx, J.extra_start, i, [&](uint32_t key, uint32_t val) {
       const uint32_t p = atomicAdd(&cur[key >> LB], 1u);
       keys[p] = (uint16_t)key;
       vals[p] = val;
@@ -480,14 +502,16 @@ __global__ void __launch_bounds__(MSM_SORT_T) k_msm_bin_scatter(const uint32_t* 
 // BINT threads per workgroup (MSM_SORT_BINT).  A 256-thread variant for small MSMs measured
 // neutral on config 5 (1906.7 vs 1894.0 proofs/s, 3 alternations, profiles/r04_ab_c5_small_keys.log).
 template <int BINT, int NL>
-__global__ void __launch_bounds__(BINT) k_msm_bin_sort(const uint32_t* __restrict__ bin_start,
-                                                      const uint16_t* __restrict__ tk,
-                                                      const uint32_t* __restrict__ tv,
-                                                      uint16_t* __restrict__ ko,
-                                                      uint32_t* __restrict__ vo) {
+__global__ void __launch_bounds__(BINT) k_msm_bin_sort(const MsmSortArgs A) {
   static_assert(BINT >= NL && BINT <= 1024 && NL >= 64, "bins: one thread per low counter");
   ZK_WT(WT_SORT_BINS);
   ZK_LIGHT();
+  const MsmSortJob& J = A.j[blockIdx.y];
+  const uint32_t* __restrict__ bin_start = J.bin_start;
+  const uint16_t* __restrict__ tk = J.keys_in;
+  const uint32_t* __restrict__ tv = J.vals_in;
+  uint16_t* __restrict__ ko = J.keys_out;
+  uint32_t* __restrict__ vo = J.vals_out;
   __shared__ uint32_t c[NL];
   const uint32_t b0 = bin_start[blockIdx.x], b1 = bin_start[blockIdx.x + 1], t = threadIdx.x;
   if (b0 == b1) return;
@@ -579,15 +603,14 @@ ZK_DEV void msm_mark_live(uint32_t* __restrict__ live, int level, bool open) {
 // Software-pipelined: the key/index of entry p+1 and its base are in flight while entry p is
 // added.  MINW: minimum waves per SIMD the register allocator must allow (chosen per curve,
 // DESIGN.md §5).
-template <class F, int MINW, class S = typename MsmIO<F>::S>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
-    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<S>* __restrict__ bases,
-    const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
-    XYZZ<S>* __restrict__ buckets, uint32_t target, uint32_t* __restrict__ live) {
-  ZK_WT(WT_ACC | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+// Chunk c of one MSM (the body of k_msm_accumulate and k_msm_accumulate_multi; 64-thread blocks).
+template <class F, class S = typename MsmIO<F>::S>
+ZK_DEV void msm_acc_chunk(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                          const Affine<S>* __restrict__ bases, const uint32_t* __restrict__ nnz_ptr,
+                          uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
+                          XYZZ<S>* __restrict__ buckets, uint32_t target, uint32_t* __restrict__ live, size_t c) {
   using IO = MsmIO<F>;
   constexpr bool PF = sizeof(typename S::T) == 32 ? MSM_G1_PREFETCH : MSM_G2_PREFETCH;
-  const size_t c = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / IO::LANES;
   const uint32_t nnz = *nnz_ptr;
   const uint32_t L = msm_chunk_len<S>(nnz, target);
   const size_t p0 = c * L;
@@ -672,6 +695,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW)))
   if (!slot0) item_key[2 * c] = (uint32_t)keys[p0] | MSM_ITEM_DUMMY;
   if (!slot1) item_key[2 * c + 1] = (uint32_t)keys[p1 - 1] | MSM_ITEM_DUMMY;
   msm_mark_live(live, 0, open);
+}
+
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate(
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const Affine<S>* __restrict__ bases,
+    const uint32_t* __restrict__ nnz_ptr, uint32_t* __restrict__ item_key, XYZZ<S>* __restrict__ item_val,
+    XYZZ<S>* __restrict__ buckets, uint32_t target, uint32_t* __restrict__ live) {
+  ZK_WT(WT_ACC | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u));
+  msm_acc_chunk<F>(keys, vals, bases, nnz_ptr, item_key, item_val, buckets, target, live,
+                   ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / MsmIO<F>::LANES);
+}
+
+// The accumulations of up to MSM_TAIL_MAX independent MSMs of one curve in one launch (blockIdx.y
+// = MSM): a small key's A, B1 and C + H, so the proof's chain waits for one launch, not three.
+template <class S>
+struct MsmAccArgs {
+  const uint16_t* keys[MSM_TAIL_MAX];
+  const uint32_t* vals[MSM_TAIL_MAX];
+  const Affine<S>* bases[MSM_TAIL_MAX];
+  const uint32_t* nnz[MSM_TAIL_MAX];
+  uint32_t* item_key[MSM_TAIL_MAX];
+  XYZZ<S>* item_val[MSM_TAIL_MAX];
+  XYZZ<S>* buckets[MSM_TAIL_MAX];
+  uint32_t target[MSM_TAIL_MAX];
+  uint32_t* live[MSM_TAIL_MAX];
+};
+template <class F, int MINW, class S = typename MsmIO<F>::S>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW))) k_msm_accumulate_multi(
+    const MsmAccArgs<S> A) {
+  ZK_WT(WT_ACC | (MsmIO<F>::LANES == 2 ? WT_G2 : 0u) | WT_JOINT);
+  const int y = blockIdx.y;
+  msm_acc_chunk<F>(A.keys[y], A.vals[y], A.bases[y], A.nnz[y], A.item_key[y], A.item_val[y], A.buckets[y],
+                   A.target[y], A.live[y], ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / MsmIO<F>::LANES);
 }
 
 }  // namespace zkfl
@@ -1173,38 +1229,58 @@ hipError_t msm_tails_reset(MsmTail<F>* const* t, int n, hipStream_t st) {
 }
 
 // digits (+ nnz) -> sort by bucket into pl.keys_out / pl.vals_out (the first *nnz pairs; the sort
-// writes *nnz)
+// writes *nnz), for n <= MSM_TAIL_MAX independent MSMs of one window width at once (blockIdx.y =
+// MSM): the same four launches whatever n, each MSM with its own scratch.
 template <class F>
-hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
-                    const uint32_t* d_extra, hipStream_t st) {
-  const size_t n = b.n;
-  if (n > pl.cap) return hipErrorInvalidValue;
-  if (n == 0) return hipSuccess;
-  // count / scan / scatter / bins (see k_msm_bin_count); keys_in/vals_in hold the high-bin order
-  const size_t per_blk = (n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
-                             ? (size_t)MSM_SORT_T
-                             : ((n + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
-  const uint32_t nblk = (uint32_t)((n + per_blk - 1) / per_blk);
-  if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
-  if (b.c != pl.c) return hipErrorInvalidValue;
-  uint32_t* cnt = static_cast<uint32_t*>(pl.sort_tmp);
-  uint32_t* bin_start = cnt + MSM_SORT_HB * MSM_SORT_MAXBLK;
-  return msm_with_c(b.c, [&](auto cc) {
+hipError_t msm_sort_multi(const MsmBases<F>* const* b, MsmScratch<F>* const* pl, uint32_t* const* nnz,
+                          const uint32_t* const* sc, const uint32_t* const* ex, int n, hipStream_t st) {
+  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  MsmSortArgs A = {};
+  uint32_t gx = 0;
+  int ny = 0;
+  bool sorted = true;
+  const int c = b[0]->c;
+  for (int i = 0; i < n; i++) {
+    const size_t m = b[i]->n;
+    if (m > pl[i]->cap || b[i]->c != c || pl[i]->c != c) return hipErrorInvalidValue;
+    if (m == 0) {  // nothing to sort: nnz = 0 (the tail reset left it so)
+      continue;
+    }
+    // count / scan / scatter / bins (see k_msm_bin_count); keys_in/vals_in hold the high-bin order
+    const size_t per_blk = (m + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK < MSM_SORT_T
+                               ? (size_t)MSM_SORT_T
+                               : ((m + MSM_SORT_MAXBLK - 1) / MSM_SORT_MAXBLK + MSM_SORT_T - 1) / MSM_SORT_T * MSM_SORT_T;
+    const uint32_t nblk = (uint32_t)((m + per_blk - 1) / per_blk);
+    if (nblk > MSM_SORT_MAXBLK) return hipErrorInvalidValue;
+    MsmSortJob& J = A.j[ny++];
+    J = {sc[i], ex[i], b[i]->sidx, b[i]->extra_start, (uint32_t)m, (uint32_t)per_blk, nblk,
+         static_cast<uint32_t*>(pl[i]->sort_tmp), static_cast<uint32_t*>(pl[i]->sort_tmp) + MSM_SORT_HB * MSM_SORT_MAXBLK,
+         nnz[i], pl[i]->keys_in, pl[i]->vals_in, pl[i]->keys_out, pl[i]->vals_out};
+    gx = std::max(gx, nblk);
+    sorted = sorted && pl[i]->ko_sorted;
+    pl[i]->ko_sorted = 1;
+  }
+  if (ny == 0) return hipSuccess;
+  return msm_with_c(c, [&](auto cc) {
     constexpr int C = decltype(cc)::value;
     constexpr int NL = msm_sort_nl<C>();
     static_assert(NL >= 64 && NL <= 1024 && MSM_SORT_BINT >= NL, "bins: one thread per low counter");
-    hipLaunchKernelGGL((k_msm_bin_count<C>), dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
-                       b.extra_start, n, per_blk, cnt);
-    hipLaunchKernelGGL(k_msm_bin_scan, dim3(1), dim3(MSM_SORT_BT), 0, st, cnt, nblk, bin_start, nnz);
-    if (!(ZK_KNOCKOUT & 2) || !pl.ko_sorted) {  // knock-out: an MSM's own scratch keeps its first sort
-      pl.ko_sorted = 1;
-      hipLaunchKernelGGL((k_msm_bin_scatter<C>), dim3(nblk), dim3(MSM_SORT_T), 0, st, d_scalars, d_extra, b.sidx,
-                         b.extra_start, n, per_blk, cnt, pl.keys_in, pl.vals_in);
-      hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB), dim3(MSM_SORT_BINT), 0, st,
-                         bin_start, pl.keys_in, pl.vals_in, pl.keys_out, pl.vals_out);
+    hipLaunchKernelGGL((k_msm_bin_count<C>), dim3(gx, ny), dim3(MSM_SORT_T), 0, st, A);
+    hipLaunchKernelGGL(k_msm_bin_scan, dim3(1, ny), dim3(MSM_SORT_BT), 0, st, A);
+    if (!(ZK_KNOCKOUT & 2) || !sorted) {  // knock-out: an MSM's own scratch keeps its first sort
+      hipLaunchKernelGGL((k_msm_bin_scatter<C>), dim3(gx, ny), dim3(MSM_SORT_T), 0, st, A);
+      hipLaunchKernelGGL((k_msm_bin_sort<MSM_SORT_BINT, NL>), dim3(MSM_SORT_HB, ny), dim3(MSM_SORT_BINT), 0, st, A);
     }
     return hipGetLastError();
   });
+}
+
+template <class F>
+hipError_t msm_sort(const MsmBases<F>& b, MsmScratch<F>& pl, uint32_t* nnz, const uint32_t* d_scalars,
+                    const uint32_t* d_extra, hipStream_t st) {
+  const MsmBases<F>* bp = &b;
+  MsmScratch<F>* pp = &pl;
+  return msm_sort_multi(&bp, &pp, &nnz, &d_scalars, &d_extra, 1, st);
 }
 
 // Accumulation (level 0: fixed chunks, closed runs straight into the buckets, open runs as items)
@@ -1230,6 +1306,42 @@ hipError_t msm_accumulate_sorted(const MsmBases<F>& b, const uint16_t* keys, con
     hipLaunchKernelGGL((k_msm_accumulate<FC, AW>), dim3(zk_grid(chunks * LN, 64)), dim3(64), pad_lds, st, keys, vals,
                        b.bases_w, t.nnz, t.item_key[0], t.item_val[0], t.buckets, msm_target_arg(t), t.live);
   if (prof) prof->end(pidx, st, 0.0, t.nnz);
+  return hipGetLastError();
+}
+
+// The accumulations of n <= MSM_TAIL_MAX MSMs of one curve over their sorted pairs (keys[i],
+// vals[i]) in ONE launch (k_msm_accumulate_multi); each tail must have been reset.
+template <class F>
+hipError_t msm_accumulate_sorted_multi(const MsmBases<F>* const* b, const uint16_t* const* keys,
+                                       const uint32_t* const* vals, MsmTail<F>* const* t, int n, hipStream_t st) {
+  if (n < 1 || n > MSM_TAIL_MAX) return hipErrorInvalidValue;
+  using FC = typename MsmCompute<F>::type;
+  constexpr int LN = MsmIO<FC>::LANES;
+  constexpr int AW = sizeof(typename F::T) == 32 ? MSM_G1_WAVES : MSM_G2_WAVES;
+  MsmAccArgs<F> A = {};
+  size_t gx = 0;
+  int ny = 0;
+  for (int i = 0; i < n; i++) {
+    if (b[i]->n == 0) continue;
+    if (b[i]->c != t[i]->c) return hipErrorInvalidValue;
+    const size_t m = b[i]->n * msm_w_of(b[i]->c);
+    size_t chunks = (m + t[i]->l0 - 1) / t[i]->l0;
+    if (t[i]->target) chunks = std::min<size_t>(chunks, t[i]->target);
+    if (chunks > t[i]->max_chunks) return hipErrorInvalidValue;
+    gx = std::max<size_t>(gx, zk_grid(chunks * LN, 64));
+    A.keys[ny] = keys[i];
+    A.vals[ny] = vals[i];
+    A.bases[ny] = b[i]->bases_w;
+    A.nnz[ny] = t[i]->nnz;
+    A.item_key[ny] = t[i]->item_key[0];
+    A.item_val[ny] = t[i]->item_val[0];
+    A.buckets[ny] = t[i]->buckets;
+    A.target[ny] = msm_target_arg(*t[i]);
+    A.live[ny] = t[i]->live;
+    ny++;
+  }
+  if (ny && !((ZK_KNOCKOUT & 64) && LN == 1))
+    hipLaunchKernelGGL((k_msm_accumulate_multi<FC, AW>), dim3((uint32_t)gx, ny), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 
@@ -1399,6 +1511,15 @@ hipError_t msm_run(const MsmBases<F>& b, MsmScratch<F>& pl, MsmTail<F>& t, const
   hipError_t msm_accumulate_sorted_##SUF(const MsmBases<F>& b, const uint16_t* keys, const uint32_t* vals,  \
                                          MsmTail<F>& t, hipStream_t st, Profiler* prof, const char* tag) { \
     return msm_accumulate_sorted(b, keys, vals, t, st, prof, tag);                                       \
+  }                                                                                                      \
+  hipError_t msm_sort_multi_##SUF(const MsmBases<F>* const* b, MsmScratch<F>* const* s, uint32_t* const* nnz, \
+                                  const uint32_t* const* sc, const uint32_t* const* ex, int n, hipStream_t st) { \
+    return msm_sort_multi(b, s, nnz, sc, ex, n, st);                                                     \
+  }                                                                                                      \
+  hipError_t msm_accumulate_sorted_multi_##SUF(const MsmBases<F>* const* b, const uint16_t* const* keys,      \
+                                               const uint32_t* const* vals, MsmTail<F>* const* t, int n,  \
+                                               hipStream_t st) {                                          \
+    return msm_accumulate_sorted_multi(b, keys, vals, t, n, st);                                         \
   }                                                                                                      \
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st, bool fast) { \
     return msm_tails(t, outs, n, st, fast);                                                              \

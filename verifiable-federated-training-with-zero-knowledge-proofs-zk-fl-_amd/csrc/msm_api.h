@@ -204,7 +204,14 @@ constexpr int MSM_TAIL_RED = 4 * MSM_RB;  // reduction block outputs per bucket 
   hipError_t msm_tails_##SUF(MsmTail<F>* const* t, XYZZ<F>* const* outs, int n, hipStream_t st,     \
                              bool fast = false);                                                      \
   hipError_t msm_run_##SUF(const MsmBases<F>& b, MsmScratch<F>& s, MsmTail<F>& t, const uint32_t* scalars, \
-                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag);
+                           const uint32_t* extra, XYZZ<F>* out, hipStream_t st, Profiler* prof, const char* tag); \
+  /* n <= MSM_TAIL_MAX independent MSMs of one window width: their sorts in the same four launches, */   \
+  /* their accumulations in one launch (blockIdx.y = MSM) */                                             \
+  hipError_t msm_sort_multi_##SUF(const MsmBases<F>* const* b, MsmScratch<F>* const* s, uint32_t* const* nnz, \
+                                  const uint32_t* const* sc, const uint32_t* const* ex, int n, hipStream_t st); \
+  hipError_t msm_accumulate_sorted_multi_##SUF(const MsmBases<F>* const* b, const uint16_t* const* keys,      \
+                                               const uint32_t* const* vals, MsmTail<F>* const* t, int n,  \
+                                               hipStream_t st);
 
 ZKFL_MSM_DECLARE(g1, FqOps)
 ZKFL_MSM_DECLARE(g2, Fq2Ops)

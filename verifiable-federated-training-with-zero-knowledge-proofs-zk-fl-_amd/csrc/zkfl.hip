@@ -944,6 +944,10 @@ struct zkfl_key {
   // holds no separate C and H bases (they were ~0.5 GB of expanded bases per key at 2^18)
   Fr* dbg_zero = nullptr;
   bool share_b = false;  // B1 and B2 have the same base index map: one digit sort serves both
+  // small keys (domain <= 2^16, config 5's circuits): a proof sorts A, B1 and C + H in the same four
+  // launches and accumulates them in one (msm_sort_multi / msm_accumulate_sorted_multi), after ABC /
+  // NTT; the slots hold A's and B's sort scratch for it (g1s_a, g1s_b)
+  bool front = false;
   int msm_c = MSM_C;     // window bits of every base set of the key (msm_pick_c of its largest)
   NttPlan ntt;
   std::vector<ProofSlot*> slots;
@@ -1067,6 +1071,10 @@ hipError_t slot_create(zkfl_key* k, ProofSlot** out) {
     s->nnz_alias = true;
   }
   if (graph_mode()) ZK_CHECK(hipMalloc(&s->w_stage, nV * 32));
+  if (k->front) {  // A's and B's own sort scratch (C + H sorts in g1s)
+    ZK_CHECK(msm_scratch_alloc_g1(s->g1s_a, k->bA.n, c, st));
+    ZK_CHECK(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, c, st));
+  }
   ZK_CHECK(hipMalloc(&s->h, (n + 4) * 32));   // h, then the extra slots (the merged C+H MSM's scalars)
   s->extra = s->h + n;
   ZK_CHECK(hipMalloc(&s->abc, n * 3 * 32));
@@ -1531,9 +1539,11 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   // One stream (the default): B1's digit sort also serves B2 (same scalars, same index map), so
   // B2 runs right after B1 on the main stream, before C reuses the sort scratch.
   const bool share = k->share_b && st_g2 == st && !(ZK_KNOCKOUT & 32);
-  // the G2 tail joins the G1 tails' launches (msm_tails_joint) instead of running right after B2
-  static const bool joint_on = !getenv("ZKFL_JOINT_TAILS") || atoi(getenv("ZKFL_JOINT_TAILS")) != 0;
-  const bool joint = share && joint_on;
+  // Small keys: the G2 tail joins the G1 tails' launches (msm_tails_joint) instead of running right
+  // after B2 -- config 5 2,712 vs 2,385 proofs/s (3 same-box alternations); the metric key keeps the
+  // separate tails (M 433 vs 439 and 431 vs 433 with them joint, two boxes:
+  // profiles/r06_ab_joint_tails.log, r06_ab_front.log)
+  const bool joint = share && k->front;
   if (!share) {  // G2 stream
     HIP_TRY(hipStreamWaitEvent(st_g2, s->ev_ready, 0), "wait");
     if (!(ZK_KNOCKOUT & 32))
@@ -1547,12 +1557,34 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
 #else
   MsmScratch<FqOps>&sA = s->g1s, &sB = s->g1s, &sCH = s->g1s;
 #endif
-  if (light_first) {
+  // small keys: ABC / NTT, then A, B1 and C + H sorted together and accumulated in one launch, B2
+  // from B1's pairs (their proofs are chains of latency-bound launches: fewer links, shorter chain;
+  // config 5 2,802 vs 2,748 proofs/s, 3 same-box alternations, profiles/r06_ab_front.log)
+  const bool front = joint && merge && !(ZK_KNOCKOUT & 2) && s->g1s_a.keys_out && s->g1s_b.keys_out;
+  if (front) {
+    const int rc = abc_ntt();
+    if (rc) return rc;
+    const MsmBases<FqOps>* bs[3] = {&k->bA, &k->bB1, &k->bCH};
+    MsmScratch<FqOps>* ss[3] = {&s->g1s_a, &s->g1s_b, &s->g1s};
+    uint32_t* nn[3] = {s->g1t[0].nnz, s->g1t[1].nnz, s->g1t[2].nnz};
+    const uint32_t* sc[3] = {W, W, W};
+    const uint32_t* ex[3] = {E, E, (const uint32_t*)s->h};
+    HIP_TRY(msm_sort_multi_g1(bs, ss, nn, sc, ex, 3, st), "msm A, B1, C+H sorts");
+    const uint16_t* kk[3] = {ss[0]->keys_out, ss[1]->keys_out, ss[2]->keys_out};
+    const uint32_t* vv[3] = {ss[0]->vals_out, ss[1]->vals_out, ss[2]->vals_out};
+    HIP_TRY(msm_accumulate_sorted_multi_g1(bs, kk, vv, tails, 3, st), "msm A, B1, C+H");
+    if (!s->nnz_alias)
+      HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
+    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, ss[1]->keys_out, ss[1]->vals_out, s->g2t, st, prof, "msm_accumulate_g2"),
+            "msm B2");
+  }
+  if (light_first && !front) {
     const int rc = abc_ntt();
     if (rc) return rc;
   }
-  HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
-  if (share) {
+  if (!front) HIP_TRY(msm_accumulate_g1(k->bA, sA, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
+  if (front) {
+  } else if (share) {
     MsmTail<Fq2Ops>* t2 = &s->g2t;
     G2P* o2 = s->resB2;
     HIP_TRY(msm_sort_g1(k->bB1, sB, s->g1t[1].nnz, W, E, st), "msm B1 sort");
@@ -1573,11 +1605,12 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
     HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, Z, st, prof, "msm_accumulate_g1"), "msm C");
   else if (!merge)
     HIP_TRY(msm_accumulate_g1(k->bC, s->g1s, s->g1t[2], W, E, st, prof, "msm_accumulate_g1"), "msm C");
-  if (!light_first) {
+  if (!light_first && !front) {
     const int rc = abc_ntt();
     if (rc) return rc;
   }
-  if (merge) {
+  if (front) {
+  } else if (merge) {
     HIP_TRY(msm_accumulate_g1(k->bCH, sCH, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
             "msm C+H");
   } else if (split_ch) {
@@ -2237,6 +2270,7 @@ int zkey_load_parsed(zkfl_ctx* ctx, const ZkeyHost& z, size_t len, double parse_
     // B_i(tau) G1 and B_i(tau) G2 vanish together in an honest zkey; the sort is shared only when
     // the two index maps really are equal
     k->share_b = !ZK_NO_SHARE_B && im[QB1].sidx == im[QB2].sidx && !im[QB1].sidx.empty();
+    k->front = MSM_MERGE_CH && k->share_b && nshards == 1 && logn <= 16;
     if (e == hipSuccess && MSM_MERGE_CH) e = upload(k->bCH, im[QCH], false, X);
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bC, im[QC], false, X);
     if (e == hipSuccess && !MSM_MERGE_CH) e = upload(k->bH, im[QH], h_identity, 0xFFFFFFFFu);
