@@ -995,7 +995,8 @@ def main():
     if args.merkle_log2n:
         merkle = merkle_leg(ctx, rank, args.merkle_log2n)
         log(f"[bench r{rank}] dataset commitment: {merkle}")
-    split_res = None
+    split_res = {"skipped": "off by default (--split-proofs N runs it): one proof split over the ranks is bounded "
+                            "by one GPU's latency schedule (DESIGN.md §7)"}
     if args.split_proofs:  # last: the other legs never run beside a second (shard) key
         split_res = split_leg(ctx, rank, world, zk, split_wts, key, dist, args.split_proofs)
         log(f"[bench r{rank}] split proof: {split_res}")
