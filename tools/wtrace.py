@@ -40,7 +40,7 @@ SYMBOL = {"acc": "k_msm_accumulate", "stitch": "k_msm_stitch", "wsum0": "k_msm_w
           "sort_count": "k_msm_bin_count", "sort_scan": "k_msm_bin_scan", "sort_scatter": "k_msm_bin_scatter",
           "sort_bins": "k_msm_bin_sort", "tail_reset": "k_msm_tail_reset", "ntt_cols_inv": "k_ntt_colsILb1",
           "ntt_lds": "k_ntt_lds_pair", "ntt_cols_fwd": "k_ntt_colsILb0", "abc": "k_abc_chunks", "abc_rows": "k_abc_rows",
-          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_proof_start", "witness": "k_wit_level"}
+          "join": "k_join", "assemble": "k_assemble", "set_extra": "k_proof_start", "witness": "k_wit_lvl"}
 
 
 def kind_name(k):

@@ -1,7 +1,7 @@
 // BN254 Fr in nine 29-bit limbs (Montgomery R = 2^261): the witness engine's arithmetic.
 //
 // The witness program is a chain of dependent levels with few lanes each (config 5: 8 witnesses
-// per key and round), so the Poseidon permutations of k_wit_pos run one wave per SIMD and pay the
+// per key and round), so the Poseidon permutations of k_wit_lvl run one wave per SIMD and pay the
 // full latency -- issue and dependency -- of every product.  The 29-bit engine (field29.h, the
 // product-scanning f29_mont over modulus R29) takes one v_mad_u64_u32 per limb product and no
 // carry words: ~2.5x less single-wave latency than the 32-bit fp_mul (field29.h header).

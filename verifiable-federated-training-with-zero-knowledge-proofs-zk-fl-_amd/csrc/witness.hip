@@ -79,36 +79,30 @@ __global__ __launch_bounds__(256) void k_wit_to_m261(Fr* a, size_t n) {
 // per group of T lanes: lane i of a group holds state element i (9 VGPRs, no scratch), applies
 // the ARK constant and, in full rounds or for i = 0, the S-box (writing x^2, x^4, x^5 when the
 // template marks that S-box live), then computes MDS row i from the group's state read with
-// cross-lane shuffles, 4 products per Montgomery reduction.  The latency of a round is one row,
-// not T rows (one lane per permutation), and nothing is spilled.  Every lane of the wave executes
+// cross-lane shuffles, 4 products per Montgomery reduction (pos_rounds).  The latency of a round is
+// one row, not T rows (one lane per permutation), and nothing is spilled.  Every lane of the wave executes
 // the shuffles; lanes without a job compute on zeros and store nothing.
-__global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t op0, uint32_t cnt, uint32_t T,
-                                                Fr* W) {
-  ZK_WT(WT_WITNESS);
-  const uint32_t lane = threadIdx.x, G = 64 / T;
-  const uint32_t g = lane / T, i = lane - g * T;
-  const size_t job = (size_t)blockIdx.x * G + g;
-  const bool active = g < G && job < n * cnt;
-  const size_t jj = active ? job : 0;
-  const uint4 op = P.ops[op0 + (uint32_t)(jj % cnt)];
-  Fr* w = W + (jj / cnt) * P.n_wires;
-  const uint32_t gb = (g < G ? g : 0) * T;  // the group's first lane
-  Fr29 st = (active && i > 0) ? lc_eval(P, w, op.z + i - 1) : f29_zero();
-  const PosWidth pw = P.width[T];
-  const Fr* __restrict__ C = P.consts + pw.c_off;
-  const Fr* __restrict__ Mrow = P.consts + pw.m_off + (size_t)i * T;
+// The rounds of one permutation for widths T <= 4 NC: the MDS row is NC independent 4-term sums
+// (unrolled, so their shuffles, LDS reads and products overlap; a row's terms past T are zeros), the
+// MDS matrix is read from LDS (staged once per block) and the next round's ARK constant is loaded
+// while this round runs -- the round's latency is the S-box chain and one product, not a global
+// load and T / 4 serial products.
+struct PosCtx {
+  const Fr* C;     // round constants of the width (global)
+  const Fr* mrow;  // this lane's MDS row (LDS)
+  Fr* w;
+  uint4 op;
+  uint32_t T, i, gb, rp;
   uint32_t lw[7], pre[7];  // live S-box bitmap of the op's template and its word prefix counts
-  const uint32_t* live = P.tmpl + 8 * (op.w >> 8) + 1;
-  uint32_t acc_live = 0;
-#pragma unroll
-  for (int q = 0; q < 7; q++) {
-    lw[q] = active ? live[q] : 0u;
-    pre[q] = acc_live;
-    acc_live += __popc(lw[q]);
-  }
-  const uint32_t rp = pw.rp, rounds = 8 + rp;
+};
+template <int NC>
+ZK_DEV void pos_rounds(const PosCtx& X, Fr29 st) {
+  const uint32_t T = X.T, i = X.i, rp = X.rp, rounds = 8 + rp;
+  Fr cn = X.C[i];
   for (uint32_t r = 0; r < rounds; r++) {
-    st = fr29_add(st, fr29_ld(C[r * T + i]));
+    const Fr cr = cn;
+    if (r + 1 < rounds) cn = X.C[(r + 1) * T + i];  // in flight during this round
+    st = fr29_add(st, fr29_ld(cr));
     const bool full = r < 4 || r >= 4 + rp;
     if (full || i == 0) {
       const uint32_t sb = r < 4 ? r * T + i : (r < 4 + rp ? 4 * T + (r - 4) : 4 * T + rp + (r - 4 - rp) * T + i);
@@ -118,31 +112,74 @@ __global__ __launch_bounds__(64) void k_wit_pos(ProgView P, size_t n, uint32_t o
 #pragma unroll
       for (int k = 0; k < 7; k++)
         if ((uint32_t)k == q) {
-          word = lw[k];
-          rank = pre[k];
+          word = X.lw[k];
+          rank = X.pre[k];
         }
       if ((word >> bit) & 1u) {
-        const uint32_t k = op.y + 3 * (rank + __popc(word & ((1u << bit) - 1u)));
-        w[k] = fr29_st(x2);
-        w[k + 1] = fr29_st(x4);
-        w[k + 2] = fr29_st(x5);
+        const uint32_t k = X.op.y + 3 * (rank + __popc(word & ((1u << bit) - 1u)));
+        X.w[k] = fr29_st(x2);
+        X.w[k + 1] = fr29_st(x4);
+        X.w[k + 2] = fr29_st(x5);
       }
       st = x5;
     }
-    Fr29 acc = f29_zero();
-    for (uint32_t j0 = 0; j0 < T; j0 += 4) {
+    Fr29 part[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
       Fr29 x[4], y[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const uint32_t j = j0 + k;
-        const uint32_t src = gb + (j < T ? j : 0);
+        const uint32_t j = 4 * c + k;
+        const uint32_t src = X.gb + (j < T ? j : 0);
 #pragma unroll
         for (int v = 0; v < 9; v++) x[k].v[v] = __shfl((int)st.v[v], (int)src);
-        y[k] = j < T ? fr29_ld(Mrow[j]) : f29_zero();
+        y[k] = j < T ? fr29_ld(X.mrow[j]) : f29_zero();
       }
-      acc = fr29_add(acc, fr29_mulsum<4>(x, y));
+      part[c] = fr29_mulsum<4>(x, y);
     }
+    Fr29 acc = part[0];
+#pragma unroll
+    for (int c = 1; c < NC; c++) acc = fr29_add(acc, part[c]);
     st = acc;
+  }
+}
+
+// (block bx of a K_POS segment: 64 / T permutations; every thread of the block calls it)
+ZK_DEV void wit_pos_block(const ProgView& P, size_t n, uint32_t op0, uint32_t cnt, uint32_t T, Fr* W, size_t bx) {
+  const uint32_t lane = threadIdx.x, G = 64 / T;
+  const uint32_t g = lane / T, i = lane - g * T;
+  const size_t job = bx * G + g;
+  const bool active = g < G && job < n * cnt;
+  const size_t jj = active ? job : 0;
+  PosCtx X;
+  X.op = P.ops[op0 + (uint32_t)(jj % cnt)];
+  X.w = W + (jj / cnt) * P.n_wires;
+  X.gb = (g < G ? g : 0) * T;  // the group's first lane
+  X.T = T;
+  X.i = i;
+  const PosWidth pw = P.width[T];
+  X.rp = pw.rp;
+  X.C = P.consts + pw.c_off;
+  __shared__ Fr mds[MAX_T * MAX_T];  // the width's MDS matrix, read every round
+  const Fr* __restrict__ Mg = P.consts + pw.m_off;
+  for (uint32_t e = lane; e < T * T; e += 64) mds[e] = Mg[e];
+  __syncthreads();
+  X.mrow = mds + (size_t)i * T;
+  const uint32_t* live = P.tmpl + 8 * (X.op.w >> 8) + 1;
+  uint32_t acc_live = 0;
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    X.lw[q] = active ? live[q] : 0u;
+    X.pre[q] = acc_live;
+    acc_live += __popc(X.lw[q]);
+  }
+  const Fr29 st = (active && i > 0) ? lc_eval(P, X.w, X.op.z + i - 1) : f29_zero();
+  switch ((T + 3) / 4) {
+    case 1: pos_rounds<1>(X, st); break;
+    case 2: pos_rounds<2>(X, st); break;
+    case 3: pos_rounds<3>(X, st); break;
+    case 4: pos_rounds<4>(X, st); break;
+    default: pos_rounds<5>(X, st); break;
   }
 }
 
@@ -162,9 +199,8 @@ __global__ __launch_bounds__(64) void k_wit_inputs(size_t n, uint32_t nw, uint32
   w[in_first + i] = fr29_st(fr29_from_plain(v));
 }
 
-__global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t op0, uint32_t cnt, Fr* W) {
-  ZK_WT(WT_WITNESS);
-  size_t l = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// lane l of a segment of LC / MUL / INV / BITS ops: op l % cnt of witness l / cnt
+ZK_DEV void wit_op_lane(const ProgView& P, size_t n, uint32_t op0, uint32_t cnt, Fr* W, size_t l) {
   if (l >= n * cnt) return;
   const size_t j = l / cnt;
   const uint4 op = P.ops[op0 + (uint32_t)(l % cnt)];
@@ -197,9 +233,31 @@ __global__ __launch_bounds__(64) void k_wit_level(ProgView P, size_t n, uint32_t
       }
       break;
     }
-    default:  // K_POS ops run in k_wit_pos (wprog_load groups them per level and width)
+    default:  // K_POS ops run in lane groups (wit_pos_block: wprog_load groups them per level and width)
       break;
   }
+}
+
+// One level of the program in ONE launch: its segments (the LC / MUL / INV / BITS ops, then the
+// Poseidon permutations of each width) side by side, blocks [blk0[s], blk0[s + 1]) for segment s.
+// The ops of a level are independent, so a level's Poseidon widths no longer wait for each other:
+// the config-5 training circuit's first level holds permutations of widths 3, 5 and 6, which ran
+// as three dependent ~0.3-ms launches.
+constexpr int WIT_MAX_SEGS = MAX_T + 1;
+struct WitLevel {
+  uint32_t n;  // segments
+  uint32_t op0[WIT_MAX_SEGS], cnt[WIT_MAX_SEGS], t[WIT_MAX_SEGS];  // t = 0: LC / MUL / INV / BITS
+  uint32_t blk0[WIT_MAX_SEGS + 1];
+};
+__global__ __launch_bounds__(64) void k_wit_lvl(ProgView P, size_t n, const WitLevel L, Fr* W) {
+  ZK_WT(WT_WITNESS);
+  uint32_t s = 0;
+  while (s + 1 < L.n && blockIdx.x >= L.blk0[s + 1]) s++;
+  const size_t bx = blockIdx.x - L.blk0[s];
+  if (L.t[s] == 0)
+    wit_op_lane(P, n, L.op0[s], L.cnt[s], W, bx * 64 + threadIdx.x);
+  else
+    wit_pos_block(P, n, L.op0[s], L.cnt[s], L.t[s], W, bx);
 }
 
 __global__ __launch_bounds__(64) void k_wit_asserts(ProgView P, size_t n, uint32_t na, const Fr* W, uint32_t* fail) {
@@ -234,9 +292,10 @@ struct WProg {
   uint32_t n_ops = 0, n_levels = 0, n_asserts = 0;
   std::vector<uint32_t> level_ptr;
   struct Seg {
-    uint32_t op0, cnt, t;  // t = 0: k_wit_level ops; else K_POS ops of width t (k_wit_pos)
+    uint32_t op0, cnt, t;  // t = 0: LC / MUL / INV / BITS ops; else K_POS ops of width t
   };
-  std::vector<Seg> segs;        // launch order: level by level
+  std::vector<Seg> segs;            // level by level
+  std::vector<uint32_t> seg_level;  // segs of level L: [seg_level[L], seg_level[L + 1]) -- one launch each
   ProgView view = {};
   std::vector<void*> allocs;
 };
@@ -283,9 +342,10 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
   const uint32_t n_lcs = H.n_lcs, n_terms = H.n_terms, n_tmpl = H.n_tmpl;
   const uint8_t *lcp = H.lc_ptr, *tw = H.term_wire, *tc = H.term_coef, *as = H.asserts, *tm = H.tmpl;
   // Ops of a level are independent: regroup each level as [other ops][K_POS by width] so the
-  // Poseidon permutations run in k_wit_pos lane groups of their width.
+  // Poseidon permutations run in lane groups of their width (k_wit_lvl: one launch per level).
   std::vector<uint4> ops_v(p->n_ops);
   for (uint32_t L = 0; L < p->n_levels; L++) {
+    p->seg_level.push_back((uint32_t)p->segs.size());
     const uint32_t a = p->level_ptr[L], b = p->level_ptr[L + 1];
     uint32_t o = a;
     for (uint32_t t = 0; t <= (uint32_t)MAX_T; t++) {
@@ -299,6 +359,7 @@ int wprog_load(const uint8_t* img, size_t len, hipStream_t st, WProg** out, std:
       if (o > first) p->segs.push_back({first, o - first, t});
     }
   }
+  p->seg_level.push_back((uint32_t)p->segs.size());
   const uint8_t* ops = reinterpret_cast<const uint8_t*>(ops_v.data());
   std::vector<uint8_t>& consts = H.consts;
   struct Up {
@@ -361,12 +422,20 @@ hipError_t wprog_enqueue(const WProg* p, size_t m, const uint32_t* d_in, Fr* W, 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_wit_inputs, dim3(zk_grid(m * (n_in + 1), 64)), dim3(64), 0, st, m, nw, p->in_first, n_in, d_in,
                      W);
-  for (const WProg::Seg& g : p->segs) {
-    if (g.t == 0)
-      hipLaunchKernelGGL(k_wit_level, dim3(zk_grid(m * g.cnt, 64)), dim3(64), 0, st, p->view, m, g.op0, g.cnt, W);
-    else
-      hipLaunchKernelGGL(k_wit_pos, dim3(zk_grid(m * g.cnt, 64 / g.t)), dim3(64), 0, st, p->view, m, g.op0, g.cnt, g.t,
-                         W);
+  for (size_t L = 0; L + 1 < p->seg_level.size(); L++) {
+    WitLevel lv = {};
+    uint32_t blocks = 0;
+    for (uint32_t q = p->seg_level[L]; q < p->seg_level[L + 1]; q++) {
+      const WProg::Seg& g = p->segs[q];
+      lv.op0[lv.n] = g.op0;
+      lv.cnt[lv.n] = g.cnt;
+      lv.t[lv.n] = g.t;
+      lv.blk0[lv.n] = blocks;
+      blocks += g.t == 0 ? zk_grid(m * g.cnt, 64) : zk_grid(m * g.cnt, 64 / g.t);
+      lv.n++;
+    }
+    lv.blk0[lv.n] = blocks;
+    if (blocks) hipLaunchKernelGGL(k_wit_lvl, dim3(blocks), dim3(64), 0, st, p->view, m, lv, W);
   }
   if (p->n_asserts)
     hipLaunchKernelGGL(k_wit_asserts, dim3(zk_grid(m * p->n_asserts, 64)), dim3(64), 0, st, p->view, m, p->n_asserts,
