@@ -395,7 +395,7 @@ def roofline(prof, key, traffic=True, nprof=1, pmc_path=PMC_TRAFFIC, sq_path=SQ_
                      "clock_source": clk_src}}
 
 
-def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
+def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0, check=True):
     """BASELINE config 5: federated rounds of 8 clients x {training sgd_verified(8,4,3), secure
     aggregation SecureMaskedUpdate(4,7)} (tests/full_system_simulation.mjs:1278-1343), both keys
     resident, input.json text -> C parse -> GPU witness -> proof through zkfl_groth16_full_prove_multi
@@ -403,7 +403,8 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
       strong: `rounds` rounds in total, global proof k -> GPU k mod G (SURVEY.md §8e);
       weak:   `weak_rounds` rounds of 8 clients per GPU (each rank its own clients, ids offset by
               8 x rank), so per-GPU work is fixed as G grows -- "batch-sharded across 8 MI355X".
-    Every proof is GPU-verified afterwards.  -> (strong report, weak report or None) (rank 0)."""
+    Every proof is GPU-verified afterwards (check=False: counted, not enforced -- knock-out probes
+    only, tools/c5_probe.py --no-check).  -> (strong report, weak report or None) (rank 0)."""
     from zkfl import circuits, clients, groth16, native, wprog, zkey
     t0 = time.perf_counter()
     circ = {"train": circuits.build("sgd_verified", 8, 4, 3, 1000), "secagg": circuits.build("secure_masked_update", 4, 7)}
@@ -460,7 +461,7 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
     run(warm)
     elapsed, out = timed(mine, "strong")
     ok = verified(mine, out)
-    if ok != rounds * 16:
+    if check and ok != rounds * 16:
         raise SystemExit(f"[bench r{rank}] c5: {rounds * 16 - ok} proofs do not verify")
     workload = ("8 clients x {sgd_verified(8,4,3,1000) training, SecureMaskedUpdate(4,7) secagg} per round, "
                 "input.json -> C parse -> GPU witness groups per key -> proof (zkfl_groth16_full_prove_multi, "
@@ -475,7 +476,7 @@ def c5_leg(ctx, rank, world, rounds, slots, dist, weak_rounds=0):
         elapsed_w, out_w = timed(mine_w, "weak")
         ok_w = verified(mine_w, out_w)
         total = world * weak_rounds * 16
-        if ok_w != total:
+        if check and ok_w != total:
             raise SystemExit(f"[bench r{rank}] c5 weak: {total - ok_w} proofs do not verify")
         weak = {"value": round(total / elapsed_w, 3), "unit": "proofs/s", "proofs": total, "verified": ok_w,
                 "rounds_per_gpu": weak_rounds, "clients_per_gpu": 8, "scaling": "weak",

@@ -12,7 +12,9 @@ OUT=$R/build_ab/$NAME
 mkdir -p "$OUT"
 CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$R/include -I$PKG/csrc -Wno-unused-result $FLAGS"
 pids=()
-for s in zkfl ntt msm_g1 msm_g2 verify witness merkle setup; do
+# the library's HIP sources, as the package Makefile lists them
+SRCS=$(sed -n 's/^SRCS := //p' "$PKG/Makefile")
+for s in $SRCS; do
   $CXX -c -o "$OUT/$s.o" "$PKG/csrc/$s.hip" & pids+=($!)
 done
 g++ -O2 -fPIC -std=c++17 -I"$R/include" -I"$PKG/csrc" -c -o "$OUT/host_parse.o" "$PKG/csrc/host_parse.cc" & pids+=($!)

@@ -212,9 +212,9 @@ ZK_HD void f29_keep(uint64_t& a) {
 #endif
 }
 
-// NACC: accumulators per column (chains a lone wave can issue from; the latency-bound kernels --
-// k_assemble's quad operations -- take 4, the throughput kernels 2: every extra chain costs one
-// 64-bit join per column).  M: the modulus (P29 = Fq; R29 = Fr, fr29.h) -- MASK, NINV, P[9].
+// NACC: accumulators per column (chains a lone wave can issue from; every extra chain costs one
+// 64-bit join per column: the throughput kernels take 2, and so do k_assemble's quad additions,
+// where 4 measured no better, profiles/r05_ab_q29_acc.log).  M: the modulus (P29 = Fq; R29 = Fr, fr29.h) -- MASK, NINV, P[9].
 template <int NP, int NACC = (F29_SPLIT ? 2 : 1), class M = P29>
 ZK_HD F29 f29_mont(const F29 (&x)[NP], const F29 (&y)[NP]) {
   static_assert(NACC == 1 || NACC == 2 || NACC == 4, "accumulators per column");

@@ -12,7 +12,7 @@
 //      pi_c = C + H + s pi_a + r (B1 + beta1 + s delta1) - r s delta1
 //      The constant terms are folded into the MSMs as extra bases (alpha1/delta1 on A,
 //      beta1/delta1 on B1, beta2/delta2 on B2, delta1 with scalar -rs on C); only
-//      s*pi_a + r*B1 remains for k_assemble (Shamir double-and-add), then affine, std form.
+//      s*pi_a + r*B1 remains for k_assemble (GLV halves, windowed, one wave each), then affine.
 // Everything from the device-resident witness to the 256-byte proof runs on the GPU; the host
 // only parses files, uploads, and launches.
 #include <hip/hip_runtime.h>
@@ -436,6 +436,114 @@ struct Q29 {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Row policy (glv_row_mul): one value per 16-lane row of a wave, lane j of the row holding limb j
+// of the nine 29-bit limbs (lanes 9..15 zero), same Montgomery domain (2^261) and the same integer
+// results as Q29.  A product is spread over its row: limb i of a is broadcast by DPP row_newbcast,
+// each lane accumulates column i + j in 64 bits, and the row shifts down one lane per reduction
+// step (DPP row_shl, lane 0's carry kept): 18 v_mad_u64_u32 per lane instead of 162, so one wave
+// evaluates a level's four products (one per row) at ~1/9 of the quad's multiply issue.  Products
+// cross rows by the gfx950 row swaps (bcast<K>).  Limbs are lazy: lanes 0..7 below 2^29 + 2^7 (one or two
+// carry-save steps per operation), lane 8 the exact top; the integer bounds are Q29's.
+// ---------------------------------------------------------------------------
+ZK_DEV uint32_t row_j() { return __lane_id() & 15u; }
+template <int CTRL, bool BOUND>
+ZK_DEV uint32_t row_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, BOUND);
+}
+template <int I>
+ZK_DEV uint32_t row_limb(uint32_t v) { return row_dpp<0x150 + I, false>(v); }  // row_newbcast:I
+ZK_DEV uint32_t row_up(uint32_t v) { return row_dpp<0x101, true>(v); }         // row_shl:1, lane 15 <- 0
+ZK_DEV uint32_t row_down(uint32_t v) { return row_dpp<0x111, true>(v); }       // row_shr:1, lane 0 <- 0
+ZK_DEV uint32_t limb_at(const Limbs9& c, uint32_t j) {  // c.v[j] (0 for j > 8)
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r = j == (uint32_t)i ? c.v[i] : r;
+  return r;
+}
+// k p + 2^31 (limbs 0..7) - 4 (limbs 1..8): a + this - b keeps every lane in [0, 2^32) for lazy b
+// (limbs < 2^29 + 2^7); the top limb may wrap below zero and is made whole by the carries
+__host__ __device__ constexpr Limbs9 row_kp(uint32_t k) {
+  Limbs9 r = p29_times(k, false);
+  for (int i = 0; i < 9; i++) r.v[i] += (i < 8 ? 0x80000000u : 0u) - (i > 0 ? 4u : 0u);
+  return r;
+}
+struct Row29 {
+  struct T {
+    uint32_t v;
+  };
+  // one carry-save step: lanes 0..7 keep 29 bits and pass the rest up one lane
+  static ZK_DEV uint32_t carry(uint32_t x) {
+    const bool top = row_j() >= 8;
+    const uint32_t h = top ? 0u : x >> 29;
+    return (top ? x : x & P29::MASK) + row_down(h);
+  }
+  static ZK_DEV T mul(const T& a, const T& b) {
+    const uint32_t j = row_j();
+    const uint32_t pj = limb_at(p29_times(1, false), j);
+    const uint32_t ai[9] = {row_limb<0>(a.v), row_limb<1>(a.v), row_limb<2>(a.v), row_limb<3>(a.v), row_limb<4>(a.v),
+                            row_limb<5>(a.v), row_limb<6>(a.v), row_limb<7>(a.v), row_limb<8>(a.v)};
+    uint64_t t = 0;  // lane j: column i + j
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      t += (uint64_t)ai[i] * b.v;
+      const uint32_t m = (row_limb<0>((uint32_t)t) * P29::NINV) & P29::MASK;
+      t += (uint64_t)m * pj;  // lane 0: column i is now 0 mod 2^29
+      // shift down one lane; lane 0 adds its own carry (t >> 29), as 32-bit add / add-with-carry
+      const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
+      const uint32_t clo = j == 0 ? __builtin_amdgcn_alignbit(hi, lo, 29) : 0u, chi = j == 0 ? hi >> 29 : 0u;
+      const uint32_t nlo = row_up(lo) + clo;
+      const uint32_t nhi = row_up(hi) + chi + (nlo < clo ? 1u : 0u);
+      t = ((uint64_t)nhi << 32) | nlo;
+    }
+    // lanes 0..8: columns 9..17 (< 2^63); two carry-save steps -> limbs < 2^29 + 2^7
+    const bool top = j >= 8;
+    const uint64_t h = top ? 0 : t >> 29;
+    const uint64_t x = (top ? t : t & P29::MASK) + (((uint64_t)row_down((uint32_t)(h >> 32)) << 32) | row_down((uint32_t)h));
+    const uint32_t h2 = top ? 0u : (uint32_t)(x >> 29);
+    return {(top ? (uint32_t)x : (uint32_t)x & P29::MASK) + row_down(h2)};
+  }
+  static ZK_DEV T add(const T& a, const T& b) { return {carry(a.v + b.v)}; }
+  template <int K>
+  static ZK_DEV T sub(const T& a, const T& b) {
+    constexpr Limbs9 k = row_kp(K);
+    return {carry(a.v + limb_at(k, row_j()) - b.v)};
+  }
+  static ZK_DEV T dbl(const T& a) { return add(a, a); }
+  static ZK_DEV T zero() { return {0u}; }
+  static ZK_DEV T one() {
+    constexpr Limbs9 o{{P29::ONE[0], P29::ONE[1], P29::ONE[2], P29::ONE[3], P29::ONE[4], P29::ONE[5], P29::ONE[6],
+                        P29::ONE[7], P29::ONE[8]}};
+    return {limb_at(o, row_j())};
+  }
+  // row K's value to every row: v_permlane16_swap of v with itself gives rows (0, 0, 2, 2) and
+  // (1, 1, 3, 3), v_permlane32_swap of either with itself rows (k, k, k, k) and (k + 2, ...): three
+  // VALU swaps serve all four K (the formulas' bcast<K> of one product share them)
+  template <int K>
+  static ZK_DEV T bcast(const T& v) {
+    const auto s = __builtin_amdgcn_permlane16_swap(v.v, v.v, false, false);
+    const uint32_t e = (K & 1) ? s[1] : s[0];
+    const auto u = __builtin_amdgcn_permlane32_swap(e, e, false, false);
+    return {(K & 2) ? u[1] : u[0]};
+  }
+  static ZK_DEV T pick4(int q, T a, T b, T c, T d) { return {(q & 2) ? ((q & 1) ? d.v : c.v) : ((q & 1) ? b.v : a.v)}; }
+  // a full value (every lane) -> its row form, and back (row 0, normalized limbs)
+  static ZK_DEV T from(const F29& x) {
+    const uint32_t j = row_j();
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r = j == (uint32_t)i ? x.v[i] : r;
+    return {r};
+  }
+  static ZK_DEV F29 to(const T& x) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.v, i);
+    f29_norm(r);
+    return r;
+  }
+};
+
 template <class QF>
 struct QPoint {
   typename QF::T X, Y, ZZ, ZZZ;
@@ -456,10 +564,14 @@ ZK_DEV G1P g1q_to(const G1Q& p) {  // canonical coordinates out
 // dbl-2008-s-1 by levels: {U^2, X^2} -> {U V, X V, V ZZ, M^2} -> {M (S - X3), W Y, W ZZZ}
 // Bounds (X < 8p, Y < 4p, ZZ, ZZZ < 2p in): U < 8p; V, X2 < 2p (64 p^2); M < 6p; W, S, ZZ3, M2
 // < 2p (36 p^2); X3 < 6p; S - X3 < 8p; Y3's products < 2p (48 p^2), Y3 < 4p.
-template <class QF>
+// CHECK = false: the operands are known to be finite and distinct (the row chains of glv_row_mul),
+// so the special cases are not tested (the row policy has no is_zero)
+template <class QF, bool CHECK = true>
 ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
   using T = typename QF::T;
-  if (qp_is_inf(p)) return p;
+  if constexpr (CHECK) {
+    if (qp_is_inf(p)) return p;
+  }
   const T U = QF::dbl(p.Y);
   const T a1 = QF::pick4(q & 1, U, p.X, U, p.X);
   T t = QF::mul(a1, a1);
@@ -482,18 +594,22 @@ ZK_DEV QPoint<QF> quad_dbl(const QPoint<QF>& p, int q) {
 // Bounds (both points X < 8p, Y < 4p, ZZ, ZZZ < 2p): U1, U2, S1, S2 < 2p (16 p^2); P, R < 4p;
 // PP, R2, Z12, ZZZ12 < 2p; PPP, Q, ZZ3 < 2p; X3 < 8p; Q - X3 < 10p; Y3's products < 2p
 // (40 p^2), Y3 < 4p.
-template <class QF>
+template <class QF, bool CHECK = true>
 ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
   using T = typename QF::T;
-  if (qp_is_inf(o)) return p;
-  if (qp_is_inf(p)) return o;
+  if constexpr (CHECK) {
+    if (qp_is_inf(o)) return p;
+    if (qp_is_inf(p)) return o;
+  }
   T t = QF::mul(QF::pick4(q, p.X, o.X, p.Y, o.Y), QF::pick4(q, o.ZZ, p.ZZ, o.ZZZ, p.ZZZ));
   const T U1 = QF::template bcast<0>(t), U2 = QF::template bcast<1>(t), S1 = QF::template bcast<2>(t),
           S2 = QF::template bcast<3>(t);
   const T P = QF::template sub<2>(U2, U1), R = QF::template sub<2>(S2, S1);
-  if (QF::template is_zero<4>(P)) {
-    if (QF::template is_zero<4>(R)) return quad_dbl<QF>(p, q);
-    return qp_inf<QF>();
+  if constexpr (CHECK) {
+    if (QF::template is_zero<4>(P)) {
+      if (QF::template is_zero<4>(R)) return quad_dbl<QF>(p, q);
+      return qp_inf<QF>();
+    }
   }
   t = QF::mul(QF::pick4(q, P, R, p.ZZ, p.ZZZ), QF::pick4(q, P, R, o.ZZ, o.ZZZ));
   const T PP = QF::template bcast<0>(t), R2 = QF::template bcast<1>(t), Z12 = QF::template bcast<2>(t),
@@ -541,11 +657,22 @@ ZK_DEV Affine<Fq2Ops> g2_to_affine_bgcd(const G2P& p) {
   return {f2_mul(p.X, f2_sqr(iZ)), f2_mul(p.Y, iZZZ)};
 }
 
-// One quad's GLV half of the assembly's scalar multiplications: quad g < 4 of wave 0 computes
-// k_g * P_g for (s1, A'), (s2, phi(A')), (r1, B1'), (r2, phi(B1')) (res[0] = A', res[1] = B1'),
-// the GLV halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows over the quad's
-// table of 1P..8P in LDS (tab: its row), each point operation evaluated by the quad.
-ZK_DEV G1Q glv_quad_mul(const G1P* __restrict__ res, const GlvScalar* __restrict__ ks, G1Q* tab, int g, int q) {
+// One GLV half of the assembly's scalar multiplications, on one whole wave in the row policy (Row29):
+// wave g < 4 computes k_g * P_g for (s1, A'), (s2, phi(A')), (r1, B1'), (r2, phi(B1')) (res[0] =
+// A', res[1] = B1'), the GLV halves of s and r (glv.h): 128-bit scalars in signed 4-bit windows
+// over a table of 1P..8P in LDS, the wave's four rows evaluating each level's products side by
+// side (a quad chain in one wave, the round-4..6 form, took 664 us per assembly under config 5's
+// load against 405 us: profiles/r06_ab_row_assembly.log).  No special cases are tested, and
+// none can occur: P' = +-P or +-phi(P) is finite (checked) of prime order r; the table j P'
+// (j <= 8) is built by one doubling and additions (j - 1) P' + P', j >= 3; the accumulator starts
+// at the first nonzero window and is then m P' with m >= 1 -- the signed base-16 prefix of a
+// non-negative scalar is >= 0, and 16 m' + d >= 9 once m' >= 1 -- so every addition adds
+// d P' (|d| <= 8) to 16 m' P' with 16 <= 16 m' < 2^133 < r - 8 (never equal, opposite or
+// infinity), and a doubling never meets a point of order 2.  The proof bytes are the quad
+// chain's (same integers: the row product is the same Montgomery reduction).
+// tab: this wave's LDS table, 8 points x 4 coordinates x 64 lanes.
+ZK_DEV G1Q glv_row_mul(const G1P* __restrict__ res, const GlvScalar* __restrict__ ks, uint32_t* tab, int g) {
+  using RPt = QPoint<Row29>;
   G1P P = res[g >> 1];
   if (g & 1) {  // phi(X/ZZ, Y/ZZZ) = (beta X/ZZ, Y/ZZZ)
     Fq beta;
@@ -556,13 +683,22 @@ ZK_DEV G1Q glv_quad_mul(const G1P* __restrict__ res, const GlvScalar* __restrict
   const GlvScalar k = ks[g];
   if (k.neg) P = xyzz_neg<FqOps>(P);
   const G1Q P29 = g1q_from(P);
-  if (q == 0) tab[0] = P29;
-  G1Q Q = quad_dbl<Q29>(P29, q);
-  if (q == 0) tab[1] = Q;
+  if (qp_is_inf(P29)) return qp_inf<Q29>();
+  const int lane = (int)__lane_id(), q = lane >> 4;
+  const RPt Pr = {Row29::from(P29.X), Row29::from(P29.Y), Row29::from(P29.ZZ), Row29::from(P29.ZZZ)};
+  auto put = [&](int e, const RPt& t) {
+    tab[(4 * e + 0) * 64 + lane] = t.X.v;
+    tab[(4 * e + 1) * 64 + lane] = t.Y.v;
+    tab[(4 * e + 2) * 64 + lane] = t.ZZ.v;
+    tab[(4 * e + 3) * 64 + lane] = t.ZZZ.v;
+  };
+  put(0, Pr);
+  RPt Q = quad_dbl<Row29, false>(Pr, q);
+  put(1, Q);
 #pragma unroll 1
-  for (int j = 2; j < 8; j++) {
-    Q = quad_add<Q29>(Q, P29, q);
-    if (q == 0) tab[j] = Q;
+  for (int e = 2; e < 8; e++) {
+    Q = quad_add<Row29, false>(Q, Pr, q);
+    put(e, Q);
   }
   // signed base-16 digits d_0..d_32 in [-7, 8], packed as nibbles (d & 15): word i holds
   // d_8i .. d_8i+7, word 4 holds d_32 (the final carry)
@@ -574,36 +710,51 @@ ZK_DEV G1Q glv_quad_mul(const G1P* __restrict__ res, const GlvScalar* __restrict
     dg[w >> 3] |= (carry ? (v - 16) & 15u : v) << (4 * (w & 7));
   }
   dg[4] = carry;
-  G1Q acc = qp_inf<Q29>();
+  bool inf = true;
+  RPt acc = Pr;
 #pragma unroll 1
   for (int w = 32; w >= 0; w--) {
-    if (w < 32)
-      for (int j = 0; j < 4; j++) acc = quad_dbl<Q29>(acc, q);
+    if (!inf)
+      for (int i = 0; i < 4; i++) acc = quad_dbl<Row29, false>(acc, q);
     const int wi = w >> 3;
     const uint32_t word = wi == 0 ? dg[0] : wi == 1 ? dg[1] : wi == 2 ? dg[2] : wi == 3 ? dg[3] : dg[4];
     const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
     if (nib) {
       const int d = nib >= 9 ? (int)nib - 16 : (int)nib;
-      G1Q t = tab[(d < 0 ? -d : d) - 1];
-      const F29 ny = Q29::sub<4>(Q29::zero(), t.Y);  // Y < 4p
-#pragma unroll
-      for (int i = 0; i < 9; i++) t.Y.v[i] = d < 0 ? ny.v[i] : t.Y.v[i];  // per-limb: no stack copy
-      acc = quad_add<Q29>(acc, t, q);
+      const int e = (d < 0 ? -d : d) - 1;
+      RPt t = {{tab[(4 * e + 0) * 64 + lane]}, {tab[(4 * e + 1) * 64 + lane]}, {tab[(4 * e + 2) * 64 + lane]},
+               {tab[(4 * e + 3) * 64 + lane]}};
+      if (d < 0) t.Y = Row29::sub<4>(Row29::zero(), t.Y);  // Y < 4p
+      if (inf)
+        acc = t;
+      else
+        acc = quad_add<Row29, false>(acc, t, q);
+      inf = false;
     }
   }
-  return acc;
+  if (inf) return qp_inf<Q29>();
+  return {Row29::to(acc.X), Row29::to(acc.Y), Row29::to(acc.ZZ), Row29::to(acc.ZZZ)};
 }
 
-// Proof assembly, one block of three waves (replaces snarkjs's final
+constexpr int ASM_THREADS = 64 * 6;    // k_assemble: four chain waves + C' + H / pi_a, pi_b
+constexpr int ASM_T_THREADS = 64 * 5;  // k_assemble_t: four chain waves + pi_a
+
+struct AsmLds {
+  uint32_t rtab[4][8 * 4 * 64];  // the chains' tables
+  G1Q part[6];                   // the four products, C' + H, then the sum of parts 2 + 3
+};
+
+// Proof assembly, one block (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
-//   wave 0, quads 0..3 (lanes 0..15): the four GLV halves (glv_quad_mul);
-//     quad 4: C' + H meanwhile; then quads 0, 1 sum the parts and quad 0 adds C' + H and writes
-//     pi_c (one inversion) -> proof[48..63]
-//   wave 1, lane 0: pi_a affine -> proof[0..15];  wave 2, lane 0: pi_b affine -> proof[16..47]
-// The critical path is 132 quad doublings + 33 quad additions + 2 additions + one inversion; the
-// quad operations run in the 29-bit engine (Q29, canonical values), every inversion is a binary GCD.
-__global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
-                                                  const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
+//   waves 0..3: the four GLV halves (glv_row_mul) -> part[0..3];
+//   wave 4: C' + H meanwhile (quad 0), and pi_a affine (lane 32) -> proof[0..15];
+//   wave 5, lane 0: pi_b affine -> proof[16..47];
+//   then quads 0, 1 of wave 0 sum the parts and quad 0 adds C' + H and writes pi_c (one inversion)
+//   -> proof[48..63]
+// The critical path is 132 doublings + 33 additions on the chains, 3 quad additions and one
+// inversion; the quad operations run in the 29-bit engine (Q29), every inversion is a binary GCD.
+__global__ void __launch_bounds__(ASM_THREADS) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
+                                                          const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
   ZK_WT(WT_ASSEMBLE);
   ZK_LIGHT();
   // one block per proof: block b reads res[5b..], resB2[b], ks[4b..] and writes proof[64b..]
@@ -611,31 +762,30 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
   resB2 += blockIdx.x;
   ks += 4 * blockIdx.x;
   proof += 64 * blockIdx.x;
-  __shared__ G1Q tab[4][8];
-  __shared__ G1Q part[6];  // the four products, C' + H, then the sum of parts 2 + 3
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ AsmLds sh;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int g = lane >> 2, q = lane & 3;
-  if (wave == 0 && g < 4) {
-    const G1Q acc = glv_quad_mul(res, ks, tab[g], g, q);
-    if (q == 0) part[g] = acc;
-  } else if (wave == 0 && g == 4) {  // C' + H, off the critical path
+  if (wave < 4) {
+    const G1Q acc = glv_row_mul(res, ks, sh.rtab[wave], wave);
+    if (lane == 0) sh.part[wave] = acc;
+  } else if (wave == 4 && g == 0) {  // C' + H, off the critical path
     const G1Q c = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
-    if (q == 0) part[4] = c;
-  } else if (wave == 1 && lane == 0) {
+    if (q == 0) sh.part[4] = c;
+  } else if (wave == 4 && lane == 32) {
     store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
-  } else if (wave == 2 && lane == 0) {
+  } else if (wave == 5 && lane == 0) {
     store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
   }
   __syncthreads();
   if (wave == 0 && g == 1) {
-    const G1Q t = quad_add<Q29>(part[2], part[3], q);
-    if (q == 0) part[5] = t;
+    const G1Q t = quad_add<Q29>(sh.part[2], sh.part[3], q);
+    if (q == 0) sh.part[5] = t;
   }
   G1Q t01 = qp_inf<Q29>();
-  if (wave == 0 && g == 0) t01 = quad_add<Q29>(part[0], part[1], q);
+  if (wave == 0 && g == 0) t01 = quad_add<Q29>(sh.part[0], sh.part[1], q);
   __syncthreads();
   if (wave == 0 && g == 0) {
-    const G1Q C = quad_add<Q29>(quad_add<Q29>(t01, part[5], q), part[4], q);
+    const G1Q C = quad_add<Q29>(quad_add<Q29>(t01, sh.part[5], q), sh.part[4], q);
     if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
   }
 }
@@ -646,30 +796,29 @@ __global__ void __launch_bounds__(192) k_assemble(const G1P* __restrict__ res, c
 // k_assemble_c at the end: pi_c = (C' + H) + T -> proof[48..63] and pi_b -> proof[16..47].
 // pi_c is the same point as k_assemble's (the group sum does not depend on the order), so the
 // proof bytes are identical.
-__global__ void __launch_bounds__(128) k_assemble_t(G1P* __restrict__ res, const GlvScalar* __restrict__ ks,
-                                                    uint32_t* __restrict__ proof) {
+__global__ void __launch_bounds__(ASM_T_THREADS) k_assemble_t(G1P* __restrict__ res, const GlvScalar* __restrict__ ks,
+                                                              uint32_t* __restrict__ proof) {
   ZK_WT(WT_ASSEMBLE);
   ZK_LIGHT();
-  __shared__ G1Q tab[4][8];
-  __shared__ G1Q part[6];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ AsmLds sh;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int g = lane >> 2, q = lane & 3;
-  if (wave == 0 && g < 4) {
-    const G1Q acc = glv_quad_mul(res, ks, tab[g], g, q);
-    if (q == 0) part[g] = acc;
-  } else if (wave == 1 && lane == 0) {
+  if (wave < 4) {
+    const G1Q acc = glv_row_mul(res, ks, sh.rtab[wave], wave);
+    if (lane == 0) sh.part[wave] = acc;
+  } else if (wave == 4 && lane == 0) {
     store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
   }
   __syncthreads();
   if (wave == 0 && g == 1) {
-    const G1Q t = quad_add<Q29>(part[2], part[3], q);
-    if (q == 0) part[5] = t;
+    const G1Q t = quad_add<Q29>(sh.part[2], sh.part[3], q);
+    if (q == 0) sh.part[5] = t;
   }
   G1Q t01 = qp_inf<Q29>();
-  if (wave == 0 && g == 0) t01 = quad_add<Q29>(part[0], part[1], q);
+  if (wave == 0 && g == 0) t01 = quad_add<Q29>(sh.part[0], sh.part[1], q);
   __syncthreads();
   if (wave == 0 && g == 0) {
-    const G1Q T = quad_add<Q29>(t01, part[5], q);
+    const G1Q T = quad_add<Q29>(t01, sh.part[5], q);
     if (q == 0) res[4] = g1q_to(T);
   }
 }
@@ -1378,7 +1527,7 @@ int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w
   rc = run_segment(s, 2, d_w, sa, seg_graphs, [&]() -> int {
     G1P* outs[2] = {s->res + 0, s->res + 1};
     HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
-    hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
+    hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(ASM_T_THREADS), 0, sa, s->res,
                        reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
     return ZKFL_OK;
   });
@@ -1451,7 +1600,7 @@ int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_
     G1P* outs[2] = {s->res + 0, s->res + 1};
     HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
   }
-  hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(128), 0, sa, s->res,
+  hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(ASM_T_THREADS), 0, sa, s->res,
                      reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
   HIP_TRY(hipEventRecord(ev_t, sa), "event");
   // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
@@ -1637,7 +1786,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
   }
   if (!plain && !(ZK_KNOCKOUT & 1)) {
     const int pa = prof->begin("assemble", st);
-    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(192), 0, st, s->res, s->resB2,
+    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(ASM_THREADS), 0, st, s->res, s->resB2,
                        reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64),
                        proof_out(s));
     prof->end(pa, st, 1.0);
@@ -2538,7 +2687,7 @@ int zkfl_groth16_assemble(zkfl_ctx* ctx, size_t n, size_t n_parts, const uint8_t
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "assemble");
   if (bad) return fail(ZKFL_E_ARG, "assemble: a part holds a point that is not on its curve");
-  hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n), dim3(192), 0, st, (const G1P*)d_res, (const G2P*)d_b2,
+  hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n), dim3(ASM_THREADS), 0, st, (const G1P*)d_res, (const G2P*)d_b2,
                      (const GlvScalar*)d_ks, (uint32_t*)d_proof);
   e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(proofs_out, d_proof, n * 256, hipMemcpyDeviceToHost, st);
