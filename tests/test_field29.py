@@ -108,17 +108,17 @@ def test_sqr_normalized_extremes(f29):
 
 
 def test_inverse_and_canon(f29):
-    """The assembly's inversion (binary extended Euclid, k_assemble's affine conversions) and the
+    """The assembly's inversion (divsteps, k_assemble's affine conversions) and the
     canonicalization, against Python big integers."""
     rng = random.Random(31)
-    vals = [1, 2, P - 1, R % P] + [rng.randrange(1, P) for _ in range(40)]
+    vals = [1, 2, 3, P - 1, P - 2, R % P, (1 << 253) % P, P // 2] + [rng.randrange(1, P) for _ in range(440)]
     lifted = [v + rng.randrange(2) * P for v in vals]          # inputs < 2p
-    got = f29(["invb " + limbs(v) for v in lifted])          # canonical out
+    got = f29(["invd " + limbs(v) for v in lifted])          # canonical out
     for v, (r,) in zip(vals, got):
         assert r == pow(v * RINV, -1, P) * R % P
-    # 0 and p (both 0 mod p) have no inverse: 0 comes back at once (it used to halve u = 0 forever,
-    # ADVICE r3: a malformed split-proof part reached it through k_assemble)
-    assert [list(x) for x in f29(["invb " + limbs(0), "invb " + limbs(P)])] == [[0], [0]]
+    # 0 and p (both 0 mod p) have no inverse: 0 comes back (as the Fermat inverse's 0^(p-2); a
+    # malformed split-proof part can reach it through k_assemble, ADVICE r3)
+    assert [list(x) for x in f29(["invd " + limbs(0), "invd " + limbs(P)])] == [[0], [0]]
     cv = [rng.randrange(4 * P) for _ in range(200)] + [0, P, 2 * P, 3 * P, 4 * P - 1, P - 1]
     got = f29(["canon " + limbs(v) for v in cv])
     for v, (r,) in zip(cv, got):

@@ -175,8 +175,8 @@ int main() {
       wr(f29_pack(fr29_to_m256(rd(in)).v));
     } else if (op == "sqr") {
       wr(f29_sqr(rd(in)));
-    } else if (op == "invb") {
-      wr(f29_inv_bgcd(rd(in)));
+    } else if (op == "invd") {
+      wr(f29_inv_divsteps(rd(in)));
     } else if (op == "canon") {  // normalized a < 4p -> canonical
       wr(f29_canon_sub<3>(rd(in)));
     } else if (op == "mulsum2") {

@@ -670,96 +670,187 @@ ZK_HD F29 f29_canon_sub(F29 a) {
   return a;
 }
 
-// a^-1 by the binary extended Euclidean algorithm (one lane, no products in the loop: shifts,
-// compares and subtractions of 9-limb values; ~1.4 x 254 steps): the assembly's inversions sit on
-// a proof's critical path, where Fermat's chain of ~316 dependent Montgomery products is ~5x
-// longer.  In: normalized a < 2p, a != 0 mod p (Montgomery form a R); out: a^-1 R, < p.
 struct P29Inv {
   // R^3 mod p (R = 2^261): a plain inverse x = (aR)^-1 times R^3 through a Montgomery product is
   // a^-1 R (the Montgomery form of the inverse)
   static constexpr uint32_t R3[9] = {0x0e2312b2u, 0x16c05ca2u, 0x0bc84389u, 0x1cdf310bu, 0x11adafddu,
                                      0x032e568eu, 0x1d6ae48cu, 0x10d4cd1fu, 0x0026c2d2u};
 };
-ZK_HD bool f29_even(const F29& a) { return (a.v[0] & 1u) == 0; }
-ZK_HD bool f29_is_one_plain(const F29& a) {
-  uint32_t z = a.v[0] ^ 1u;
-#pragma unroll
-  for (int i = 1; i < 9; i++) z |= a.v[i];
-  return z == 0;
-}
-ZK_HD F29 f29_shr1(const F29& a) {  // normalized -> normalized
-  F29 r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (a.v[i] >> 1) | ((a.v[i + 1] & 1u) << 28);
-  r.v[8] = a.v[8] >> 1;
+
+// a^-1 (the assembly's inversions, one lane each): in normalized a < 2p (Montgomery form a R), out
+// a^-1 R < p; a = 0 mod p gives 0 (as the Fermat inverse 0^(p-2)).  Bernstein-Yang divsteps ("Fast
+// constant-time gcd computation and modular inversion", 2019) in the 30-bit-limb form of
+// libsecp256k1's modinv32: 20 batches of 30 divsteps,
+// each batch run on the low 30 bits of f and g alone (a 2 x 2 transition matrix scaled by 2^30),
+// then applied to the full f, g and to the Bezout coefficients d, e -- the latter mod p, plus the
+// multiple of p that makes them divisible by 2^30.  600 >= 590 divsteps settle any input below
+// 2^256 (f = +-1, d = +-(aR)^-1).  A fixed sequence of ~13 k 32/64-bit integer instructions on one
+// lane: the binary extended Euclid it replaced (~500 data-dependent rounds of 9-limb shifts and
+// subtractions) took 248 against 123 us in k_assemble_c (profiles/r06_ab_divsteps.log), Fermat's
+// chain of ~316 dependent products ~5x the Euclid.
+struct S30 {
+  int32_t v[9];  // signed 30-bit limbs: 0..7 in [0, 2^30), limb 8 signed
+};
+constexpr int32_t S30_M = (1 << 30) - 1;
+// normalized 29-bit limbs (value < 2^261) -> 30-bit limbs
+ZK_HD constexpr S30 s30_from29(const uint32_t (&a)[9]) {
+  S30 r{};
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)a[i] << bits;
+    bits += 29;
+    if (bits >= 30) {
+      r.v[k++] = (int32_t)(acc & S30_M);
+      acc >>= 30;
+      bits -= 30;
+    }
+  }
+  r.v[8] = (int32_t)acc;
   return r;
 }
-// a - b (normalized, a >= b as values) -> normalized; returns false (and garbage) when a < b
-ZK_HD bool f29_sub_plain(const F29& a, const F29& b, F29& r) {
-  int32_t c = 0;
+// 30-bit limbs of a value in [0, 2^261) -> normalized 29-bit limbs
+ZK_HD F29 f29_from30(const S30& a) {
+  F29 r;
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int32_t x = (int32_t)a.v[i] - (int32_t)b.v[i] + c;
-    r.v[i] = (uint32_t)x & P29::MASK;
-    c = x >> 29;
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)(uint32_t)a.v[i] << bits;
+    bits += 30;
+    while (bits >= 29 && k < 8) {
+      r.v[k++] = (uint32_t)acc & P29::MASK;
+      acc >>= 29;
+      bits -= 29;
+    }
   }
-  const int32_t top = (int32_t)a.v[8] - (int32_t)b.v[8] + c;
-  r.v[8] = (uint32_t)top;
-  return top >= 0;
+  r.v[8] = (uint32_t)acc;
+  return r;
 }
-// a == 0 (mod p) has no inverse: it returns 0, as the Fermat inverse does (0^(p-2) = 0), instead
-// of halving u = 0 forever.  Every step below removes at least one bit from u or v (both < 2^254),
-// so a valid input takes at most 2 x 254 outer iterations; the bound only guards the kernel.
-ZK_HD F29 f29_inv_bgcd(const F29& a_in) {
-  F29 u = f29_canon_sub<1>(a_in), v = f29_const(P29::P), x1 = f29_zero(), x2 = f29_zero();
+ZK_HD constexpr uint32_t inv_mod2_30(uint32_t a) {  // a^-1 mod 2^30, a odd (Newton doubles the good bits)
+  uint32_t x = a;
+  for (int i = 0; i < 5; i++) x *= 2u - a * x;
+  return x & (uint32_t)S30_M;
+}
+struct P30 {
+  static constexpr S30 P = s30_from29(P29::P);
+  static constexpr uint32_t INV = inv_mod2_30((uint32_t)s30_from29(P29::P).v[0]);  // p^-1 mod 2^30
+};
+struct DivTrans {
+  int32_t u, v, q, r;
+};
+// 30 divsteps on the low bits of f (odd) and g; zeta = -(delta + 1/2).  Branch-free: masks pick
+// g +- f, and the swap when delta > 0 and g is odd.
+ZK_HD int32_t divsteps30(int32_t zeta, uint32_t f, uint32_t g, DivTrans& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int i = 0; i < 30; i++) {
+    uint32_t c1 = (uint32_t)(zeta >> 31);  // delta > 0
+    const uint32_t c2 = 0u - (g & 1u);     // g odd
+    const uint32_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+    g += x & c2;
+    q += y & c2;
+    r += z & c2;
+    c1 &= c2;  // swap
+    zeta = (zeta ^ (int32_t)c1) - 1;
+    f += g & c1;
+    u += q & c1;
+    v += r & c1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t = {(int32_t)u, (int32_t)v, (int32_t)q, (int32_t)r};
+  return zeta;
+}
+// (f, g) <- t (f, g) / 2^30 (exact)
+ZK_HD void update_fg30(S30& f, S30& g, const DivTrans& t) {
+  int64_t cf = (int64_t)t.u * f.v[0] + (int64_t)t.v * g.v[0];
+  int64_t cg = (int64_t)t.q * f.v[0] + (int64_t)t.r * g.v[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    cf += (int64_t)t.u * f.v[i] + (int64_t)t.v * g.v[i];
+    cg += (int64_t)t.q * f.v[i] + (int64_t)t.r * g.v[i];
+    f.v[i - 1] = (int32_t)cf & S30_M;
+    g.v[i - 1] = (int32_t)cg & S30_M;
+    cf >>= 30;
+    cg >>= 30;
+  }
+  f.v[8] = (int32_t)cf;
+  g.v[8] = (int32_t)cg;
+}
+// (d, e) <- (t (d, e) + p (md, me)) / 2^30, md, me chosen so the division is exact; d, e stay in
+// (-2p, p)
+ZK_HD void update_de30(S30& d, S30& e, const DivTrans& t) {
+  const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+  int32_t md = (t.u & sd) + (t.v & se), me = (t.q & sd) + (t.r & se);
+  int64_t cd = (int64_t)t.u * d.v[0] + (int64_t)t.v * e.v[0];
+  int64_t ce = (int64_t)t.q * d.v[0] + (int64_t)t.r * e.v[0];
+  md -= (int32_t)((P30::INV * (uint32_t)cd + (uint32_t)md) & (uint32_t)S30_M);
+  me -= (int32_t)((P30::INV * (uint32_t)ce + (uint32_t)me) & (uint32_t)S30_M);
+  cd += (int64_t)P30::P.v[0] * md;
+  ce += (int64_t)P30::P.v[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    cd += (int64_t)t.u * d.v[i] + (int64_t)t.v * e.v[i] + (int64_t)P30::P.v[i] * md;
+    ce += (int64_t)t.q * d.v[i] + (int64_t)t.r * e.v[i] + (int64_t)P30::P.v[i] * me;
+    d.v[i - 1] = (int32_t)cd & S30_M;
+    e.v[i - 1] = (int32_t)ce & S30_M;
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d.v[8] = (int32_t)cd;
+  e.v[8] = (int32_t)ce;
+}
+// x + s p (s = 0 or +-1) with the limbs carried: 0..7 in [0, 2^30), limb 8 signed
+ZK_HD S30 s30_addp(const S30& x, int32_t s) {
+  S30 r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c += (int64_t)x.v[i] + (int64_t)s * P30::P.v[i];
+    r.v[i] = i < 8 ? (int32_t)c & S30_M : (int32_t)c;
+    c >>= 30;
+  }
+  return r;
+}
+ZK_HD F29 f29_inv_divsteps(const F29& a_in) {
+  const F29 a = f29_canon_sub<1>(a_in);
   {
     uint32_t z = 0;
 #pragma unroll
-    for (int i = 0; i < 9; i++) z |= u.v[i];
+    for (int i = 0; i < 9; i++) z |= a.v[i];
     if (z == 0) return f29_zero();
   }
-  x1.v[0] = 1;
-  const F29 P = f29_const(P29::P);
-  auto half = [&](F29& x) {  // x / 2 mod p for canonical x
-    if (!f29_even(x)) {
-      x = f29_add_lazy(x, P);
-      f29_norm(x);
-    }
-    x = f29_shr1(x);
-  };
-  int guard = 0;
+  S30 f = P30::P, g = s30_from29(a.v), d{}, e{};
+  e.v[0] = 1;
+  int32_t zeta = -1;
 #pragma unroll 1
-  while (!f29_is_one_plain(u) && !f29_is_one_plain(v) && guard++ < 2 * 261) {
-#pragma unroll 1
-    while (f29_even(u)) {
-      u = f29_shr1(u);
-      half(x1);
-    }
-#pragma unroll 1
-    while (f29_even(v)) {
-      v = f29_shr1(v);
-      half(x2);
-    }
-    F29 t;
-    if (f29_sub_plain(u, v, t)) {
-      u = t;
-      if (!f29_sub_plain(x1, x2, t)) {
-        t = f29_add_lazy(t, P);  // x1 - x2 + p (t's top limb wrapped: the sum carries it back)
-        f29_norm(t);
-      }
-      x1 = t;
-    } else {
-      f29_sub_plain(v, u, t);
-      v = t;
-      if (!f29_sub_plain(x2, x1, t)) {
-        t = f29_add_lazy(t, P);
-        f29_norm(t);
-      }
-      x2 = t;
-    }
+  for (int i = 0; i < 20; i++) {
+    DivTrans t;
+    zeta = divsteps30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    update_de30(d, e, t);
+    update_fg30(f, g, t);
   }
-  const F29 x = f29_is_one_plain(u) ? x1 : x2;  // (a R)^-1, canonical
-  return f29_canon_sub<1>(f29_mul(x, f29_const(P29Inv::R3)));
+  // f = +-1: d (in (-2p, p)) times its sign is (aR)^-1 mod p; carry it, then bring it into [0, p)
+  const int32_t neg = f.v[8] >> 31;
+  S30 x;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c += (int64_t)((d.v[i] ^ neg) - neg);
+    x.v[i] = i < 8 ? (int32_t)c & S30_M : (int32_t)c;
+    c >>= 30;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) x = s30_addp(x, x.v[8] < 0 ? 1 : 0);  // (-2p, 2p) -> [0, 2p)
+  const S30 y = s30_addp(x, -1);
+  if (y.v[8] >= 0) x = y;  // [0, p)
+  return f29_canon_sub<1>(f29_mul(f29_from30(x), f29_const(P29Inv::R3)));
 }
 
 // add-2008-s.  In: X, Y < 6p, ZZ, ZZZ < 2p (both).  U1, U2, S1, S2 < 1.08p; P = U2 + 2p - U1,

@@ -626,32 +626,32 @@ ZK_DEV QPoint<QF> quad_add(const QPoint<QF>& p, const QPoint<QF>& o, int q) {
   return r;
 }
 
-// Fq inverse on one lane by the binary extended Euclidean algorithm (field29.h, f29_inv_bgcd):
-// Montgomery 2^256 form in and out, a != 0.  The proof's last affine conversion (pi_c) sits on the
-// assembly's critical path, where Fermat's chain of ~380 dependent 32-bit products took ~0.4 ms.
-ZK_DEV Fq fq_inv_bgcd(const Fq& a) {
+// Fq inverse on one lane (f29_inv_divsteps): Montgomery 2^256 form in and out (0 -> 0).  The
+// proof's last affine conversion (pi_c) sits on the assembly's critical path.
+ZK_DEV Fq fq_inv29(const Fq& a) {
   Fq c, k = fp_zero<FqP>();
 #pragma unroll
   for (int i = 0; i < 8; i++) c.v[i] = P29::C261[i];
   const Fq a261 = fp_mul(a, c);  // A 2^256 -> A 2^261 (the 29-bit engine's Montgomery domain)
   Fq r;
-  f29_unpack(r.v, f29_inv_bgcd(f29_pack(a261.v)));  // A^-1 2^261, canonical
+  const F29 a29 = f29_pack(a261.v);
+  f29_unpack(r.v, f29_inv_divsteps(a29));  // A^-1 2^261, canonical
   k.v[7] = 1u << 27;  // 2^251: x 2^261 -> x 2^256
   return fp_mul(r, k);
 }
 
-ZK_DEV Affine<FqOps> g1_to_affine_bgcd(const G1P& p) {
+ZK_DEV Affine<FqOps> g1_to_affine29(const G1P& p) {
   if (xyzz_is_inf<FqOps>(p)) return {fp_zero<FqP>(), fp_zero<FqP>()};
-  const Fq iZZZ = fq_inv_bgcd(p.ZZZ);
+  const Fq iZZZ = fq_inv29(p.ZZZ);
   const Fq iZ = fp_mul(p.ZZ, iZZZ);  // ZZ / ZZZ = 1 / Z
   return {fp_mul(p.X, fp_mul(iZ, iZ)), fp_mul(p.Y, iZZZ)};
 }
 
 // G2 likewise: (a0 + a1 u)^-1 = (a0 - a1 u) / (a0^2 + a1^2), one Fq inverse
-ZK_DEV Affine<Fq2Ops> g2_to_affine_bgcd(const G2P& p) {
+ZK_DEV Affine<Fq2Ops> g2_to_affine29(const G2P& p) {
   if (xyzz_is_inf<Fq2Ops>(p)) return {f2_zero(), f2_zero()};
   const Fq2& z = p.ZZZ;
-  const Fq ni = fq_inv_bgcd(fp_add(fp_sqr(z.c0), fp_sqr(z.c1)));
+  const Fq ni = fq_inv29(fp_add(fp_sqr(z.c0), fp_sqr(z.c1)));
   const Fq2 iZZZ = {fp_mul(z.c0, ni), fp_neg(fp_mul(z.c1, ni))};
   const Fq2 iZ = f2_mul(p.ZZ, iZZZ);
   return {f2_mul(p.X, f2_sqr(iZ)), f2_mul(p.Y, iZZZ)};
@@ -736,23 +736,32 @@ ZK_DEV G1Q glv_row_mul(const G1P* __restrict__ res, const GlvScalar* __restrict_
   return {Row29::to(acc.X), Row29::to(acc.Y), Row29::to(acc.ZZ), Row29::to(acc.ZZZ)};
 }
 
-constexpr int ASM_THREADS = 64 * 6;    // k_assemble: four chain waves + C' + H / pi_a, pi_b
-constexpr int ASM_T_THREADS = 64 * 5;  // k_assemble_t: four chain waves + pi_a
+constexpr int ASM_THREADS = 64 * 5;    // k_assemble: four chain waves + the C' + H wave
+constexpr int ASM_T_THREADS = 64 * 4;  // k_assemble_t: four chain waves
 
 struct AsmLds {
   uint32_t rtab[4][8 * 4 * 64];  // the chains' tables
   G1Q part[6];                   // the four products, C' + H, then the sum of parts 2 + 3
 };
 
+// After the chains (part[0..3] in LDS, a barrier behind): quads 0 and 1 of wave 0 add parts 0 + 1
+// and 2 + 3 in one pass (the same instructions, operands by quad); quad 1 leaves its sum in part[5]
+// for the caller's next barrier.  -> quad 0's sum of parts 0 + 1.
+ZK_DEV G1Q asm_pair_sums(AsmLds& sh, int g, int q) {
+  const int h = g & 1;
+  const G1Q s = quad_add<Q29>(sh.part[2 * h], sh.part[2 * h + 1], q);
+  if (g == 1 && q == 0) sh.part[5] = s;
+  return s;
+}
+
 // Proof assembly, one block (replaces snarkjs's final
 // pi_c = C + H + s*A + r*B1 - rs*delta; the rs*delta term is already in the C MSM):
-//   waves 0..3: the four GLV halves (glv_row_mul) -> part[0..3];
-//   wave 4: C' + H meanwhile (quad 0), and pi_a affine (lane 32) -> proof[0..15];
-//   wave 5, lane 0: pi_b affine -> proof[16..47];
-//   then quads 0, 1 of wave 0 sum the parts and quad 0 adds C' + H and writes pi_c (one inversion)
-//   -> proof[48..63]
+//   waves 0..3: the four GLV halves (glv_row_mul) -> part[0..3]; wave 4: C' + H meanwhile;
+//   then wave 0 sums the parts (asm_pair_sums, then quad 0 adds 2 + 3 and C' + H) and writes pi_c
+//   -> proof[48..63], while lane 0 of wave 1 / wave 2 converts pi_a / pi_b -> proof[0..15] /
+//   proof[16..47] -- after the chains, so that no inversion shares a SIMD with a chain
 // The critical path is 132 doublings + 33 additions on the chains, 3 quad additions and one
-// inversion; the quad operations run in the 29-bit engine (Q29), every inversion is a binary GCD.
+// inversion; the quad operations run in the 29-bit engine (Q29), the inversions by divsteps.
 __global__ void __launch_bounds__(ASM_THREADS) k_assemble(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                           const GlvScalar* __restrict__ ks, uint32_t* __restrict__ proof) {
   ZK_WT(WT_ASSEMBLE);
@@ -768,25 +777,21 @@ __global__ void __launch_bounds__(ASM_THREADS) k_assemble(const G1P* __restrict_
   if (wave < 4) {
     const G1Q acc = glv_row_mul(res, ks, sh.rtab[wave], wave);
     if (lane == 0) sh.part[wave] = acc;
-  } else if (wave == 4 && g == 0) {  // C' + H, off the critical path
+  } else if (g == 0) {  // wave 4: C' + H
     const G1Q c = quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q);
     if (q == 0) sh.part[4] = c;
-  } else if (wave == 4 && lane == 32) {
-    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
-  } else if (wave == 5 && lane == 0) {
-    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
   }
   __syncthreads();
-  if (wave == 0 && g == 1) {
-    const G1Q t = quad_add<Q29>(sh.part[2], sh.part[3], q);
-    if (q == 0) sh.part[5] = t;
-  }
   G1Q t01 = qp_inf<Q29>();
-  if (wave == 0 && g == 0) t01 = quad_add<Q29>(sh.part[0], sh.part[1], q);
+  if (wave == 0) t01 = asm_pair_sums(sh, g, q);
   __syncthreads();
   if (wave == 0 && g == 0) {
     const G1Q C = quad_add<Q29>(quad_add<Q29>(t01, sh.part[5], q), sh.part[4], q);
-    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine29(g1q_to(C)), proof + 48);
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<FqOps>(g1_to_affine29(res[0]), proof);
+  } else if (wave == 2 && lane == 0) {
+    store_affine_std<Fq2Ops>(g2_to_affine29(resB2[0]), proof + 16);
   }
 }
 
@@ -803,23 +808,17 @@ __global__ void __launch_bounds__(ASM_T_THREADS) k_assemble_t(G1P* __restrict__ 
   __shared__ AsmLds sh;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int g = lane >> 2, q = lane & 3;
-  if (wave < 4) {
-    const G1Q acc = glv_row_mul(res, ks, sh.rtab[wave], wave);
-    if (lane == 0) sh.part[wave] = acc;
-  } else if (wave == 4 && lane == 0) {
-    store_affine_std<FqOps>(g1_to_affine_bgcd(res[0]), proof);
-  }
+  const G1Q acc = glv_row_mul(res, ks, sh.rtab[wave], wave);
+  if (lane == 0) sh.part[wave] = acc;
   __syncthreads();
-  if (wave == 0 && g == 1) {
-    const G1Q t = quad_add<Q29>(sh.part[2], sh.part[3], q);
-    if (q == 0) sh.part[5] = t;
-  }
   G1Q t01 = qp_inf<Q29>();
-  if (wave == 0 && g == 0) t01 = quad_add<Q29>(sh.part[0], sh.part[1], q);
+  if (wave == 0) t01 = asm_pair_sums(sh, g, q);
   __syncthreads();
   if (wave == 0 && g == 0) {
     const G1Q T = quad_add<Q29>(t01, sh.part[5], q);
     if (q == 0) res[4] = g1q_to(T);
+  } else if (wave == 1 && lane == 0) {
+    store_affine_std<FqOps>(g1_to_affine29(res[0]), proof);
   }
 }
 
@@ -831,9 +830,9 @@ __global__ void __launch_bounds__(128) k_assemble_c(const G1P* __restrict__ res,
   const int g = lane >> 2, q = lane & 3;
   if (wave == 0 && g == 0) {
     const G1Q C = quad_add<Q29>(quad_add<Q29>(g1q_from(res[2]), g1q_from(res[3]), q), g1q_from(res[4]), q);
-    if (q == 0) store_affine_std<FqOps>(g1_to_affine_bgcd(g1q_to(C)), proof + 48);
+    if (q == 0) store_affine_std<FqOps>(g1_to_affine29(g1q_to(C)), proof + 48);
   } else if (wave == 1 && lane == 0) {
-    store_affine_std<Fq2Ops>(g2_to_affine_bgcd(resB2[0]), proof + 16);
+    store_affine_std<Fq2Ops>(g2_to_affine29(resB2[0]), proof + 16);
   }
 }
 
