@@ -80,12 +80,11 @@ def test_metric_key_by_path_equals_key_by_bytes(metric, gpu_ctx, tmp_path):
         k2.close()
 
 
-def test_metric_latency_schedule_graph_replay(metric):
-    """A batch of one takes the latency schedule (enqueue_proof_lowlat; with ZKFL_GRAPH=2 its
-    per-stream segments are captured as graphs on a witness address's second proof, run_segment).
-    Repeated latency-schedule proofs of one resident witness equal the one-stream batch proof
-    of the same (witness, r, s) -- which test_metric_proof_and_parts_bit_exact_vs_c_oracle pins to
-    the C oracle."""
+def test_metric_latency_schedule_equals_batch(metric):
+    """A batch of one takes the latency schedule (enqueue_proof_lowlat: three streams, A / B1 and
+    B2 beside ABC / NTT / C + H, k_assemble_t + k_assemble_c).  Repeated latency-schedule proofs
+    of one resident witness equal the one-stream batch proof of the same (witness, r, s) -- which
+    test_metric_proof_and_parts_bit_exact_vs_c_oracle pins to the C oracle."""
     _, _, key, _, wts = metric
     w = key.upload(wts[1])
     try:

@@ -1051,12 +1051,6 @@ struct ProofSlot {
   // B2 shares B1's digit sort, so its tail counts with B1's nnz (g2t.nnz == g1t[1].nnz, owned
   // by g1t[1]): no copy between them
   bool nnz_alias = false;
-  // the latency schedule's per-stream segments, each captured as its own one-stream graph
-  // (enqueue_proof_lowlat): index = segment, entries per witness address
-  std::vector<Graph> seg_graphs[4];
-  // witness addresses seen once: a graph is captured on an address's second proof, so a one-off
-  // proof (a CLI run, a freshly uploaded witness) pays no capture
-  std::vector<const Fr*> seen;
   bool busy = false;
   int index = 0;                  // position among its key's slots
   size_t job = 0;                 // index of the in-flight proof in its batch
@@ -1154,13 +1148,6 @@ void slot_release(ProofSlot* s) {
     if (gr.g) (void)hipGraphDestroy(gr.g);
   }
   s->graphs.clear();
-  for (auto& v : s->seg_graphs) {
-    for (auto& gr : v) {
-      if (gr.ex) (void)hipGraphExecDestroy(gr.ex);
-      if (gr.g) (void)hipGraphDestroy(gr.g);
-    }
-    v.clear();
-  }
   for (hipEvent_t e : {s->ev_ready, s->ev_b2, s->ev_done, s->ev_lat[0], s->ev_lat[1], s->ev_lat[2]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : {s->st_main, s->st_g2, s->st_lat[0], s->st_lat[1]})
@@ -1418,150 +1405,27 @@ bool small_key_fast_wsum(const zkfl_key* k) {
 }
 
 // One proof alone (a batch of one: the CLI's `groth16 prove`, the API's prove): its latency is
-// the metric, and the GPU is mostly idle along the one-stream chain, so independent stages run on
-// side streams:
-//   main : r, s, tails reset, A (sort + accumulate), B (sort into its own scratch + B1) [ev B],
-//          ABC, coset NTT, join, C + H (sort + accumulate), its tail, wait(B2, T), k_assemble_c,
-//          proof D2H [ev_done]
-//   lat0 : wait(ev B) B2 (from B's pairs) + its tail [ev B2]
-//   lat1 : wait(ev B) the tails of A and B1, k_assemble_t (T = s pi_A + r B1, pi_a) [ev T]
-// Same proof bytes as the one-stream schedule (k_assemble_t / _c form the same points).
-// ZKFL_GRAPH (default 1): graph replay of the one-stream proof chain (0: launch kernel by kernel;
-// 2: also the latency schedule's stream segments)
+// the metric, and the GPU is mostly idle along the one-stream chain, so the two long chains start
+// at once on streams of their own:
+//   main : r, s, tails reset [ev_ready] ABC, coset NTT, join, C + H (sort + accumulate), its tail,
+//          wait(B2, T), k_assemble_c, proof D2H [ev_done]
+//   lat0 : wait(ev_ready) B sort (own scratch) [ev B sorted] B2 + its tail [ev B2]
+//   lat1 : wait(ev B sorted) B1, A (sort into its own scratch + accumulate), the tails of A and
+//          B1, k_assemble_t (T = s pi_A + r B1, pi_a) [ev T]
+// Same proof bytes as the one-stream schedule (k_assemble_t / _c form the same points).  The
+// round-4 schedule ran A and B1 on the main stream ahead of ABC / NTT (4.10 vs 4.16 ms then); with
+// the row assembly and the divsteps inversions the overlap wins: 3.586 vs 3.712 ms, 3 same-box
+// alternations (profiles/r06_ab_lowlat2.log), and the round-4 one was deleted, with its
+// per-segment graph replay (ZKFL_GRAPH=2: no gain, profiles/r04_ab_lowlat_seg_graphs.log).
+
+// ZKFL_GRAPH (default 1): graph replay of the one-stream proof chain (0: launch kernel by kernel)
 int graph_mode() {
   static const int m = getenv("ZKFL_GRAPH") ? atoi(getenv("ZKFL_GRAPH")) : 1;
   return m;
 }
 
-// One segment of a schedule on one stream: captured once per (slot, segment, witness address)
-// as a one-stream graph and replayed, or enqueued directly (graphs off, or profiling).  body()
-// enqueues on `st` only; the segments' cross-stream order stays in events recorded between them.
-// true once d_w has been proved on this slot before (it is then worth a graph)
-bool seen_before(ProofSlot* s, const Fr* d_w) {
-  for (const Fr* x : s->seen)
-    if (x == d_w) return true;
-  if (s->seen.size() >= 32) s->seen.erase(s->seen.begin());
-  s->seen.push_back(d_w);
-  return false;
-}
-
-template <class Body>
-int run_segment(ProofSlot* s, int seg, const Fr* d_w, hipStream_t st, bool use_graph, Body body) {
-  if (!use_graph) return body();
-  std::vector<ProofSlot::Graph>& cache = s->seg_graphs[seg];
-  ProofSlot::Graph* gr = nullptr;
-  for (auto& x : cache)
-    if (x.w == d_w) gr = &x;
-  if (!gr) {
-    if (cache.size() >= 8) {
-      if (cache.front().ex) (void)hipGraphExecDestroy(cache.front().ex);
-      if (cache.front().g) (void)hipGraphDestroy(cache.front().g);
-      cache.erase(cache.begin());
-    }
-    ProofSlot::Graph ng;
-    ng.w = d_w;
-    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "begin capture");
-    const int rc = body();
-    const hipError_t ec = hipStreamEndCapture(st, &ng.g);
-    if (rc) {
-      if (ng.g) (void)hipGraphDestroy(ng.g);
-      return rc;
-    }
-    HIP_TRY(ec, "end capture");
-    const hipError_t ei = hipGraphInstantiate(&ng.ex, ng.g, nullptr, nullptr, 0);
-    if (ei != hipSuccess) {
-      (void)hipGraphDestroy(ng.g);
-      return hip_fail(ei, "graph instantiate");
-    }
-    cache.push_back(ng);
-    gr = &cache.back();
-  }
-  HIP_TRY(hipGraphLaunch(gr->ex, st), "graph launch");
-  return ZKFL_OK;
-}
-
+// (the schedule above)
 int enqueue_proof_lowlat(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w) {
-  Profiler* prof = &ctx->prof;
-  hipStream_t st = s->st_main;
-  for (int i = 0; i < 2; i++)
-    if (!s->st_lat[i]) HIP_TRY(hipStreamCreateWithFlags(&s->st_lat[i], hipStreamNonBlocking), "stream");
-  for (int i = 0; i < 3; i++)
-    if (!s->ev_lat[i]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lat[i], hipEventDisableTiming), "event");
-  if (!s->g1s_b.keys_out) HIP_TRY(msm_scratch_alloc_g1(s->g1s_b, k->bB1.n, k->msm_c, st), "B sort scratch");
-  hipStream_t sb = s->st_lat[0], sa = s->st_lat[1];
-  hipEvent_t ev_b = s->ev_lat[0], ev_b2 = s->ev_lat[1], ev_t = s->ev_lat[2];
-  const uint32_t* W = (const uint32_t*)d_w;
-  const uint32_t* E = (const uint32_t*)s->extra;
-  MsmTail<FqOps>* tails[3] = {&s->g1t[0], &s->g1t[1], &s->g1t[2]};
-  MsmTail<Fq2Ops>* t2 = &s->g2t;
-  G2P* o2 = s->resB2;
-  // ZKFL_GRAPH=2: each stream's stretch between two events is one segment, replayed from its own
-  // one-stream graph.  Measured no gain (median 4.128 vs 4.125 ms over 3 same-box alternations,
-  // profiles/r04_ab_lowlat_seg_graphs.log): the gaps on the critical path are not launch cost, so
-  // it stays an A/B knob.  (One graph for the whole multi-stream schedule ran ~7x slower.)
-  const bool seg_graphs = graph_mode() >= 2 && !prof->on && seen_before(s, d_w);
-  int rc = run_segment(s, 0, d_w, st, seg_graphs, [&]() -> int {  // (tails emptied by k_proof_start)
-    HIP_TRY(msm_accumulate_g1(k->bA, s->g1s, s->g1t[0], W, E, st, prof, "msm_accumulate_g1"), "msm A");
-    HIP_TRY(msm_sort_g1(k->bB1, s->g1s_b, s->g1t[1].nnz, W, E, st), "msm B1 sort");
-    HIP_TRY(msm_accumulate_sorted_g1(k->bB1, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g1t[1], st, prof,
-                                     "msm_accumulate_g1"), "msm B1");
-    if (!s->nnz_alias)
-      HIP_TRY(hipMemcpyAsync(s->g2t.nnz, s->g1t[1].nnz, sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "nnz");
-    return ZKFL_OK;
-  });
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(ev_b, st), "event");
-  // lat0: B2 and its tail
-  HIP_TRY(hipStreamWaitEvent(sb, ev_b, 0), "wait");
-  rc = run_segment(s, 1, d_w, sb, seg_graphs, [&]() -> int {
-    HIP_TRY(msm_accumulate_sorted_g2(k->bB2, s->g1s_b.keys_out, s->g1s_b.vals_out, s->g2t, sb, prof,
-                                     "msm_accumulate_g2"), "msm B2");
-    HIP_TRY(msm_tails_g2(&t2, &o2, 1, sb, lowlat_fast_wsum()), "msm B2 tail");
-    return ZKFL_OK;
-  });
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(ev_b2, sb), "event");
-  // lat1: the tails of A and B1, then T = s pi_A + r B1 and pi_a
-  HIP_TRY(hipStreamWaitEvent(sa, ev_b, 0), "wait");
-  rc = run_segment(s, 2, d_w, sa, seg_graphs, [&]() -> int {
-    G1P* outs[2] = {s->res + 0, s->res + 1};
-    HIP_TRY(msm_tails_g1(tails, outs, 2, sa, lowlat_fast_wsum()), "msm tails A, B1");
-    hipLaunchKernelGGL(k_assemble_t, dim3(1), dim3(ASM_T_THREADS), 0, sa, s->res,
-                       reinterpret_cast<const GlvScalar*>(reinterpret_cast<const uint8_t*>(s->d_rs) + 64), proof_out(s));
-    return ZKFL_OK;
-  });
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(ev_t, sa), "event");
-  // main: ABC / NTT / h, C + H and its tail, then pi_c and pi_b
-  rc = run_segment(s, 3, d_w, st, seg_graphs, [&]() -> int {
-    const int r = enqueue_abc_ntt(k, s, d_w, st, prof);
-    if (r) return r;
-    HIP_TRY(msm_accumulate_g1(k->bCH, s->g1s, s->g1t[2], W, (const uint32_t*)s->h, st, prof, "msm_accumulate_g1"),
-            "msm C+H");
-    G1P* out2 = s->res + 2;
-    HIP_TRY(msm_tails_g1(&tails[2], &out2, 1, st, lowlat_fast_wsum()), "msm tail C+H");
-    return ZKFL_OK;
-  });
-  if (rc) return rc;
-  HIP_TRY(hipStreamWaitEvent(st, ev_b2, 0), "wait");
-  HIP_TRY(hipStreamWaitEvent(st, ev_t, 0), "wait");
-  const int pa = prof->begin("assemble", st);
-  hipLaunchKernelGGL(k_assemble_c, dim3(1), dim3(128), 0, st, s->res, s->resB2, proof_out(s));
-  prof->end(pa, st, 1.0);
-  return ZKFL_OK;
-}
-
-// The overlapped low-latency schedule (ZKFL_LOWLAT=2): the witness-scalar MSMs no longer precede
-// ABC / NTT on the main stream.  The wave timeline of the one-proof chain (tools/wtrace.py
-// --isolated) had the C + H chain critical -- ABC, NTT, join, its sort, accumulation and tail
-// (~4 ms) started only after A and B1 (~1.2 ms) -- and B2's chain (sort, G2 accumulation, G2
-// tail: ~3.4 ms) second.  Here both long chains start at once:
-//   main : r, s, tails reset [ev_ready] ABC, coset NTT, join, C + H (sort + accumulate), its tail,
-//          wait(B2, T), k_assemble_c, proof D2H [ev_done]
-//   lat0 : wait(ev_ready) B sort (own scratch) [ev B sorted] B2 + its tail [ev B2]
-//   lat1 : wait(ev B sorted) B1, A (sort into its own scratch + accumulate), the tails of A and
-//          B1, k_assemble_t [ev T]
-int enqueue_proof_lowlat2(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w) {
   Profiler* prof = &ctx->prof;
   hipStream_t st = s->st_main;
   for (int i = 0; i < 2; i++)
@@ -1659,7 +1523,7 @@ int enqueue_proof_body(zkfl_ctx* ctx, zkfl_key* k, ProofSlot* s, const Fr* d_w, 
                        reinterpret_cast<uint32_t*>(s->d_rs), s->extra, plain == 1, res3, ps);
   }
   if (lowlat_path) {
-    const int rc = lowlat == 2 ? enqueue_proof_lowlat2(ctx, k, s, d_w) : enqueue_proof_lowlat(ctx, k, s, d_w);
+    const int rc = enqueue_proof_lowlat(ctx, k, s, d_w);
     if (rc) return rc;
     prof->end(pp, st, 1.0);
     return ZKFL_OK;
@@ -1911,8 +1775,7 @@ int run_jobs(zkfl_ctx* ctx, size_t n, GetJob job) {
     size_t issued = 0;  // proofs issued in this batch
   };
   std::vector<PerKey> cursor;
-  // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain,
-  // 1: A and B before ABC / NTT, 2: overlapped)
+  // a batch of one proof runs the low-latency schedule (ZKFL_LOWLAT=0: the one-stream chain)
   static const int lowlat = getenv("ZKFL_LOWLAT") ? atoi(getenv("ZKFL_LOWLAT")) : 1;
   // A/B knob: ZKFL_LOWLAT_BATCH=1 runs every proof of a batch on the low-latency schedule
   static const bool lowlat_batch = getenv("ZKFL_LOWLAT_BATCH") && atoi(getenv("ZKFL_LOWLAT_BATCH")) != 0;
