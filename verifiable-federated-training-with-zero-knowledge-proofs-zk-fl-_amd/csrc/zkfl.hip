@@ -45,6 +45,7 @@
 #include "msm_api.h"
 #include "ntt.h"
 #include "pairing.h"
+#include "row29.h"
 #include "prof.h"
 #include "setup.h"
 #include "verify.h"
@@ -346,26 +347,6 @@ ZK_DEV void pick4_words(int q, const uint32_t (&a)[N], const uint32_t (&b)[N], c
   for (int i = 0; i < N; i++) r[i] = (q & 2) ? ((q & 1) ? d[i] : c[i]) : ((q & 1) ? b[i] : a[i]);
 }
 
-// k p (k < 64) in nine 29-bit limbs: normalized, or borrowed by one for a + k p - b (every lower
-// limb raised by 2^29, the next lowered by one, so no limb goes negative for a normalized b)
-struct Limbs9 {
-  uint32_t v[9];
-};
-__host__ __device__ constexpr Limbs9 p29_times(uint32_t k, bool borrowed) {
-  Limbs9 r{};
-  uint64_t c = 0;
-  for (int i = 0; i < 9; i++) {
-    c += (uint64_t)k * P29::P[i];
-    r.v[i] = i < 8 ? (uint32_t)(c & P29::MASK) : (uint32_t)c;
-    c >>= 29;
-  }
-  if (borrowed) {
-    for (int i = 0; i < 8; i++) r.v[i] += (1u << 29) - (i ? 1u : 0u);
-    r.v[8] -= 1u;
-  }
-  return r;
-}
-
 struct Q29 {
   using T = F29;
   // ZKFL_Q29_ACC: accumulators per product column of the assembly's quad operations (an A/B knob:
@@ -436,113 +417,8 @@ struct Q29 {
   }
 };
 
-// ---------------------------------------------------------------------------
-// Row policy (glv_row_mul): one value per 16-lane row of a wave, lane j of the row holding limb j
-// of the nine 29-bit limbs (lanes 9..15 zero), same Montgomery domain (2^261) and the same integer
-// results as Q29.  A product is spread over its row: limb i of a is broadcast by DPP row_newbcast,
-// each lane accumulates column i + j in 64 bits, and the row shifts down one lane per reduction
-// step (DPP row_shl, lane 0's carry kept): 18 v_mad_u64_u32 per lane instead of 162, so one wave
-// evaluates a level's four products (one per row) at ~1/9 of the quad's multiply issue.  Products
-// cross rows by the gfx950 row swaps (bcast<K>).  Limbs are lazy: lanes 0..7 below 2^29 + 2^7 (one or two
-// carry-save steps per operation), lane 8 the exact top; the integer bounds are Q29's.
-// ---------------------------------------------------------------------------
-ZK_DEV uint32_t row_j() { return __lane_id() & 15u; }
-template <int CTRL, bool BOUND>
-ZK_DEV uint32_t row_dpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, BOUND);
-}
-template <int I>
-ZK_DEV uint32_t row_limb(uint32_t v) { return row_dpp<0x150 + I, false>(v); }  // row_newbcast:I
-ZK_DEV uint32_t row_up(uint32_t v) { return row_dpp<0x101, true>(v); }         // row_shl:1, lane 15 <- 0
-ZK_DEV uint32_t row_down(uint32_t v) { return row_dpp<0x111, true>(v); }       // row_shr:1, lane 0 <- 0
-ZK_DEV uint32_t limb_at(const Limbs9& c, uint32_t j) {  // c.v[j] (0 for j > 8)
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 9; i++) r = j == (uint32_t)i ? c.v[i] : r;
-  return r;
-}
-// k p + 2^31 (limbs 0..7) - 4 (limbs 1..8): a + this - b keeps every lane in [0, 2^32) for lazy b
-// (limbs < 2^29 + 2^7); the top limb may wrap below zero and is made whole by the carries
-__host__ __device__ constexpr Limbs9 row_kp(uint32_t k) {
-  Limbs9 r = p29_times(k, false);
-  for (int i = 0; i < 9; i++) r.v[i] += (i < 8 ? 0x80000000u : 0u) - (i > 0 ? 4u : 0u);
-  return r;
-}
-struct Row29 {
-  struct T {
-    uint32_t v;
-  };
-  // one carry-save step: lanes 0..7 keep 29 bits and pass the rest up one lane
-  static ZK_DEV uint32_t carry(uint32_t x) {
-    const bool top = row_j() >= 8;
-    const uint32_t h = top ? 0u : x >> 29;
-    return (top ? x : x & P29::MASK) + row_down(h);
-  }
-  static ZK_DEV T mul(const T& a, const T& b) {
-    const uint32_t j = row_j();
-    const uint32_t pj = limb_at(p29_times(1, false), j);
-    const uint32_t ai[9] = {row_limb<0>(a.v), row_limb<1>(a.v), row_limb<2>(a.v), row_limb<3>(a.v), row_limb<4>(a.v),
-                            row_limb<5>(a.v), row_limb<6>(a.v), row_limb<7>(a.v), row_limb<8>(a.v)};
-    uint64_t t = 0;  // lane j: column i + j
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      t += (uint64_t)ai[i] * b.v;
-      const uint32_t m = (row_limb<0>((uint32_t)t) * P29::NINV) & P29::MASK;
-      t += (uint64_t)m * pj;  // lane 0: column i is now 0 mod 2^29
-      // shift down one lane; lane 0 adds its own carry (t >> 29), as 32-bit add / add-with-carry
-      const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-      const uint32_t clo = j == 0 ? __builtin_amdgcn_alignbit(hi, lo, 29) : 0u, chi = j == 0 ? hi >> 29 : 0u;
-      const uint32_t nlo = row_up(lo) + clo;
-      const uint32_t nhi = row_up(hi) + chi + (nlo < clo ? 1u : 0u);
-      t = ((uint64_t)nhi << 32) | nlo;
-    }
-    // lanes 0..8: columns 9..17 (< 2^63); two carry-save steps -> limbs < 2^29 + 2^7
-    const bool top = j >= 8;
-    const uint64_t h = top ? 0 : t >> 29;
-    const uint64_t x = (top ? t : t & P29::MASK) + (((uint64_t)row_down((uint32_t)(h >> 32)) << 32) | row_down((uint32_t)h));
-    const uint32_t h2 = top ? 0u : (uint32_t)(x >> 29);
-    return {(top ? (uint32_t)x : (uint32_t)x & P29::MASK) + row_down(h2)};
-  }
-  static ZK_DEV T add(const T& a, const T& b) { return {carry(a.v + b.v)}; }
-  template <int K>
-  static ZK_DEV T sub(const T& a, const T& b) {
-    constexpr Limbs9 k = row_kp(K);
-    return {carry(a.v + limb_at(k, row_j()) - b.v)};
-  }
-  static ZK_DEV T dbl(const T& a) { return add(a, a); }
-  static ZK_DEV T zero() { return {0u}; }
-  static ZK_DEV T one() {
-    constexpr Limbs9 o{{P29::ONE[0], P29::ONE[1], P29::ONE[2], P29::ONE[3], P29::ONE[4], P29::ONE[5], P29::ONE[6],
-                        P29::ONE[7], P29::ONE[8]}};
-    return {limb_at(o, row_j())};
-  }
-  // row K's value to every row: v_permlane16_swap of v with itself gives rows (0, 0, 2, 2) and
-  // (1, 1, 3, 3), v_permlane32_swap of either with itself rows (k, k, k, k) and (k + 2, ...): three
-  // VALU swaps serve all four K (the formulas' bcast<K> of one product share them)
-  template <int K>
-  static ZK_DEV T bcast(const T& v) {
-    const auto s = __builtin_amdgcn_permlane16_swap(v.v, v.v, false, false);
-    const uint32_t e = (K & 1) ? s[1] : s[0];
-    const auto u = __builtin_amdgcn_permlane32_swap(e, e, false, false);
-    return {(K & 2) ? u[1] : u[0]};
-  }
-  static ZK_DEV T pick4(int q, T a, T b, T c, T d) { return {(q & 2) ? ((q & 1) ? d.v : c.v) : ((q & 1) ? b.v : a.v)}; }
-  // a full value (every lane) -> its row form, and back (row 0, normalized limbs)
-  static ZK_DEV T from(const F29& x) {
-    const uint32_t j = row_j();
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < 9; i++) r = j == (uint32_t)i ? x.v[i] : r;
-    return {r};
-  }
-  static ZK_DEV F29 to(const T& x) {
-    F29 r;
-#pragma unroll
-    for (int i = 0; i < 9; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.v, i);
-    f29_norm(r);
-    return r;
-  }
-};
+// The row policy of the GLV chains (glv_row_mul): row29.h over Fq
+using Row29 = RowF<P29>;
 
 template <class QF>
 struct QPoint {
