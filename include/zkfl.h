@@ -169,6 +169,13 @@ int zkfl_debug_prove_parts(zkfl_ctx* ctx, zkfl_key* key, const uint8_t* wtns, si
  * k = k1 + k2 * lambda (mod r), |k_i| < 2^128 (csrc/glv.h; tests/test_abi.py checks it). */
 int zkfl_debug_glv_split(const uint8_t k[32], uint8_t out[40]);
 
+/* The assembly's scalar multiplication on the device (parity hook): out[i] = k_i * P_i for n pairs,
+ * P_i affine std (64 B, (0, 0) = infinity), k_i 32 B std < r, out affine std (infinity = zeros) --
+ * the GLV halves of k_i as two row-distributed chains, summed, affine by the divsteps inverse, as
+ * k_assemble computes s pi_A + r B1 (no reference counterpart: snarkjs's G1.timesFr inside
+ * groth16_prove). */
+int zkfl_debug_g1_glv_mul(zkfl_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t* out);
+
 /* Wave-level kernel timeline (measurement only; libraries built with -DZK_WTRACE=1, otherwise every
  * op returns ZKFL_E_ARG).  op 1: start recording into a fresh device buffer of `cap` records (any
  * earlier one is freed); op 2: wait for the device, stop recording, copy min(count, cap) records of

@@ -52,6 +52,30 @@ def test_gen_mul_g1_g2_match_oracle(gpu_ctx):
 
 
 # ---------------------------------------------------------------------------
+# the assembly's scalar multiplications (s pi_A + r B1 in k_assemble): GLV halves as row-distributed
+# chains, the parts summed, affine by the divsteps inverse
+# ---------------------------------------------------------------------------
+def test_assembly_glv_mul_matches_oracle(gpu_ctx):
+    """k P through the assembly's own machinery (zkfl_debug_g1_glv_mul) against the oracle's
+    double-and-add: edge scalars (0, 1, 2, r - 1, lambda, 2^128 +- 1, digits that carry into the top
+    window, scalars whose GLV halves are negative or zero), the point at infinity, P = -G and seeded
+    random points and scalars."""
+    rnd = random.Random(23)
+    lam = 0xb3c4d79d41a917585bfc41088d8daaa78b17ea66b99c90dd
+    ks = [0, 1, 2, 3, 8, 9, 16, R - 1, R - 2, lam, R - lam, (1 << 128) - 1, 1 << 128, (1 << 128) + 1,
+          int("8" * 32, 16), int("9" * 32, 16) % R, (1 << 253) + 7, R // 2]
+    ks += [rnd.randrange(R) for _ in range(46)]
+    pts = [bn.mul(bn.G1_GEN, rnd.randrange(1, R)) for _ in ks]
+    pts[3] = None                       # infinity
+    pts[4] = bn.neg(bn.G1_GEN)          # -G
+    pts[5] = bn.G1_GEN
+    out = gpu_ctx.g1_glv_mul(b"".join(bn.g1_to_bytes_std(p) for p in pts), _scal(ks))
+    for i, (p, k) in enumerate(zip(pts, ks)):
+        want = None if p is None else bn.mul(p, k)
+        assert _g1_std(out[64 * i:64 * i + 64]) == want, (i, k)
+
+
+# ---------------------------------------------------------------------------
 # NTT (odd-coset shift of snarkjs groth16_prove)
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("logn", [1, 2, 5, 10, 11, 13])

@@ -698,6 +698,39 @@ __global__ void __launch_bounds__(ASM_T_THREADS) k_assemble_t(G1P* __restrict__ 
   }
 }
 
+// Parity hook for the assembly's scalar multiplications (zkfl_debug_g1_glv_mul): block b computes
+// k_b P_b as k_assemble computes s pi_A' -- two row chains (glv_row_mul over (k1, P) and
+// (k2, phi(P)), the GLV halves of k), their sum by a quad addition, affine by the divsteps inverse.
+// pts: affine std (x, y), (0, 0) = infinity; out: affine std, infinity as zeros.
+__global__ void __launch_bounds__(128) k_debug_glv_mul(const uint32_t* __restrict__ pts,
+                                                       const GlvScalar* __restrict__ ks, uint32_t* __restrict__ out) {
+  const uint32_t* pa = pts + 16 * blockIdx.x;
+  ks += 2 * blockIdx.x;
+  out += 16 * blockIdx.x;
+  __shared__ uint32_t rtab[2][8 * 4 * 64];
+  __shared__ G1Q part[2];
+  __shared__ G1P P;
+  if (threadIdx.x == 0) {
+    Fq x, y;
+    uint32_t z = 0;
+    for (int i = 0; i < 8; i++) {
+      x.v[i] = pa[i];
+      y.v[i] = pa[8 + i];
+      z |= x.v[i] | y.v[i];
+    }
+    P = z ? G1P{fp_to_mont(x), fp_to_mont(y), fp_one<FqP>(), fp_one<FqP>()} : xyzz_inf<FqOps>();
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const G1Q acc = glv_row_mul(&P, ks, rtab[wave], wave);
+  if (lane == 0) part[wave] = acc;
+  __syncthreads();
+  if (wave == 0 && lane < 4) {
+    const G1Q S = quad_add<Q29>(part[0], part[1], lane & 3);
+    if (lane == 0) store_affine_std<FqOps>(g1_to_affine29(g1q_to(S)), out);
+  }
+}
+
 __global__ void __launch_bounds__(128) k_assemble_c(const G1P* __restrict__ res, const G2P* __restrict__ resB2,
                                                     uint32_t* __restrict__ proof) {
   ZK_WT(WT_ASSEMBLE);
@@ -1897,6 +1930,39 @@ int zkfl_debug_glv_split(const uint8_t k[32], uint8_t out[40]) {
   memcpy(out + 20, b.mag, 16);
   memcpy(out + 36, &b.neg, 4);
   return ZKFL_OK;
+}
+
+int zkfl_debug_g1_glv_mul(zkfl_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t* out) {
+  if (!ctx || (n && (!points || !scalars || !out))) return fail(ZKFL_E_ARG, "null argument");
+  if (n == 0) return ZKFL_OK;
+  if (n > (1u << 20)) return fail(ZKFL_E_ARG, "glv mul: n too large");
+  std::vector<GlvScalar> ks(2 * n);
+  for (size_t i = 0; i < n; i++) {
+    uint32_t kk[8];
+    memcpy(kk, scalars + 32 * i, 32);
+    if (!lt_r(kk)) return fail(ZKFL_E_ARG, "glv mul: scalar " + std::to_string(i) + " is not < r");
+    glv_split(kk, ks[2 * i], ks[2 * i + 1]);
+  }
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->st;
+  uint8_t *d_p = nullptr, *d_k = nullptr, *d_o = nullptr;
+  int rc = ZKFL_OK;
+  hipError_t e = hipMalloc(&d_p, n * 64);
+  if (e == hipSuccess) e = hipMalloc(&d_k, ks.size() * sizeof(GlvScalar));
+  if (e == hipSuccess) e = hipMalloc(&d_o, n * 64);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_p, points, n * 64, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_k, ks.data(), ks.size() * sizeof(GlvScalar), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_debug_glv_mul, dim3((uint32_t)n), dim3(128), 0, st, (const uint32_t*)d_p,
+                       (const GlvScalar*)d_k, (uint32_t*)d_o);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_o, n * 64, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) rc = hip_fail(e, "glv mul");
+  for (void* q : {(void*)d_p, (void*)d_k, (void*)d_o})
+    if (q) (void)hipFree(q);
+  return rc;
 }
 
 const char* zkfl_last_error(void) { return g_err.c_str(); }

@@ -58,6 +58,7 @@ SIGNATURES = {
     "zkfl_groth16_prove_batch": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(_P), C.c_char_p, _U8P]),
     "zkfl_debug_prove_parts": (C.c_int, [_P, _P, C.c_char_p, C.c_size_t, _U8P, _U8P]),
     "zkfl_debug_glv_split": (C.c_int, [C.c_char_p, _U8P]),
+    "zkfl_debug_g1_glv_mul": (C.c_int, [_P, C.c_size_t, C.c_char_p, C.c_char_p, _U8P]),
     "zkfl_debug_wtrace": (C.c_int, [_P, C.c_int, C.c_uint32, _P, C.POINTER(C.c_uint32)]),
     "zkfl_msm_g1": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
     "zkfl_msm_g2": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, _U8P]),
@@ -261,6 +262,14 @@ class Context:
         assert len(bases) == 64 * n
         out = _buf(64)
         check(lib().zkfl_msm_g1(self.h, bases, scalars, n, out))
+        return bytes(out)
+
+    def g1_glv_mul(self, points: bytes, scalars: bytes) -> bytes:
+        """The assembly's scalar multiplications (parity hook): k_i P_i, affine std in and out."""
+        n = len(scalars) // 32
+        assert len(points) == 64 * n
+        out = _buf(64 * n)
+        check(lib().zkfl_debug_g1_glv_mul(self.h, n, points, scalars, out))
         return bytes(out)
 
     def msm_g2(self, bases: bytes, scalars: bytes) -> bytes:
