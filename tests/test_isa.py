@@ -61,6 +61,21 @@ def test_accumulation_kernels_do_not_spill(acc):
         assert r["group_segment_fixed_size"] == 8192, (name, r)  # two 4 KB LDS-DMA buffers per wave
 
 
+def test_assembly_row_chains(acc):
+    """The assembly's GLV chains in row form (csrc/row29.h): the kernels that run them hold no
+    scratch, and their products use the DPP row broadcasts and row shifts and the gfx950 row swaps
+    they were written for (a compiler fallback to LDS or scalar paths would show as their absence)."""
+    res = isa_check.resources(SO, r"k_assemble|k_debug_glv_mul")
+    assert len(res) == 4, list(res)  # k_assemble, k_assemble_t, k_assemble_c, k_debug_glv_mul
+    for name, r in res.items():
+        assert r.get("vgpr_spill_count", 0) == 0 and r.get("private_segment_fixed_size", 0) == 0, (name, r)
+    for name, lines in isa_check.disassemble(SO, r"k_assemble_t|k_debug_glv_mul").items():
+        text = "\n".join(lines)
+        for op in ("row_newbcast:0", "row_newbcast:8", "row_shl:1", "row_shr:1", "v_permlane16_swap",
+                   "v_permlane32_swap"):
+            assert op in text, (name, op)
+
+
 def test_accumulation_census(acc):
     """The main loops hold the point formula's products exactly (G1 madd: 6 products x 162 + 2
     squares x 126 + the Y3 sum 243 = 1467 v_mad_u64_u32; G2 per lane 2187), and the G1 formula's
