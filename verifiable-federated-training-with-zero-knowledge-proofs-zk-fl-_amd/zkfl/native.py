@@ -117,7 +117,11 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ZkflError(-5, f"{LIB_PATH} not built (run make in the package dir / __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
+        # an A/B build named by ZKFL_LIB (tools/ab.sh) may predate an entry point: bind what it has
+        ab = bool(os.environ.get("ZKFL_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
